@@ -1,0 +1,250 @@
+#!/usr/bin/env python3
+"""Benchmark of the MaxK-GNN aggregation hot path on MI355X.
+
+One step = forward SpGEMM + backward SSpMM over the whole (synthetic,
+Reddit-shaped by default) graph, inputs resident in HBM.  Prints ONE JSON
+line on rank 0 (contract in the task statement / DESIGN.md "Measurement").
+
+  python bench.py [--gpus N] [--steps K] [--warmup W] [--graph reddit] [--k 32] [--h 256]
+
+N>1: launched by torch.distributed.run, one rank per GPU; the graph is 1-D
+row-partitioned (nnz-balanced) and halo CBSR rows / dXs partial sums move with
+RCCL all-to-all-v (spgemm_new_amd.distributed).  value = algorithmic bytes of
+the WHOLE graph per step / max-over-ranks step time (strong scaling).
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+import torch
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md, chip-level parameters)
+
+
+def parse():
+    p = argparse.ArgumentParser()
+    p.add_argument("--gpus", type=int, default=1)
+    p.add_argument("--steps", type=int, default=20)
+    p.add_argument("--warmup", type=int, default=5)
+    p.add_argument("--graph", default="reddit")
+    p.add_argument("--k", type=int, default=32)
+    p.add_argument("--h", type=int, default=256)
+    p.add_argument("--seed", type=int, default=123)
+    p.add_argument("--bwd-algo", default="auto", choices=["auto", "atomic", "staged"])
+    p.add_argument("--panel-cost", type=int, default=None)
+    p.add_argument("--row-cost", type=int, default=None)
+    p.add_argument("--no-cpu-baseline", action="store_true")
+    p.add_argument("--cpu-seconds", type=float, default=12.0)
+    p.add_argument("--verbose", action="store_true")
+    return p.parse_args()
+
+
+def log(*a):
+    print(*a, file=sys.stderr, flush=True)
+
+
+def cpu_baseline(indptr, indices, values, x_masked, grad, mask, k, h, budget_s):
+    """The reference's CPU aggregation path (utils/models.py:281-287:
+    torch.sparse.mm(adj, x)), forward and backward (A^T G * mask), on a bounded
+    row sample of the same graph, timed on the host cores."""
+    import numpy as np
+    threads = min(16, os.cpu_count() or 1)
+    torch.set_num_threads(threads)
+    ip = indptr.cpu().numpy().astype(np.int64)
+    V = len(ip) - 1
+    E = int(ip[-1])
+
+    def run(rows):
+        e = int(ip[rows])
+        a = torch.sparse_csr_tensor(torch.from_numpy(ip[: rows + 1]),
+                                    indices[:e].cpu().long(), values[:e].cpu(), size=(rows, V))
+        xm = x_masked
+        g = grad[:rows]
+        t0 = time.perf_counter()
+        y = torch.sparse.mm(a, xm)                                   # forward
+        t1 = time.perf_counter()
+        dx = torch.sparse.mm(a.to_sparse_coo().t().coalesce(), g) * mask   # backward
+        t2 = time.perf_counter()
+        del y, dx
+        return e, t1 - t0, t2 - t1
+
+    rows = max(1, min(V, V // 200))
+    e, tf, tb = run(rows)
+    per_edge = (tf + tb) / max(e, 1)
+    target_e = min(E, int(budget_s / 2 / max(per_edge, 1e-12)))
+    rows = int(np.searchsorted(ip, target_e))
+    rows = max(1, min(V, rows))
+    run(rows)  # warm-up
+    res = [run(rows) for _ in range(3)]
+    e = res[0][0]
+    tf = sorted(r[1] for r in res)[1]
+    tb = sorted(r[2] for r in res)[1]
+    nbytes = 2 * (8 * e + 5 * k * e + 4 * h * rows)
+    return {
+        "value": round(nbytes / (tf + tb) / 1e9, 3), "unit": "GB/s", "cores": threads,
+        "kind": "reference",
+        "ms_per_step_sample": round((tf + tb) * 1e3, 2),
+        "sample": (f"rows [0,{rows}) of the same graph ({e} edges, {e / E:.1%} of E): "
+                   "torch.sparse.mm(A,X*mask) + torch.sparse.mm(A^T,G)*mask on CPU fp32, "
+                   "median of 3 after 1 warm-up (reference CPU path utils/models.py:281-287)"),
+        "cpu_model": _cpu_model(),
+    }
+
+
+def _cpu_model():
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return "unknown"
+
+
+def main():
+    args = parse()
+    import spgemm_new_amd as S
+    from spgemm_new_amd import _lib
+    from spgemm_new_amd.graphs import CONFIGS, synthetic_csr_gpu
+    from spgemm_new_amd.models import cbsr_topk
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus and world > 1:
+        log(f"warning: WORLD_SIZE={world} but --gpus {args.gpus}")
+    torch.cuda.set_device(local_rank)
+    dev = torch.device("cuda", local_rank)
+    dist = None
+    if world > 1:
+        import torch.distributed as dist
+        dist.init_process_group("nccl", device_id=dev)
+
+    V, E = CONFIGS[args.graph]
+    h, k = args.h, args.k
+    t0 = time.time()
+    indptr, indices = synthetic_csr_gpu(V, E, seed=args.seed, device=dev,
+                                        self_loops=(args.graph == "flickr"))
+    gen = torch.Generator(device=dev)
+    gen.manual_seed(args.seed + 1)
+    values = torch.rand(E, generator=gen, device=dev)          # main.cu:83-84 U(0,1)
+    X = torch.rand((V, h), generator=gen, device=dev)
+    G = torch.rand((V, h), generator=gen, device=dev)
+    data, sel = cbsr_topk(X, k)
+    log(f"[bench] graph {args.graph} V={V} E={E} built in {time.time() - t0:.1f}s")
+
+    algo = {"auto": _lib.MAXK_BWD_AUTO, "atomic": _lib.MAXK_BWD_ATOMIC,
+            "staged": _lib.MAXK_BWD_STAGED}[args.bwd_algo]
+    kw = {}
+    if args.panel_cost:
+        kw["panel_cost"] = args.panel_cost
+    if args.row_cost:
+        kw["row_cost"] = args.row_cost
+
+    if world > 1:
+        from spgemm_new_amd.distributed import PartitionedMaxK
+        model = PartitionedMaxK(indptr, indices, values, rank, world, dev, **kw)
+        data_l, sel_l = model.local_rows(data), model.local_rows(sel)
+        G_l = model.local_rows(G)
+
+        def step():
+            y = model.forward(data_l, sel_l, h)
+            dx = model.backward(G_l, sel_l)
+            return y, dx
+        fwd_call = bwd_call = None
+    else:
+        g = S.MaxKGraph(indptr, indices, values, **kw)
+        y = torch.empty((V, h), device=dev)
+        dx = torch.empty((V, k), device=dev)
+        g.backward(G, sel, out=dx, algo=algo)  # builds CSC/workspaces once
+
+        def fwd_call():
+            g.forward(data, sel, h, out=y)
+
+        def bwd_call():
+            g.backward(G, sel, out=dx, algo=algo)
+
+        def step():
+            fwd_call()
+            bwd_call()
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize()
+    if dist:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t_start = time.perf_counter()
+    for _ in range(args.steps):
+        step()
+    torch.cuda.synchronize()
+    if dist:
+        dist.barrier()
+    t_el = time.perf_counter() - t_start
+    if dist:
+        tt = torch.tensor([t_el], device=dev, dtype=torch.float64)
+        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+        t_el = float(tt)
+    ms = t_el / args.steps * 1e3
+    nbytes_iter = 2 * (8 * E + 5 * k * E + 4 * h * V)
+    value = nbytes_iter / (ms / 1e3) / 1e9
+
+    result = {
+        "metric": "effective HBM GB/s + ms/iter, SpGEMM fwd+SSpMM bwd, Reddit h=256 k=32",
+        "value": round(value, 2), "unit": "GB/s", "n_gpus": world, "steps": args.steps,
+        "warmup": args.warmup, "ms_per_step": round(ms, 4), "higher_is_better": True,
+        "scaling": "strong", "vs_baseline": None, "dtype": "fp32",
+        "data": "synthetic (power-law degrees, uniform columns, seed 123; values/X/G U(0,1))",
+        "config": {"workload": f"{args.graph} fwd SpGEMM + bwd SSpMM", "graph": args.graph,
+                   "num_nodes": V, "num_edges": E, "hidden": h, "k": k,
+                   "parallelism": f"rowpart{world}" if world > 1 else "single",
+                   "bwd_algo": args.bwd_algo},
+    }
+
+    if world == 1:
+        # per-call timing with HIP events on the launch stream (the current stream)
+        st = torch.cuda.current_stream()
+        fw, bw = [], []
+        for _ in range(args.steps):
+            e0, e1, e2 = (torch.cuda.Event(enable_timing=True) for _ in range(3))
+            e0.record(st)
+            fwd_call()
+            e1.record(st)
+            bwd_call()
+            e2.record(st)
+            e2.synchronize()
+            fw.append(e0.elapsed_time(e1))
+            bw.append(e1.elapsed_time(e2))
+        fms, bms = sum(fw) / len(fw), sum(bw) / len(bw)
+        b_call = 8 * E + 5 * k * E + 4 * h * V
+        dom = ("sspmm_backward", bms) if bms >= fms else ("spgemm_forward", fms)
+        ach = b_call / (dom[1] / 1e3) / 1e9
+        result["roofline"] = {"bound": "hbm", "achieved": round(ach, 1), "peak": HBM_PEAK_GBS,
+                              "unit": "GB/s", "frac": round(ach / HBM_PEAK_GBS, 4),
+                              "traffic": None, "kernel": dom[0],
+                              "algorithmic_bytes_per_launch": b_call}
+        result["fwd_ms"] = round(fms, 4)
+        result["bwd_ms"] = round(bms, 4)
+        result["fwd_GBs"] = round(b_call / fms / 1e6, 1)
+        result["bwd_GBs"] = round(b_call / bms / 1e6, 1)
+        if not args.no_cpu_baseline and rank == 0:
+            mask = torch.zeros((V, h), device=dev)
+            mask.scatter_(1, sel.long(), 1.0)
+            xm = (X * mask).cpu()
+            result["cpu_baseline"] = cpu_baseline(indptr, indices, values, xm, G.cpu(),
+                                                  mask.cpu(), k, h, args.cpu_seconds)
+    if rank == 0:
+        print(json.dumps(result), flush=True)
+    if dist:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,125 @@
+/*
+ * maxk_spgemm.h -- C ABI of the MI355X (gfx950) MaxK-GNN aggregation hot path.
+ *
+ * This is the drop-in boundary.  It replaces the reference's launch layer,
+ *   cuda_kernel_wrappers.cu:36-93   extern "C" spmm_kernel_opt2_sparse_v3_wrapper /
+ *                                    spmm_kernel_opt2_sparse_backward_v3_wrapper
+ *   cuda_kernel_bindings.cpp:42-161 spmm_maxk_forward / spmm_maxk_backward
+ *   kernels/spmm_maxk.cu:108-131, kernels/spmm_maxk_backward.cu:117-139 (SPMM_*::run/do_test)
+ *   kernels/generate_meta.py:26-48  (warp4 schedule, now built on the device)
+ * and is what a reference-side binding (ctypes / pybind11 / cgo) would bind;
+ * see INTEGRATION.md.
+ *
+ * Conventions
+ *  - All pointers are device pointers (hipMalloc / torch CUDA tensors) unless
+ *    stated otherwise; sizes are element counts.
+ *  - `stream` is a hipStream_t passed as void* (NULL = legacy default stream).
+ *    Every call is asynchronous on that stream and performs no allocation and
+ *    no host synchronisation, so calls can be captured into a hipGraph.
+ *  - Return value: 0 on success; a negative MAXK_E* code for an invalid
+ *    argument (nothing launched); a positive hipError_t for a launch failure.
+ *  - Layouts (row-major, contiguous):
+ *      CSR    indptr int32[V+1] (indptr[0] may be non-zero), indices int32[E],
+ *             values fp32[E]
+ *      CBSR   cbsr_data fp32[V,k], cbsr_sel uint8[V,k]  (k distinct columns
+ *             < dim_origin per row; the selector is a uint8, so
+ *             dim_origin <= 256, as in the reference, spmm_maxk.cu:17)
+ *      dense  out / grad fp32[V,dim_origin];  dxs fp32[V,k]
+ */
+#ifndef MAXK_SPGEMM_H
+#define MAXK_SPGEMM_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define MAXK_OK 0
+#define MAXK_E_ARG (-1)        /* bad size / null pointer                  */
+#define MAXK_E_DIM (-2)        /* dim_origin > 256 or dim_k outside [1,dim] */
+#define MAXK_E_WORKSPACE (-3)  /* workspace too small                       */
+
+/* Default merge-path cost model: one edge costs 1, one output row costs
+ * MAXK_DEFAULT_ROW_COST; a panel (one wavefront's work item) costs
+ * MAXK_DEFAULT_PANEL_COST. */
+#define MAXK_DEFAULT_PANEL_COST 2048
+#define MAXK_DEFAULT_ROW_COST 16
+
+/* Library build identification (string, host memory, static). */
+const char *maxk_version(void);
+
+/* ---------------------------------------------------------------------------
+ * Schedule.  Replaces the offline .warp4 file (generate_meta.py:26-48,
+ * loaded by cuda_kernel_bindings.cpp:287-317 / spmm_maxk.cu:117).
+ * A schedule is int32[2*(P+1)]: for p = 0..P the merge-path coordinate
+ * (row, edge) at cost p*panel_cost over the sequence "edges of row 0, end of
+ * row 0, edges of row 1, ...".  Panel p = [coord p, coord p+1) is one
+ * wavefront's work; it is balanced in edges + rows by construction.
+ * ------------------------------------------------------------------------- */
+int maxk_schedule_num_panels(int64_t num_rows, int64_t num_edges, int panel_cost,
+                             int row_cost, int64_t *num_panels /* host out */);
+int maxk_schedule_build(const int32_t *indptr, int num_rows, int panel_cost, int row_cost,
+                        int32_t *sched, int64_t num_panels, void *stream);
+
+/* warp4 schedule on the device (generate_meta.py:26-48 semantics, any
+ * warp_max_nz).  chunk_offsets: int32[V+1] scratch.  Count first (returns the
+ * chunk count in *num_warps, host memory; this call synchronises the stream),
+ * then fill warp4 int32[4*W]. */
+int maxk_warp4_build(const int32_t *indptr, int num_rows, int warp_max_nz,
+                     int32_t *chunk_offsets, int32_t *warp4, int64_t warp4_capacity,
+                     int64_t *num_warps, void *stream);
+
+/* ---------------------------------------------------------------------------
+ * Forward SpGEMM  Y = A . scatter(CBSR)      (spmm_maxk.cu:17-106, K1)
+ * Writes every row of out (rows of degree 0 become 0); out need not be
+ * zeroed.  Workspace: maxk_forward_workspace_bytes(P, dim_origin) bytes.
+ * ------------------------------------------------------------------------- */
+size_t maxk_forward_workspace_bytes(int64_t num_panels, int dim_origin);
+int maxk_spgemm_forward(const int32_t *sched, int64_t num_panels, const int32_t *indptr,
+                        const int32_t *indices, const float *values,
+                        const float *cbsr_data, const uint8_t *cbsr_sel, int num_rows,
+                        int dim_origin, int dim_k, float *out, void *workspace,
+                        size_t workspace_bytes, void *stream);
+
+/* ---------------------------------------------------------------------------
+ * Backward SSpMM  dXs[c,l] = sum_{e: idx[e]=c} val[e] * G[row(e), sel[c,l]]
+ * (spmm_maxk_backward.cu:15-115, K2).  Writes every element of dxs (no
+ * pre-zeroing needed).  Workspace: maxk_backward_workspace_bytes(...).
+ * algo: MAXK_BWD_AUTO picks the fastest measured algorithm for the shape.
+ * ------------------------------------------------------------------------- */
+#define MAXK_BWD_AUTO 0
+#define MAXK_BWD_ATOMIC 1      /* push + global float atomics (reference's scheme) */
+#define MAXK_BWD_STAGED 2      /* push to per-edge staging rows + CSC segmented sum */
+size_t maxk_backward_workspace_bytes(int algo, int64_t num_edges, int dim_k,
+                                     int64_t csc_num_panels);
+int maxk_sspmm_backward(int algo, const int32_t *sched, int64_t num_panels,
+                        const int32_t *indptr, const int32_t *indices, const float *values,
+                        const float *grad, const uint8_t *cbsr_sel, int num_rows,
+                        int64_t num_edges, int dim_origin, int dim_k, float *dxs,
+                        const int32_t *csc_pos, const int32_t *csc_sched,
+                        int64_t csc_num_panels, const int32_t *csc_indptr,
+                        void *workspace, size_t workspace_bytes, void *stream);
+
+/* ---------------------------------------------------------------------------
+ * Exact drop-ins for the reference's extern "C" launchers
+ * (cuda_kernel_wrappers.cu:38-56 and :58-76), minus the CUDA launch geometry
+ * (grid/block/shared_size), which the implementation chooses.  They consume
+ * the reference's warp4 chunks and, like the reference, ACCUMULATE into the
+ * caller's (normally zeroed, cuda_kernel_bindings.cpp:71,128) output.
+ * Defects of the reference are not reproduced (SURVEY.md §2.4-1,-7).
+ * ------------------------------------------------------------------------- */
+int maxk_spmm_forward_warp4(const int32_t *warp4, const int32_t *idx, const float *val,
+                            const float *vin_data, const uint8_t *vin_selector, float *vout,
+                            int num_v, int num_e, int feat_in, int dim_sparse,
+                            int num_warps, void *stream);
+int maxk_spmm_backward_warp4(const int32_t *warp4, const int32_t *idx, const float *val,
+                             const float *vin_data, const uint8_t *vin_selector, float *vout,
+                             int num_v, int num_e, int feat_in, int dim_sparse,
+                             int num_warps, void *stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* MAXK_SPGEMM_H */

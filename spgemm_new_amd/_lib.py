@@ -1,0 +1,89 @@
+"""ctypes binding of the C ABI declared in include/maxk_spgemm.h.
+
+This is the thin shim that replaces the reference's pybind11/torch extension
+(cuda_kernel_bindings.cpp:429-490).  The shared library is built in-tree by
+``__graft_entry__.build()`` (hipcc --offload-arch=gfx950) into
+``spgemm_new_amd/lib/libmaxk_spgemm.so``.  There is no fallback: if the library
+is missing every entry point raises.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+
+import torch  # noqa: F401  -- must be imported first so its HIP runtime is the one we bind to
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "lib", "libmaxk_spgemm.so")
+SOURCES = [os.path.join(_HERE, "csrc", "maxk_spgemm.hip")]
+HEADER = os.path.join(os.path.dirname(_HERE), "include", "maxk_spgemm.h")
+
+MAXK_OK = 0
+MAXK_E_ARG = -1
+MAXK_E_DIM = -2
+MAXK_E_WORKSPACE = -3
+MAXK_BWD_AUTO = 0
+MAXK_BWD_ATOMIC = 1
+MAXK_BWD_STAGED = 2
+DEFAULT_PANEL_COST = 2048
+DEFAULT_ROW_COST = 16
+
+_ERRORS = {MAXK_E_ARG: "invalid argument", MAXK_E_DIM: "invalid dimension (dim_origin must be "
+           "<= 256 and 1 <= dim_k <= dim_origin)", MAXK_E_WORKSPACE: "workspace too small"}
+
+# name -> (restype, argtypes); every symbol here is declared in include/maxk_spgemm.h
+_P = ctypes.c_void_p
+_I = ctypes.c_int
+_L = ctypes.c_int64
+_S = ctypes.c_size_t
+SIGNATURES = {
+    "maxk_version": (ctypes.c_char_p, []),
+    "maxk_schedule_num_panels": (_I, [_L, _L, _I, _I, ctypes.POINTER(ctypes.c_int64)]),
+    "maxk_schedule_build": (_I, [_P, _I, _I, _I, _P, _L, _P]),
+    "maxk_warp4_build": (_I, [_P, _I, _I, _P, _P, _L, ctypes.POINTER(ctypes.c_int64), _P]),
+    "maxk_forward_workspace_bytes": (_S, [_L, _I]),
+    "maxk_spgemm_forward": (_I, [_P, _L, _P, _P, _P, _P, _P, _I, _I, _I, _P, _P, _S, _P]),
+    "maxk_backward_workspace_bytes": (_S, [_I, _L, _I, _L]),
+    "maxk_sspmm_backward": (_I, [_I, _P, _L, _P, _P, _P, _P, _P, _I, _L, _I, _I, _P, _P, _P, _L,
+                                 _P, _P, _S, _P]),
+    "maxk_spmm_forward_warp4": (_I, [_P, _P, _P, _P, _P, _P, _I, _I, _I, _I, _I, _P]),
+    "maxk_spmm_backward_warp4": (_I, [_P, _P, _P, _P, _P, _P, _I, _I, _I, _I, _I, _P]),
+}
+
+_lib = None
+
+
+class MaxKError(RuntimeError):
+    pass
+
+
+def load():
+    """Load the HIP library (raises if it has not been built)."""
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            raise MaxKError(
+                f"MI355X HIP library not found at {LIB_PATH}; build it with "
+                "`python -c 'import __graft_entry__ as g; g.build()'` (no CPU fallback exists)")
+        L = ctypes.CDLL(LIB_PATH)
+        for name, (res, args) in SIGNATURES.items():
+            f = getattr(L, name)
+            f.restype = res
+            f.argtypes = args
+        _lib = L
+    return _lib
+
+
+def check(rc: int, what: str) -> None:
+    if rc != MAXK_OK:
+        if rc < 0:
+            raise MaxKError(f"{what}: {_ERRORS.get(rc, 'error')} ({rc})")
+        raise MaxKError(f"{what}: HIP error {rc}")
+
+
+def stream_ptr(device=None) -> int:
+    return torch.cuda.current_stream(device).cuda_stream
+
+
+def ptr(t) -> int | None:
+    return None if t is None else t.data_ptr()

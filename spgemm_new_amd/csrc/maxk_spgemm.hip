@@ -1,0 +1,965 @@
+// maxk_spgemm.hip -- MI355X (gfx950) kernels for MaxK-GNN aggregation.
+//
+// Forward  SpGEMM  Y[r,:]   = sum_e val[e] * scatter_h(data[c], sel[c])   (K1, spmm_maxk.cu:17-106)
+// Backward SSpMM   dXs[c,l] = sum_{e:idx[e]=c} val[e] * G[row(e), sel[c,l]] (K2, spmm_maxk_backward.cu:15-115)
+//
+// Design (DESIGN.md has the full rationale and the rooflines):
+//  * Work decomposition: merge-path panels over "edges of row r, end of row r"
+//    (one wavefront = one panel, equal edge+row cost), built on the device
+//    from indptr.  Rows are never assumed short; a row split across panels is
+//    finished by a carry fixup, so no output is pre-zeroed and no global
+//    atomic touches a row that one wave owns.
+//  * Forward: per wave a fp32 row accumulator in LDS (dim_origin floats).
+//    Each lane gathers 16 B of a neighbour's CBSR values (dwordx4) and the
+//    matching 4 selector bytes (dword), then ds_add_f32's the 4 products into
+//    the accumulator at the selected columns.  A finished row leaves with one
+//    coalesced 16 B/lane store.
+//  * Backward, two algorithms behind one entry point:
+//      ATOMIC  push: G[r,:] staged in LDS once per (row, panel); per edge the
+//              k sampled gradients are gathered from LDS and added into
+//              dXs[c,:] with no-return global float atomics, 256 contiguous
+//              bytes per wave-instruction.
+//      STAGED  push to staging rows: the same gather writes each edge's
+//              k-vector to P[csc_pos[e]] (full 16 B/lane rows, non-temporal),
+//              then a merge-path segmented sum over the CSC ranges writes
+//              dXs with plain stores (no atomics at all).
+//  * wave64 everywhere; no CUDA-isms, no warp32 tiling.
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "../../include/maxk_spgemm.h"
+
+#define MAXK_VERSION_STRING "maxk-mi355x 0.1 (gfx950, wave64)"
+
+namespace {
+
+constexpr int kWave = 64;
+constexpr int kWavesPerBlock = 4;
+constexpr int kBlock = kWave * kWavesPerBlock;
+constexpr int kMaxDim = 256;
+
+typedef float f4 __attribute__((ext_vector_type(4)));
+
+__device__ __forceinline__ int lane_id() { return threadIdx.x & (kWave - 1); }
+
+__device__ __forceinline__ void wave_sync_lds()
+{
+    // LDS operations of one wave complete in issue order; this keeps the
+    // compiler from moving LDS accesses across the point and makes every
+    // lane's ds_add visible to the following ds_read of another lane.
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+__device__ __forceinline__ void lds_add(float *p, float v)
+{
+    __hip_atomic_fetch_add(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
+}
+
+__device__ __forceinline__ void gbl_add(float *p, float v)
+{
+    // no-return global_atomic_add_f32 (agent scope: adders may sit on any XCD)
+    __hip_atomic_fetch_add(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// ---------------------------------------------------------------------------
+// Merge-path schedule
+// ---------------------------------------------------------------------------
+// Cost of the point where row i starts: f(i) = (indptr[i]-indptr[0]) + i*row_cost.
+// For cost d, row i(d) = max{i : f(i) <= d}; edge j(d) = min(indptr[i] + d - f(i), indptr[i+1]).
+__global__ void schedule_kernel(const int32_t *__restrict__ indptr, int num_rows, int panel_cost,
+                                int row_cost, int2 *__restrict__ sched, int64_t num_panels)
+{
+    const int64_t p = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (p > num_panels) return;
+    const int32_t base = indptr[0];
+    const int64_t total = (int64_t)(indptr[num_rows] - base) + (int64_t)num_rows * row_cost;
+    int64_t d = p * (int64_t)panel_cost;
+    if (d > total || p == num_panels) d = total;
+    int lo = 0, hi = num_rows;  // invariant: f(lo) <= d; answer in [lo, hi]
+    while (lo < hi) {
+        const int mid = (int)(((int64_t)lo + hi + 1) >> 1);
+        const int64_t f = (int64_t)(indptr[mid] - base) + (int64_t)mid * row_cost;
+        if (f <= d) lo = mid; else hi = mid - 1;
+    }
+    int j;
+    if (lo >= num_rows) {
+        j = indptr[num_rows];
+    } else {
+        const int64_t f = (int64_t)(indptr[lo] - base) + (int64_t)lo * row_cost;
+        const int64_t jj = (int64_t)indptr[lo] + (d - f);
+        j = (int)(jj < (int64_t)indptr[lo + 1] ? jj : (int64_t)indptr[lo + 1]);
+    }
+    sched[p] = make_int2(lo, j);
+}
+
+// warp4 (generate_meta.py:26-48) on the device: per-row chunk counts, then fill.
+__global__ void warp4_count_kernel(const int32_t *__restrict__ indptr, int num_rows, int nz,
+                                   int32_t *__restrict__ counts)
+{
+    const int r = blockIdx.x * blockDim.x + threadIdx.x;
+    if (r >= num_rows) return;
+    const int deg = indptr[r + 1] - indptr[r];
+    counts[r] = (deg + nz - 1) / nz;
+}
+
+__global__ void warp4_fill_kernel(const int32_t *__restrict__ indptr, int num_rows, int nz,
+                                  const int32_t *__restrict__ offsets, int4 *__restrict__ warp4)
+{
+    const int r = blockIdx.x * blockDim.x + threadIdx.x;
+    if (r >= num_rows) return;
+    const int b = indptr[r], deg = indptr[r + 1] - b;
+    int w = offsets[r];
+    for (int t = 0; t < deg; t += nz, ++w)
+        warp4[w] = make_int4(r, b + t, deg - t < nz ? deg - t : nz, 0);
+}
+
+// Exclusive scan of c[0:n) in place by one workgroup (once-per-graph builder),
+// total written to *total.
+__global__ __launch_bounds__(256) void exclusive_scan_1block(int32_t *c, int n, int32_t *total)
+{
+    __shared__ int32_t part[256];
+    __shared__ int32_t carry_in;
+    if (threadIdx.x == 0) carry_in = 0;
+    __syncthreads();
+    for (int base = 0; base < n; base += 256 * 16) {
+        int loc[16];
+        int s = 0;
+        for (int t = 0; t < 16; ++t) {
+            const int i = base + threadIdx.x * 16 + t;
+            loc[t] = i < n ? c[i] : 0;
+            s += loc[t];
+        }
+        part[threadIdx.x] = s;
+        __syncthreads();
+        for (int off = 1; off < 256; off <<= 1) {
+            const int v = threadIdx.x >= off ? part[threadIdx.x - off] : 0;
+            __syncthreads();
+            part[threadIdx.x] += v;
+            __syncthreads();
+        }
+        int run = carry_in + part[threadIdx.x] - s;
+        for (int t = 0; t < 16; ++t) {
+            const int i = base + threadIdx.x * 16 + t;
+            if (i < n) c[i] = run;
+            run += loc[t];
+        }
+        __syncthreads();
+        if (threadIdx.x == 255) carry_in += part[255];
+        __syncthreads();
+    }
+    if (threadIdx.x == 0) *total = carry_in;
+}
+
+// ---------------------------------------------------------------------------
+// Forward: gather-scatter of one edge range into the wave's LDS row.
+// K % 4 == 0: each lane owns 4 consecutive CBSR entries of one edge.
+// ---------------------------------------------------------------------------
+template <int K>
+__device__ __forceinline__ void fwd_edges_vec(int e0, int e1, const int32_t *__restrict__ idx,
+                                              const float *__restrict__ val,
+                                              const float *__restrict__ data,
+                                              const uint8_t *__restrict__ sel, float *acc)
+{
+    constexpr int LPE = K / 4;          // lanes per edge
+    constexpr int EPS = kWave / LPE;    // edges per step
+    constexpr int STEPS = kWave / EPS;  // steps per 64-edge batch (== LPE)
+    constexpr int U = STEPS < 8 ? STEPS : 8;
+    const int lane = lane_id();
+    const int sub = lane % LPE;
+    const int slot = lane / LPE;
+    for (int base = e0; base < e1; base += kWave) {
+        const int n = (e1 - base) < kWave ? (e1 - base) : kWave;
+        int my_c = 0;
+        float my_v = 0.f;
+        if (lane < n) {
+            my_c = __builtin_nontemporal_load(idx + base + lane);
+            my_v = __builtin_nontemporal_load(val + base + lane);
+        }
+#pragma unroll
+        for (int s0 = 0; s0 < STEPS; s0 += U) {
+            if (s0 * EPS >= n) break;
+            f4 d[U];
+            uint32_t sb[U];
+            float v[U];
+#pragma unroll
+            for (int u = 0; u < U; ++u) {
+                const int t = (s0 + u) * EPS + slot;
+                const int c = __shfl(my_c, t < kWave ? t : 0);
+                v[u] = __shfl(my_v, t < kWave ? t : 0);
+                if (t < n) {
+                    const size_t off = (size_t)c * K + sub * 4;
+                    d[u] = *reinterpret_cast<const f4 *>(data + off);
+                    sb[u] = *reinterpret_cast<const uint32_t *>(sel + off);
+                } else {
+                    v[u] = 0.f;
+                    d[u] = f4{0.f, 0.f, 0.f, 0.f};
+                    sb[u] = 0;
+                }
+            }
+#pragma unroll
+            for (int u = 0; u < U; ++u) {
+                const int t = (s0 + u) * EPS + slot;
+                if (t < n) {
+                    lds_add(acc + (sb[u] & 0xff), v[u] * d[u].x);
+                    lds_add(acc + ((sb[u] >> 8) & 0xff), v[u] * d[u].y);
+                    lds_add(acc + ((sb[u] >> 16) & 0xff), v[u] * d[u].z);
+                    lds_add(acc + (sb[u] >> 24), v[u] * d[u].w);
+                }
+            }
+        }
+    }
+}
+
+// Any k: one CBSR entry per lane.
+__device__ __forceinline__ void fwd_edges_scalar(int e0, int e1, int k,
+                                                 const int32_t *__restrict__ idx,
+                                                 const float *__restrict__ val,
+                                                 const float *__restrict__ data,
+                                                 const uint8_t *__restrict__ sel, float *acc)
+{
+    const int lane = lane_id();
+    if (k <= kWave) {
+        const int eps = kWave / k;
+        const int slot = lane / k, l = lane % k;
+        for (int e = e0; e < e1; e += eps) {
+            const int my = e + slot;
+            if (slot < eps && my < e1) {
+                const int c = idx[my];
+                const float v = val[my];
+                const size_t off = (size_t)c * k + l;
+                lds_add(acc + sel[off], v * data[off]);
+            }
+        }
+    } else {
+        for (int e = e0; e < e1; ++e) {
+            const int c = idx[e];
+            const float v = val[e];
+            for (int l = lane; l < k; l += kWave) {
+                const size_t off = (size_t)c * k + l;
+                lds_add(acc + sel[off], v * data[off]);
+            }
+        }
+    }
+}
+
+template <int K>
+__device__ __forceinline__ void fwd_edges(int e0, int e1, int k, const int32_t *__restrict__ idx,
+                                          const float *__restrict__ val,
+                                          const float *__restrict__ data,
+                                          const uint8_t *__restrict__ sel, float *acc)
+{
+    if constexpr (K > 0)
+        fwd_edges_vec<K>(e0, e1, idx, val, data, sel, acc);
+    else
+        fwd_edges_scalar(e0, e1, k, idx, val, data, sel, acc);
+}
+
+// acc (dim floats, dim % 4 == 0 padded) -> dst row, then zero acc.
+__device__ __forceinline__ void flush_store(float *acc, float *__restrict__ dst, int dim)
+{
+    const int lane = lane_id();
+    wave_sync_lds();
+    if ((dim & 3) == 0) {
+        for (int c4 = lane; c4 < (dim >> 2); c4 += kWave) {
+            f4 a = reinterpret_cast<f4 *>(acc)[c4];
+            reinterpret_cast<f4 *>(dst)[c4] = a;
+            reinterpret_cast<f4 *>(acc)[c4] = f4{0.f, 0.f, 0.f, 0.f};
+        }
+    } else {
+        for (int c = lane; c < dim; c += kWave) {
+            dst[c] = acc[c];
+            acc[c] = 0.f;
+        }
+    }
+    wave_sync_lds();
+}
+
+__device__ __forceinline__ void flush_atomic(float *acc, float *__restrict__ dst, int dim)
+{
+    const int lane = lane_id();
+    wave_sync_lds();
+    for (int c = lane; c < dim; c += kWave) {  // 256 contiguous bytes per instruction
+        gbl_add(dst + c, acc[c]);
+        acc[c] = 0.f;
+    }
+    wave_sync_lds();
+}
+
+__device__ __forceinline__ void flush_rmw(float *acc, float *__restrict__ dst, int dim)
+{
+    const int lane = lane_id();
+    wave_sync_lds();
+    for (int c = lane; c < dim; c += kWave) {
+        dst[c] += acc[c];
+        acc[c] = 0.f;
+    }
+    wave_sync_lds();
+}
+
+__device__ __forceinline__ void zero_lds(float *acc, int n)
+{
+    for (int c = lane_id(); c < n; c += kWave) acc[c] = 0.f;
+    wave_sync_lds();
+}
+
+// Panel-scheduled forward.  Rows [i0, i1) are finished and owned by this
+// wave (plain store); row i1 is in progress at the panel end -> carry.
+template <int K>
+__global__ __launch_bounds__(kBlock) void fwd_panel_kernel(
+    const int2 *__restrict__ sched, int64_t num_panels, const int32_t *__restrict__ indptr,
+    const int32_t *__restrict__ idx, const float *__restrict__ val,
+    const float *__restrict__ data, const uint8_t *__restrict__ sel, int num_rows, int dim,
+    int k, float *__restrict__ out, float *__restrict__ carry, int32_t *__restrict__ carry_row)
+{
+    extern __shared__ __attribute__((aligned(16))) float lds[];
+    const int dimp = (dim + 3) & ~3;
+    float *acc = lds + (threadIdx.x / kWave) * kMaxDim;  // selectors are uint8: never out of bounds
+    const int64_t w = (int64_t)blockIdx.x * kWavesPerBlock + threadIdx.x / kWave;
+    if (w >= num_panels) return;
+    zero_lds(acc, kMaxDim);
+    const int2 a = sched[w], b = sched[w + 1];
+    const int i0 = a.x, j0 = a.y, i1 = b.x, j1 = b.y;
+    int e = j0;
+    for (int r = i0; r < i1; ++r) {
+        const int re = indptr[r + 1];
+        if (e < re) fwd_edges<K>(e, re, k, idx, val, data, sel, acc);
+        flush_store(acc, out + (size_t)r * dim, dim);
+        e = re;
+    }
+    int has_carry = 0;
+    if (i1 < num_rows) {
+        const int eb = e > indptr[i1] ? e : indptr[i1];
+        if (eb < j1) {
+            fwd_edges<K>(eb, j1, k, idx, val, data, sel, acc);
+            has_carry = 1;
+        }
+    }
+    if (has_carry) {
+        flush_store(acc, carry + (size_t)w * dimp, dimp);
+        if (lane_id() == 0) carry_row[w] = i1;
+    } else if (lane_id() == 0) {
+        carry_row[w] = -1;
+    }
+}
+
+// Adds each panel's carry row into the output (after the owner stored it).
+__global__ __launch_bounds__(kBlock) void carry_fixup_kernel(
+    int64_t num_panels, const float *__restrict__ carry, const int32_t *__restrict__ carry_row,
+    float *__restrict__ out, int dim, int carry_stride)
+{
+    const int64_t w = (int64_t)blockIdx.x * kWavesPerBlock + threadIdx.x / kWave;
+    if (w >= num_panels) return;
+    const int r = carry_row[w];
+    if (r < 0) return;
+    const float *src = carry + (size_t)w * carry_stride;
+    float *dst = out + (size_t)r * dim;
+    for (int c = lane_id(); c < dim; c += kWave) gbl_add(dst + c, src[c]);
+}
+
+// warp4-driven forward (drop-in for the reference launcher).  A wave takes a
+// run of `run` consecutive chunks; rows entirely inside the run are added
+// with plain read-modify-write, rows crossing a run edge with global atomics.
+template <int K>
+__global__ __launch_bounds__(kBlock) void fwd_warp4_kernel(
+    const int4 *__restrict__ warp4, int num_warps, int run, const int32_t *__restrict__ idx,
+    const float *__restrict__ val, const float *__restrict__ data,
+    const uint8_t *__restrict__ sel, int dim, int k, float *__restrict__ out)
+{
+    extern __shared__ __attribute__((aligned(16))) float lds[];
+    float *acc = lds + (threadIdx.x / kWave) * kMaxDim;  // selectors are uint8: never out of bounds
+    const int64_t w = (int64_t)blockIdx.x * kWavesPerBlock + threadIdx.x / kWave;
+    const int64_t q0 = w * run;
+    if (q0 >= num_warps) return;
+    const int q1 = (int)((q0 + run) < num_warps ? (q0 + run) : num_warps);
+    zero_lds(acc, kMaxDim);
+    const int head_row = q0 > 0 ? warp4[q0 - 1].x : -1;
+    const int tail_row = q1 < num_warps ? warp4[q1].x : -1;
+    int cur = -1;
+    for (int q = (int)q0; q < q1; ++q) {
+        const int4 ch = warp4[q];
+        if (ch.x != cur) {
+            if (cur >= 0) {
+                float *dst = out + (size_t)cur * dim;
+                if (cur == head_row) flush_atomic(acc, dst, dim);
+                else flush_rmw(acc, dst, dim);
+            }
+            cur = ch.x;
+        }
+        fwd_edges<K>(ch.y, ch.y + ch.z, k, idx, val, data, sel, acc);
+    }
+    if (cur >= 0) {
+        float *dst = out + (size_t)cur * dim;
+        if (cur == head_row || cur == tail_row) flush_atomic(acc, dst, dim);
+        else flush_rmw(acc, dst, dim);
+    }
+}
+
+// ---------------------------------------------------------------------------
+// Backward
+// ---------------------------------------------------------------------------
+// Stage G[r, 0:dim] into the wave's LDS row.
+__device__ __forceinline__ void stage_row(float *gs, const float *__restrict__ g, int dim)
+{
+    wave_sync_lds();
+    const int lane = lane_id();
+    if ((dim & 3) == 0) {
+        for (int c4 = lane; c4 < (dim >> 2); c4 += kWave)
+            reinterpret_cast<f4 *>(gs)[c4] = reinterpret_cast<const f4 *>(g)[c4];
+    } else {
+        for (int c = lane; c < dim; c += kWave) gs[c] = g[c];
+    }
+    wave_sync_lds();
+}
+
+// ATOMIC push over one edge range of row r (G[r] already staged in gs).
+__device__ __forceinline__ void bwd_edges_atomic(int e0, int e1, int k,
+                                                 const int32_t *__restrict__ idx,
+                                                 const float *__restrict__ val,
+                                                 const uint8_t *__restrict__ sel,
+                                                 const float *gs, float *__restrict__ dxs)
+{
+    const int lane = lane_id();
+    if (k <= kWave) {
+        const int eps = kWave / k;
+        const int slot = lane / k, l = lane % k;
+        for (int base = e0; base < e1; base += kWave) {
+            const int n = (e1 - base) < kWave ? (e1 - base) : kWave;
+            int my_c = 0;
+            float my_v = 0.f;
+            if (lane < n) {
+                my_c = __builtin_nontemporal_load(idx + base + lane);
+                my_v = __builtin_nontemporal_load(val + base + lane);
+            }
+            for (int s = 0; s < n; s += eps) {
+                const int t = s + slot;
+                const int c = __shfl(my_c, t < kWave ? t : 0);
+                const float v = __shfl(my_v, t < kWave ? t : 0);
+                if (slot < eps && t < n) {
+                    const size_t off = (size_t)c * k + l;
+                    gbl_add(dxs + off, v * gs[sel[off]]);
+                }
+            }
+        }
+    } else {
+        for (int e = e0; e < e1; ++e) {
+            const int c = idx[e];
+            const float v = val[e];
+            for (int l = lane; l < k; l += kWave) {
+                const size_t off = (size_t)c * k + l;
+                gbl_add(dxs + off, v * gs[sel[off]]);
+            }
+        }
+    }
+}
+
+// STAGED push: P[csc_pos[e], 0:K] = val[e] * G[r, sel[c, 0:K]].
+template <int K>
+__device__ __forceinline__ void bwd_edges_stage_vec(int e0, int e1,
+                                                    const int32_t *__restrict__ idx,
+                                                    const float *__restrict__ val,
+                                                    const int32_t *__restrict__ csc_pos,
+                                                    const uint8_t *__restrict__ sel,
+                                                    const float *gs, float *__restrict__ P)
+{
+    constexpr int LPE = K / 4;
+    constexpr int EPS = kWave / LPE;
+    constexpr int STEPS = kWave / EPS;
+    constexpr int U = STEPS < 8 ? STEPS : 8;
+    const int lane = lane_id();
+    const int sub = lane % LPE;
+    const int slot = lane / LPE;
+    for (int base = e0; base < e1; base += kWave) {
+        const int n = (e1 - base) < kWave ? (e1 - base) : kWave;
+        int my_c = 0, my_p = 0;
+        float my_v = 0.f;
+        if (lane < n) {
+            my_c = __builtin_nontemporal_load(idx + base + lane);
+            my_v = __builtin_nontemporal_load(val + base + lane);
+            my_p = __builtin_nontemporal_load(csc_pos + base + lane);
+        }
+#pragma unroll
+        for (int s0 = 0; s0 < STEPS; s0 += U) {
+            if (s0 * EPS >= n) break;
+            uint32_t sb[U];
+#pragma unroll
+            for (int u = 0; u < U; ++u) {
+                const int t = (s0 + u) * EPS + slot;
+                const int c = __shfl(my_c, t < kWave ? t : 0);
+                sb[u] = t < n ? *reinterpret_cast<const uint32_t *>(sel + (size_t)c * K + sub * 4) : 0u;
+            }
+#pragma unroll
+            for (int u = 0; u < U; ++u) {
+                const int t = (s0 + u) * EPS + slot;
+                const int p = __shfl(my_p, t < kWave ? t : 0);
+                const float v = __shfl(my_v, t < kWave ? t : 0);
+                if (t < n) {
+                    f4 o;
+                    o.x = v * gs[sb[u] & 0xff];
+                    o.y = v * gs[(sb[u] >> 8) & 0xff];
+                    o.z = v * gs[(sb[u] >> 16) & 0xff];
+                    o.w = v * gs[sb[u] >> 24];
+                    __builtin_nontemporal_store(o, reinterpret_cast<f4 *>(P + (size_t)p * K + sub * 4));
+                }
+            }
+        }
+    }
+}
+
+__device__ __forceinline__ void bwd_edges_stage_scalar(int e0, int e1, int k,
+                                                       const int32_t *__restrict__ idx,
+                                                       const float *__restrict__ val,
+                                                       const int32_t *__restrict__ csc_pos,
+                                                       const uint8_t *__restrict__ sel,
+                                                       const float *gs, float *__restrict__ P)
+{
+    const int lane = lane_id();
+    for (int e = e0; e < e1; ++e) {
+        const int c = idx[e];
+        const float v = val[e];
+        const size_t p = (size_t)csc_pos[e];
+        for (int l = lane; l < k; l += kWave) P[p * k + l] = v * gs[sel[(size_t)c * k + l]];
+    }
+}
+
+// Panel-scheduled backward push (ATOMIC when P == nullptr, STAGED otherwise).
+template <int K, bool STAGED>
+__global__ __launch_bounds__(kBlock) void bwd_panel_kernel(
+    const int2 *__restrict__ sched, int64_t num_panels, const int32_t *__restrict__ indptr,
+    const int32_t *__restrict__ idx, const float *__restrict__ val,
+    const float *__restrict__ grad, const uint8_t *__restrict__ sel,
+    const int32_t *__restrict__ csc_pos, int num_rows, int dim, int k,
+    float *__restrict__ dxs, float *__restrict__ P)
+{
+    extern __shared__ __attribute__((aligned(16))) float lds[];
+    float *gs = lds + (threadIdx.x / kWave) * kMaxDim;
+    zero_lds(gs, kMaxDim);  // columns >= dim read as 0
+    const int64_t w = (int64_t)blockIdx.x * kWavesPerBlock + threadIdx.x / kWave;
+    if (w >= num_panels) return;
+    const int2 a = sched[w], b = sched[w + 1];
+    const int i0 = a.x, j0 = a.y, i1 = b.x, j1 = b.y;
+    const int rlast = i1 < num_rows ? i1 : num_rows - 1;
+    for (int r = i0; r <= rlast; ++r) {
+        const int rb = indptr[r], re = indptr[r + 1];
+        const int eb = rb > j0 ? rb : j0;
+        const int ee = re < j1 ? re : j1;
+        if (eb >= ee) continue;
+        stage_row(gs, grad + (size_t)r * dim, dim);
+        if constexpr (STAGED) {
+            if constexpr (K > 0)
+                bwd_edges_stage_vec<K>(eb, ee, idx, val, csc_pos, sel, gs, P);
+            else
+                bwd_edges_stage_scalar(eb, ee, k, idx, val, csc_pos, sel, gs, P);
+        } else {
+            bwd_edges_atomic(eb, ee, k, idx, val, sel, gs, dxs);
+        }
+    }
+}
+
+// STAGED phase 2: dxs[c, :] = sum of P rows [csc_indptr[c], csc_indptr[c+1]),
+// merge-path panels over the CSC ranges, register accumulation + cross-slot
+// reduction; split destinations go through the carry fixup.
+template <int K>
+__device__ __forceinline__ f4 seg_sum_vec(int q0, int q1, const float *__restrict__ P)
+{
+    constexpr int LPE = K / 4;
+    constexpr int EPS = kWave / LPE;
+    const int lane = lane_id();
+    const int sub = lane % LPE;
+    const int slot = lane / LPE;
+    f4 s = f4{0.f, 0.f, 0.f, 0.f};
+    constexpr int U = 4;
+    int q = q0 + slot;
+    for (; q + (U - 1) * EPS < q1; q += U * EPS) {
+        f4 t[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u)
+            t[u] = __builtin_nontemporal_load(
+                reinterpret_cast<const f4 *>(P + (size_t)(q + u * EPS) * K + sub * 4));
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            s.x += t[u].x; s.y += t[u].y; s.z += t[u].z; s.w += t[u].w;
+        }
+    }
+    for (; q < q1; q += EPS) {
+        const f4 t = __builtin_nontemporal_load(
+            reinterpret_cast<const f4 *>(P + (size_t)q * K + sub * 4));
+        s.x += t.x; s.y += t.y; s.z += t.z; s.w += t.w;
+    }
+#pragma unroll
+    for (int m = LPE; m < kWave; m <<= 1) {
+        s.x += __shfl_xor(s.x, m);
+        s.y += __shfl_xor(s.y, m);
+        s.z += __shfl_xor(s.z, m);
+        s.w += __shfl_xor(s.w, m);
+    }
+    return s;  // every slot holds the total for its sub
+}
+
+template <int K>
+__global__ __launch_bounds__(kBlock) void bwd_segsum_kernel(
+    const int2 *__restrict__ sched, int64_t num_panels, const int32_t *__restrict__ cptr,
+    const float *__restrict__ P, int num_rows, int k, float *__restrict__ dxs,
+    float *__restrict__ carry, int32_t *__restrict__ carry_row)
+{
+    const int64_t w = (int64_t)blockIdx.x * kWavesPerBlock + threadIdx.x / kWave;
+    if (w >= num_panels) return;
+    const int lane = lane_id();
+    const int2 a = sched[w], b = sched[w + 1];
+    const int i0 = a.x, j0 = a.y, i1 = b.x, j1 = b.y;
+    int e = j0;
+    if constexpr (K > 0) {
+        constexpr int LPE = K / 4;
+        const int sub = lane % LPE;
+        const bool writer = lane < LPE;
+        for (int c = i0; c < i1; ++c) {
+            const int ce = cptr[c + 1];
+            const f4 s = seg_sum_vec<K>(e, ce, P);
+            if (writer) reinterpret_cast<f4 *>(dxs + (size_t)c * K)[sub] = s;
+            e = ce;
+        }
+        int has = 0;
+        f4 s = f4{0.f, 0.f, 0.f, 0.f};
+        if (i1 < num_rows) {
+            const int eb = e > cptr[i1] ? e : cptr[i1];
+            if (eb < j1) {
+                s = seg_sum_vec<K>(eb, j1, P);
+                has = 1;
+            }
+        }
+        if (has) {
+            if (writer) reinterpret_cast<f4 *>(carry + (size_t)w * K)[sub] = s;
+            if (lane == 0) carry_row[w] = i1;
+        } else if (lane == 0) {
+            carry_row[w] = -1;
+        }
+    } else {
+        // generic k: lane l accumulates column l (and l+64, ...)
+        for (int c = i0; c < i1; ++c) {
+            const int ce = cptr[c + 1];
+            for (int l = lane; l < k; l += kWave) {
+                float s = 0.f;
+                for (int q = e; q < ce; ++q) s += P[(size_t)q * k + l];
+                dxs[(size_t)c * k + l] = s;
+            }
+            e = ce;
+        }
+        int has = 0;
+        if (i1 < num_rows) {
+            const int eb = e > cptr[i1] ? e : cptr[i1];
+            if (eb < j1) {
+                for (int l = lane; l < k; l += kWave) {
+                    float s = 0.f;
+                    for (int q = eb; q < j1; ++q) s += P[(size_t)q * k + l];
+                    carry[(size_t)w * k + l] = s;
+                }
+                has = 1;
+            }
+        }
+        if (lane == 0) carry_row[w] = has ? i1 : -1;
+    }
+}
+
+// Backward, warp4-driven (drop-in): atomic push, G staged per row change.
+__global__ __launch_bounds__(kBlock) void bwd_warp4_kernel(
+    const int4 *__restrict__ warp4, int num_warps, int run, const int32_t *__restrict__ idx,
+    const float *__restrict__ val, const float *__restrict__ grad,
+    const uint8_t *__restrict__ sel, int dim, int k, float *__restrict__ dxs)
+{
+    extern __shared__ __attribute__((aligned(16))) float lds[];
+    float *gs = lds + (threadIdx.x / kWave) * kMaxDim;
+    zero_lds(gs, kMaxDim);  // columns >= dim read as 0
+    const int64_t w = (int64_t)blockIdx.x * kWavesPerBlock + threadIdx.x / kWave;
+    const int64_t q0 = w * run;
+    if (q0 >= num_warps) return;
+    const int q1 = (int)((q0 + run) < num_warps ? (q0 + run) : num_warps);
+    int cur = -1;
+    for (int q = (int)q0; q < q1; ++q) {
+        const int4 ch = warp4[q];
+        if (ch.x != cur) {
+            stage_row(gs, grad + (size_t)ch.x * dim, dim);
+            cur = ch.x;
+        }
+        bwd_edges_atomic(ch.y, ch.y + ch.z, k, idx, val, sel, gs, dxs);
+    }
+}
+
+// ---------------------------------------------------------------------------
+// Host-side dispatch
+// ---------------------------------------------------------------------------
+inline hipStream_t as_stream(void *s) { return reinterpret_cast<hipStream_t>(s); }
+
+inline int launch_status()
+{
+    const hipError_t e = hipGetLastError();
+    return e == hipSuccess ? MAXK_OK : (int)e;
+}
+
+inline int64_t ceil_div(int64_t a, int64_t b) { return (a + b - 1) / b; }
+
+inline size_t align_up(size_t x, size_t a) { return (x + a - 1) / a * a; }
+
+inline bool dims_ok(int dim, int k) { return dim >= 1 && dim <= kMaxDim && k >= 1 && k <= dim; }
+
+template <template <int> class F, typename... Args>
+int dispatch_k(int k, Args &&...args)
+{
+    switch (k) {
+    case 4: return F<4>::run(args...);
+    case 8: return F<8>::run(args...);
+    case 16: return F<16>::run(args...);
+    case 32: return F<32>::run(args...);
+    case 64: return F<64>::run(args...);
+    case 128: return F<128>::run(args...);
+    case 256: return F<256>::run(args...);
+    default: return F<0>::run(args...);
+    }
+}
+
+size_t fwd_lds_bytes(int dim) { (void)dim; return (size_t)kWavesPerBlock * kMaxDim * sizeof(float); }
+
+template <int K>
+struct FwdPanel {
+    static int run(const int32_t *sched, int64_t P, const int32_t *indptr, const int32_t *idx,
+                   const float *val, const float *data, const uint8_t *sel, int V, int dim, int k,
+                   float *out, float *carry, int32_t *carry_row, hipStream_t st)
+    {
+        const int64_t blocks = ceil_div(P, kWavesPerBlock);
+        hipLaunchKernelGGL(fwd_panel_kernel<K>, dim3((unsigned)blocks), dim3(kBlock),
+                           fwd_lds_bytes(dim), st, reinterpret_cast<const int2 *>(sched), P,
+                           indptr, idx, val, data, sel, V, dim, k, out, carry, carry_row);
+        int rc = launch_status();
+        if (rc) return rc;
+        hipLaunchKernelGGL(carry_fixup_kernel, dim3((unsigned)blocks), dim3(kBlock), 0, st, P,
+                           carry, carry_row, out, dim, (dim + 3) & ~3);
+        return launch_status();
+    }
+};
+
+template <int K>
+struct FwdWarp4 {
+    static int run(const int32_t *warp4, int W, const int32_t *idx, const float *val,
+                   const float *data, const uint8_t *sel, int dim, int k, float *out,
+                   hipStream_t st)
+    {
+        const int run = 16;
+        const int64_t waves = ceil_div(W, run);
+        hipLaunchKernelGGL(fwd_warp4_kernel<K>, dim3((unsigned)ceil_div(waves, kWavesPerBlock)),
+                           dim3(kBlock), fwd_lds_bytes(dim), st,
+                           reinterpret_cast<const int4 *>(warp4), W, run, idx, val, data, sel,
+                           dim, k, out);
+        return launch_status();
+    }
+};
+
+template <int K>
+struct BwdPanel {
+    static int run(bool staged, const int32_t *sched, int64_t P, const int32_t *indptr,
+                   const int32_t *idx, const float *val, const float *grad, const uint8_t *sel,
+                   const int32_t *csc_pos, int V, int dim, int k, float *dxs, float *Pbuf,
+                   hipStream_t st)
+    {
+        const int64_t blocks = ceil_div(P, kWavesPerBlock);
+        if (staged)
+            hipLaunchKernelGGL((bwd_panel_kernel<K, true>), dim3((unsigned)blocks), dim3(kBlock),
+                               fwd_lds_bytes(dim), st, reinterpret_cast<const int2 *>(sched), P,
+                               indptr, idx, val, grad, sel, csc_pos, V, dim, k, dxs, Pbuf);
+        else
+            hipLaunchKernelGGL((bwd_panel_kernel<K, false>), dim3((unsigned)blocks), dim3(kBlock),
+                               fwd_lds_bytes(dim), st, reinterpret_cast<const int2 *>(sched), P,
+                               indptr, idx, val, grad, sel, csc_pos, V, dim, k, dxs, Pbuf);
+        return launch_status();
+    }
+};
+
+template <int K>
+struct BwdSegsum {
+    static int run(const int32_t *csched, int64_t CP, const int32_t *cptr, const float *Pbuf,
+                   int V, int k, float *dxs, float *carry, int32_t *carry_row, hipStream_t st)
+    {
+        const int64_t blocks = ceil_div(CP, kWavesPerBlock);
+        hipLaunchKernelGGL(bwd_segsum_kernel<K>, dim3((unsigned)blocks), dim3(kBlock), 0, st,
+                           reinterpret_cast<const int2 *>(csched), CP, cptr, Pbuf, V, k, dxs,
+                           carry, carry_row);
+        int rc = launch_status();
+        if (rc) return rc;
+        hipLaunchKernelGGL(carry_fixup_kernel, dim3((unsigned)blocks), dim3(kBlock), 0, st, CP,
+                           carry, carry_row, dxs, k, k);
+        return launch_status();
+    }
+};
+
+}  // namespace
+
+// ===========================================================================
+// C ABI
+// ===========================================================================
+extern "C" {
+
+const char *maxk_version(void) { return MAXK_VERSION_STRING; }
+
+int maxk_schedule_num_panels(int64_t num_rows, int64_t num_edges, int panel_cost, int row_cost,
+                             int64_t *num_panels)
+{
+    if (!num_panels || num_rows < 0 || num_edges < 0 || panel_cost < 1 || row_cost < 1)
+        return MAXK_E_ARG;
+    const int64_t total = num_edges + num_rows * (int64_t)row_cost;
+    int64_t p = ceil_div(total, panel_cost);
+    *num_panels = p < 1 ? 1 : p;
+    return MAXK_OK;
+}
+
+int maxk_schedule_build(const int32_t *indptr, int num_rows, int panel_cost, int row_cost,
+                        int32_t *sched, int64_t num_panels, void *stream)
+{
+    if (!indptr || !sched || num_rows < 0 || panel_cost < 1 || row_cost < 1 || num_panels < 1)
+        return MAXK_E_ARG;
+    const int64_t n = num_panels + 1;
+    hipLaunchKernelGGL(schedule_kernel, dim3((unsigned)ceil_div(n, 256)), dim3(256), 0,
+                       as_stream(stream), indptr, num_rows, panel_cost, row_cost,
+                       reinterpret_cast<int2 *>(sched), num_panels);
+    return launch_status();
+}
+
+int maxk_warp4_build(const int32_t *indptr, int num_rows, int warp_max_nz, int32_t *chunk_offsets,
+                     int32_t *warp4, int64_t warp4_capacity, int64_t *num_warps, void *stream)
+{
+    if (!indptr || !chunk_offsets || !num_warps || num_rows < 0 || warp_max_nz < 1)
+        return MAXK_E_ARG;
+    hipStream_t st = as_stream(stream);
+    if (num_rows == 0) { *num_warps = 0; return MAXK_OK; }
+    hipLaunchKernelGGL(warp4_count_kernel, dim3((unsigned)ceil_div(num_rows, 256)), dim3(256), 0,
+                       st, indptr, num_rows, warp_max_nz, chunk_offsets);
+    int rc = launch_status();
+    if (rc) return rc;
+    hipLaunchKernelGGL(exclusive_scan_1block, dim3(1), dim3(256), 0, st, chunk_offsets, num_rows,
+                       chunk_offsets + num_rows);
+    rc = launch_status();
+    if (rc) return rc;
+    int32_t total = 0;
+    hipError_t e = hipMemcpyAsync(&total, chunk_offsets + num_rows, sizeof(int32_t),
+                                  hipMemcpyDeviceToHost, st);
+    if (e != hipSuccess) return (int)e;
+    e = hipStreamSynchronize(st);
+    if (e != hipSuccess) return (int)e;
+    *num_warps = total;
+    if (!warp4) return MAXK_OK;  // count-only call
+    if (warp4_capacity < total) return MAXK_E_WORKSPACE;
+    hipLaunchKernelGGL(warp4_fill_kernel, dim3((unsigned)ceil_div(num_rows, 256)), dim3(256), 0,
+                       st, indptr, num_rows, warp_max_nz, chunk_offsets,
+                       reinterpret_cast<int4 *>(warp4));
+    return launch_status();
+}
+
+size_t maxk_forward_workspace_bytes(int64_t num_panels, int dim_origin)
+{
+    const size_t dimp = (size_t)((dim_origin + 3) & ~3);
+    return align_up((size_t)num_panels * dimp * sizeof(float), 256) +
+           align_up((size_t)num_panels * sizeof(int32_t), 256);
+}
+
+int maxk_spgemm_forward(const int32_t *sched, int64_t num_panels, const int32_t *indptr,
+                        const int32_t *indices, const float *values, const float *cbsr_data,
+                        const uint8_t *cbsr_sel, int num_rows, int dim_origin, int dim_k,
+                        float *out, void *workspace, size_t workspace_bytes, void *stream)
+{
+    if (!sched || !indptr || !out || num_panels < 1 || num_rows < 0) return MAXK_E_ARG;
+    if (!dims_ok(dim_origin, dim_k)) return MAXK_E_DIM;
+    if (num_rows == 0) return MAXK_OK;
+    if (!indices || !values || !cbsr_data || !cbsr_sel) return MAXK_E_ARG;
+    if (!workspace || workspace_bytes < maxk_forward_workspace_bytes(num_panels, dim_origin))
+        return MAXK_E_WORKSPACE;
+    const size_t dimp = (size_t)((dim_origin + 3) & ~3);
+    float *carry = static_cast<float *>(workspace);
+    int32_t *carry_row = reinterpret_cast<int32_t *>(
+        static_cast<char *>(workspace) + align_up((size_t)num_panels * dimp * sizeof(float), 256));
+    return dispatch_k<FwdPanel>(dim_k, sched, num_panels, indptr, indices, values, cbsr_data,
+                                cbsr_sel, num_rows, dim_origin, dim_k, out, carry, carry_row,
+                                as_stream(stream));
+}
+
+size_t maxk_backward_workspace_bytes(int algo, int64_t num_edges, int dim_k,
+                                     int64_t csc_num_panels)
+{
+    if (algo == MAXK_BWD_ATOMIC) return 0;
+    return align_up((size_t)num_edges * dim_k * sizeof(float), 256) +
+           align_up((size_t)csc_num_panels * dim_k * sizeof(float), 256) +
+           align_up((size_t)csc_num_panels * sizeof(int32_t), 256);
+}
+
+int maxk_sspmm_backward(int algo, const int32_t *sched, int64_t num_panels,
+                        const int32_t *indptr, const int32_t *indices, const float *values,
+                        const float *grad, const uint8_t *cbsr_sel, int num_rows,
+                        int64_t num_edges, int dim_origin, int dim_k, float *dxs,
+                        const int32_t *csc_pos, const int32_t *csc_sched,
+                        int64_t csc_num_panels, const int32_t *csc_indptr, void *workspace,
+                        size_t workspace_bytes, void *stream)
+{
+    if (!sched || !indptr || !dxs || num_panels < 1 || num_rows < 0) return MAXK_E_ARG;
+    if (!dims_ok(dim_origin, dim_k)) return MAXK_E_DIM;
+    hipStream_t st = as_stream(stream);
+    if (num_rows == 0) return MAXK_OK;
+    if (!indices || !values || !grad || !cbsr_sel) return MAXK_E_ARG;
+    const bool staged_ready = csc_pos && csc_sched && csc_indptr && csc_num_panels >= 1 &&
+                              workspace;
+    if (algo == MAXK_BWD_AUTO) algo = staged_ready ? MAXK_BWD_STAGED : MAXK_BWD_ATOMIC;
+    if (algo == MAXK_BWD_ATOMIC) {
+        hipError_t e = hipMemsetAsync(dxs, 0, (size_t)num_rows * dim_k * sizeof(float), st);
+        if (e != hipSuccess) return (int)e;
+        return dispatch_k<BwdPanel>(dim_k, false, sched, num_panels, indptr, indices, values, grad,
+                                    cbsr_sel, (const int32_t *)nullptr, num_rows, dim_origin, dim_k,
+                                    dxs, (float *)nullptr, st);
+    }
+    if (algo != MAXK_BWD_STAGED || !staged_ready) return MAXK_E_ARG;
+    // workspace: [P rows (E*k floats)] [carry (CP*k floats)] [carry_row (CP ints)]
+    if (num_edges < 0) return MAXK_E_ARG;
+    if (workspace_bytes < maxk_backward_workspace_bytes(algo, num_edges, dim_k, csc_num_panels))
+        return MAXK_E_WORKSPACE;
+    const size_t pbytes = align_up((size_t)num_edges * dim_k * sizeof(float), 256);
+    const size_t carry_bytes = align_up((size_t)csc_num_panels * dim_k * sizeof(float), 256);
+    float *Pbuf = static_cast<float *>(workspace);
+    float *carry = reinterpret_cast<float *>(static_cast<char *>(workspace) + pbytes);
+    int32_t *carry_row = reinterpret_cast<int32_t *>(static_cast<char *>(workspace) + pbytes +
+                                                     carry_bytes);
+    int rc = dispatch_k<BwdPanel>(dim_k, true, sched, num_panels, indptr, indices, values, grad,
+                                  cbsr_sel, csc_pos, num_rows, dim_origin, dim_k, dxs, Pbuf, st);
+    if (rc) return rc;
+    return dispatch_k<BwdSegsum>(dim_k, csc_sched, csc_num_panels, csc_indptr, Pbuf, num_rows,
+                                 dim_k, dxs, carry, carry_row, st);
+}
+
+int maxk_spmm_forward_warp4(const int32_t *warp4, const int32_t *idx, const float *val,
+                            const float *vin_data, const uint8_t *vin_selector, float *vout,
+                            int num_v, int num_e, int feat_in, int dim_sparse, int num_warps,
+                            void *stream)
+{
+    (void)num_e;
+    if (num_warps < 0 || num_v < 0) return MAXK_E_ARG;
+    if (!dims_ok(feat_in, dim_sparse)) return MAXK_E_DIM;
+    if (num_warps == 0) return MAXK_OK;
+    if (!warp4 || !idx || !val || !vin_data || !vin_selector || !vout) return MAXK_E_ARG;
+    return dispatch_k<FwdWarp4>(dim_sparse, warp4, num_warps, idx, val, vin_data, vin_selector,
+                                feat_in, dim_sparse, vout, as_stream(stream));
+}
+
+int maxk_spmm_backward_warp4(const int32_t *warp4, const int32_t *idx, const float *val,
+                             const float *vin_data, const uint8_t *vin_selector, float *vout,
+                             int num_v, int num_e, int feat_in, int dim_sparse, int num_warps,
+                             void *stream)
+{
+    (void)num_e;
+    if (num_warps < 0 || num_v < 0) return MAXK_E_ARG;
+    if (!dims_ok(feat_in, dim_sparse)) return MAXK_E_DIM;
+    if (num_warps == 0) return MAXK_OK;
+    if (!warp4 || !idx || !val || !vin_data || !vin_selector || !vout) return MAXK_E_ARG;
+    const int run = 16;
+    const int64_t waves = ceil_div(num_warps, run);
+    hipLaunchKernelGGL(bwd_warp4_kernel, dim3((unsigned)ceil_div(waves, kWavesPerBlock)),
+                       dim3(kBlock), fwd_lds_bytes(feat_in), as_stream(stream),
+                       reinterpret_cast<const int4 *>(warp4), num_warps, run, idx, val, vin_data,
+                       vin_selector, feat_in, dim_sparse, vout);
+    return launch_status();
+}
+
+}  // extern "C"

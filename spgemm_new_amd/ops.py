@@ -1,0 +1,221 @@
+"""Host-side API of the MI355X MaxK aggregation path.
+
+``MaxKGraph`` owns a CSR adjacency resident in HBM plus everything the kernels
+need that the reference kept in files or rebuilt per call:
+
+* the merge-path panel schedule (replaces the ``.warp4`` file of
+  kernels/generate_meta.py:26-48, read per call at spmm_maxk.cu:117);
+* the CSC transpose (edge -> CSC slot, CSC row pointer and its own panel
+  schedule) used by the STAGED backward;
+* cached workspaces (carry rows, staging rows).
+
+All compute goes through the C ABI (``_lib``); there is no CPU or PyTorch
+fallback for the kernels.  Building the transpose uses torch GPU sort/scan
+ops once per graph (plumbing, outside the hot path).
+"""
+from __future__ import annotations
+
+import torch
+
+from . import _lib
+
+__all__ = ["MaxKGraph", "check_tensor", "spgemm_forward", "sspmm_backward", "warp4_build"]
+
+
+def check_tensor(t, name: str, dtype=None, cuda: bool = True, dim: int | None = None):
+    """TORCH_CHECK-style validation (cuda_kernel_bindings.cpp:52-62)."""
+    if not isinstance(t, torch.Tensor):
+        raise TypeError(f"{name} must be a torch.Tensor")
+    if cuda and not t.is_cuda:
+        raise RuntimeError(f"{name} must be CUDA tensor")
+    if dtype is not None and t.dtype != dtype:
+        raise RuntimeError(f"{name} must be {str(dtype).replace('torch.', '')}")
+    if dim is not None and t.dim() != dim:
+        raise RuntimeError(f"{name} must be {dim}D tensor")
+    if not t.is_contiguous():
+        raise RuntimeError(f"{name} must be contiguous")
+    return t
+
+
+def _stream(t):
+    return _lib.stream_ptr(t.device)
+
+
+def _build_schedule(indptr: torch.Tensor, num_rows: int, num_edges: int, panel_cost: int,
+                    row_cost: int):
+    L = _lib.load()
+    import ctypes
+    n = ctypes.c_int64(0)
+    _lib.check(L.maxk_schedule_num_panels(num_rows, num_edges, panel_cost, row_cost,
+                                          ctypes.byref(n)), "maxk_schedule_num_panels")
+    P = int(n.value)
+    sched = torch.empty(2 * (P + 1), dtype=torch.int32, device=indptr.device)
+    _lib.check(L.maxk_schedule_build(indptr.data_ptr(), num_rows, panel_cost, row_cost,
+                                     sched.data_ptr(), P, _stream(indptr)), "maxk_schedule_build")
+    return sched, P
+
+
+class MaxKGraph:
+    """A CSR graph on one GPU, ready for the MaxK SpGEMM / SSpMM kernels.
+
+    Parameters mirror the reference's graph tuple ``(indptr, indices, values)``
+    (utils/models.py:67, 227); ``values`` defaults to ones (sum aggregation, as
+    in training, utils/models.py:227).
+    """
+
+    def __init__(self, indptr: torch.Tensor, indices: torch.Tensor,
+                 values: torch.Tensor | None = None, *, panel_cost: int = _lib.DEFAULT_PANEL_COST,
+                 row_cost: int = _lib.DEFAULT_ROW_COST, bwd_panel_cost: int | None = None,
+                 csc_panel_cost: int | None = None):
+        check_tensor(indptr, "indptr", torch.int32, dim=1)
+        check_tensor(indices, "indices", torch.int32, dim=1)
+        if values is None:
+            values = torch.ones(indices.numel(), dtype=torch.float32, device=indices.device)
+        check_tensor(values, "values", torch.float32, dim=1)
+        if values.numel() != indices.numel():
+            raise RuntimeError("values and indices must have the same length")
+        if indptr.device != indices.device or values.device != indices.device:
+            raise RuntimeError("graph tensors must be on the same device")
+        self.num_rows = indptr.numel() - 1
+        self.num_edges = indices.numel()
+        if self.num_edges == 0:  # the C ABI wants valid pointers even for an empty edge list
+            indices = torch.zeros(1, dtype=torch.int32, device=indices.device)
+            values = torch.zeros(1, dtype=torch.float32, device=indices.device)
+        self.indptr, self.indices, self.values = indptr, indices, values
+        self.device = indices.device
+        self.panel_cost, self.row_cost = panel_cost, row_cost
+        self.sched, self.num_panels = _build_schedule(indptr, self.num_rows, self.num_edges,
+                                                      panel_cost, row_cost)
+        if bwd_panel_cost is not None and bwd_panel_cost != panel_cost:
+            self.bwd_sched, self.bwd_num_panels = _build_schedule(
+                indptr, self.num_rows, self.num_edges, bwd_panel_cost, row_cost)
+        else:
+            self.bwd_sched, self.bwd_num_panels = self.sched, self.num_panels
+        self.csc_panel_cost = csc_panel_cost or panel_cost
+        self._csc = None
+        self._ws = {}
+
+    # ------------------------------------------------------------------ utils
+    def _workspace(self, key, nbytes: int) -> torch.Tensor:
+        t = self._ws.get(key)
+        if t is None or t.numel() < nbytes:
+            t = torch.empty(max(nbytes, 1), dtype=torch.uint8, device=self.device)
+            self._ws[key] = t
+        return t
+
+    def csc(self):
+        """(csc_pos, csc_indptr, csc_sched, csc_num_panels), built once."""
+        if self._csc is None:
+            idx = self.indices[: self.num_edges].long()
+            order = torch.argsort(idx, stable=True)
+            csc_pos = torch.empty(self.num_edges, dtype=torch.int32, device=self.device)
+            csc_pos[order] = torch.arange(self.num_edges, dtype=torch.int32, device=self.device)
+            counts = torch.bincount(idx, minlength=self.num_rows)[: self.num_rows]
+            csc_indptr = torch.zeros(self.num_rows + 1, dtype=torch.int32, device=self.device)
+            csc_indptr[1:] = torch.cumsum(counts, 0).to(torch.int32)
+            sched, P = _build_schedule(csc_indptr, self.num_rows, self.num_edges,
+                                       self.csc_panel_cost, self.row_cost)
+            self._csc = (csc_pos, csc_indptr, sched, P)
+        return self._csc
+
+    def nbytes_fwd(self, dim_k: int, dim_origin: int) -> int:
+        """Algorithmic bytes of one forward call: 8E + 5kE + 4hV."""
+        return 8 * self.num_edges + 5 * dim_k * self.num_edges + 4 * dim_origin * self.num_rows
+
+    nbytes_bwd = nbytes_fwd
+
+    # ---------------------------------------------------------------- compute
+    def forward(self, cbsr_data: torch.Tensor, cbsr_sel: torch.Tensor, dim_origin: int = 256,
+                out: torch.Tensor | None = None, values: torch.Tensor | None = None) -> torch.Tensor:
+        """Y = A . scatter(CBSR)  (spmm_maxk.cu:17-106).  Returns fp32[V, dim_origin]."""
+        return spgemm_forward(self, cbsr_data, cbsr_sel, dim_origin, out, values)
+
+    def backward(self, grad: torch.Tensor, cbsr_sel: torch.Tensor, out: torch.Tensor | None = None,
+                 values: torch.Tensor | None = None, algo: int = _lib.MAXK_BWD_AUTO) -> torch.Tensor:
+        """dXs = (A^T G) sampled at sel  (spmm_maxk_backward.cu:15-115).  Returns fp32[V, k]."""
+        return sspmm_backward(self, grad, cbsr_sel, out, values, algo)
+
+
+def _check_cbsr(g: MaxKGraph, data, sel):
+    check_tensor(data, "input_data", torch.float32, dim=2)
+    check_tensor(sel, "sparse_selector", torch.uint8, dim=2)
+    if data.shape != sel.shape:
+        raise RuntimeError("input_data and sparse_selector must have the same shape")
+    if data.shape[0] != g.num_rows:
+        raise RuntimeError(f"CBSR has {data.shape[0]} rows, graph has {g.num_rows}")
+    if data.device != g.device or sel.device != g.device:
+        raise RuntimeError("CBSR tensors must be on the graph's device")
+
+
+def spgemm_forward(g: MaxKGraph, data, sel, dim_origin: int = 256, out=None, values=None):
+    _check_cbsr(g, data, sel)
+    k = data.shape[1]
+    if values is None:
+        values = g.values
+    check_tensor(values, "values", torch.float32, dim=1)
+    if out is None:
+        out = torch.empty((g.num_rows, dim_origin), dtype=torch.float32, device=g.device)
+    else:
+        check_tensor(out, "output", torch.float32, dim=2)
+        if tuple(out.shape) != (g.num_rows, dim_origin):
+            raise RuntimeError("output has the wrong shape")
+    L = _lib.load()
+    nbytes = L.maxk_forward_workspace_bytes(g.num_panels, dim_origin)
+    ws = g._workspace(("fwd", dim_origin), nbytes)
+    _lib.check(L.maxk_spgemm_forward(g.sched.data_ptr(), g.num_panels, g.indptr.data_ptr(),
+                                     g.indices.data_ptr(), values.data_ptr(), data.data_ptr(),
+                                     sel.data_ptr(), g.num_rows, dim_origin, k, out.data_ptr(),
+                                     ws.data_ptr(), ws.numel(), _stream(out)), "maxk_spgemm_forward")
+    return out
+
+
+def sspmm_backward(g: MaxKGraph, grad, sel, out=None, values=None, algo: int = _lib.MAXK_BWD_AUTO):
+    check_tensor(grad, "grad_output", torch.float32, dim=2)
+    check_tensor(sel, "sparse_selector", torch.uint8, dim=2)
+    if grad.shape[0] != g.num_rows or sel.shape[0] != g.num_rows:
+        raise RuntimeError("grad_output / sparse_selector rows must equal the graph's rows")
+    dim_origin, k = grad.shape[1], sel.shape[1]
+    if values is None:
+        values = g.values
+    if out is None:
+        out = torch.empty((g.num_rows, k), dtype=torch.float32, device=g.device)
+    else:
+        check_tensor(out, "grad_input", torch.float32, dim=2)
+        if tuple(out.shape) != (g.num_rows, k):
+            raise RuntimeError("grad_input has the wrong shape")
+    if algo == _lib.MAXK_BWD_AUTO:
+        algo = _lib.MAXK_BWD_STAGED
+    if g.num_edges == 0:
+        algo = _lib.MAXK_BWD_ATOMIC  # nothing to stage: the call just zeroes dXs
+    L = _lib.load()
+    csc_pos = csc_indptr = csc_sched = None
+    CP = 0
+    ws = None
+    if algo == _lib.MAXK_BWD_STAGED:
+        csc_pos, csc_indptr, csc_sched, CP = g.csc()
+        nbytes = L.maxk_backward_workspace_bytes(algo, g.num_edges, k, CP)
+        ws = g._workspace(("bwd", k), nbytes)
+    _lib.check(L.maxk_sspmm_backward(
+        algo, g.bwd_sched.data_ptr(), g.bwd_num_panels, g.indptr.data_ptr(), g.indices.data_ptr(),
+        values.data_ptr(), grad.data_ptr(), sel.data_ptr(), g.num_rows, g.num_edges, dim_origin, k,
+        out.data_ptr(), _lib.ptr(csc_pos), _lib.ptr(csc_sched), CP, _lib.ptr(csc_indptr),
+        _lib.ptr(ws), 0 if ws is None else ws.numel(), _stream(out)), "maxk_sspmm_backward")
+    return out
+
+
+def warp4_build(indptr: torch.Tensor, warp_max_nz: int = 64) -> torch.Tensor:
+    """generate_meta.py:26-48 on the device: int32[4W] (row, loc, len, 0)."""
+    import ctypes
+    check_tensor(indptr, "indptr", torch.int32, dim=1)
+    L = _lib.load()
+    V = indptr.numel() - 1
+    scratch = torch.empty(V + 1, dtype=torch.int32, device=indptr.device)
+    n = ctypes.c_int64(0)
+    st = _stream(indptr)
+    _lib.check(L.maxk_warp4_build(indptr.data_ptr(), V, warp_max_nz, scratch.data_ptr(), None, 0,
+                                  ctypes.byref(n), st), "maxk_warp4_build(count)")
+    W = int(n.value)
+    warp4 = torch.empty(4 * max(W, 1), dtype=torch.int32, device=indptr.device)
+    _lib.check(L.maxk_warp4_build(indptr.data_ptr(), V, warp_max_nz, scratch.data_ptr(),
+                                  warp4.data_ptr(), W, ctypes.byref(n), st), "maxk_warp4_build")
+    return warp4[: 4 * W]
