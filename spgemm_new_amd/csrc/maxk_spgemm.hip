@@ -153,22 +153,77 @@ __global__ __launch_bounds__(256) void exclusive_scan_1block(int32_t *c, int n, 
 }
 
 // ---------------------------------------------------------------------------
-// Forward: gather-scatter of one edge range into the wave's LDS row.
-// K % 4 == 0: each lane owns 4 consecutive CBSR entries of one edge.
+// Forward: gather-scatter of one edge range into the wave's LDS rows.
+//
+// LDS float atomics (ds_add_f32) are ~7x slower than the gathers on gfx950
+// (tools/ablate/fwd_ablate.hip), so the accumulation is a plain
+// ds_read + v_add + ds_write.  That is race-free because every lane of one
+// wave-instruction writes a distinct LDS word: the LPE lanes of one edge own
+// distinct selected columns (a CBSR row has k distinct columns), and the EPS
+// edges of one step each own a private copy of the row accumulator.  Copies
+// are summed when the row is flushed.  Later steps are ordered after earlier
+// ones by the in-order LDS queue of the wave (the compiler cannot reorder the
+// may-alias accesses of one lane).
+//
+// Layout per compile-time K: VEC consecutive CBSR entries per lane (dwordx4 /
+// dwordx2 / dword data + the matching selector bytes), LPE lanes per edge,
+// EPS = 64 / LPE edges per step = LDS row copies.  LPE >= 8 keeps the copies
+// at <= 8 KB per wave for every k >= 8.
 // ---------------------------------------------------------------------------
+template <int K>
+struct FwdLayout {
+    static constexpr int VEC = K >= 32 ? 4 : (K >= 16 ? 2 : 1);
+    static constexpr int LPE = K / VEC;
+    static constexpr int EPS = kWave / LPE;
+};
+
+__host__ __device__ constexpr int fwd_copies_generic(int k) { return k >= kWave ? 1 : kWave / k; }
+
+template <int K>
+__host__ __device__ constexpr int fwd_copies(int k)
+{
+    if constexpr (K > 0) return FwdLayout<K>::EPS;
+    else return fwd_copies_generic(k);
+}
+
+template <int VEC>
+struct VecT;
+template <> struct VecT<4> { typedef f4 D; typedef uint32_t S; };
+template <> struct VecT<2> { typedef float D __attribute__((ext_vector_type(2))); typedef uint16_t S; };
+template <> struct VecT<1> { typedef float D; typedef uint8_t S; };
+
+template <int VEC>
+__device__ __forceinline__ void rmw_acc(float *acc, typename VecT<VEC>::S sb, float v,
+                                        typename VecT<VEC>::D d)
+{
+    if constexpr (VEC == 4) {
+        float *p0 = acc + (sb & 0xff), *p1 = acc + ((sb >> 8) & 0xff);
+        float *p2 = acc + ((sb >> 16) & 0xff), *p3 = acc + (sb >> 24);
+        *p0 += v * d.x; *p1 += v * d.y; *p2 += v * d.z; *p3 += v * d.w;
+    } else if constexpr (VEC == 2) {
+        float *p0 = acc + (sb & 0xff), *p1 = acc + (sb >> 8);
+        *p0 += v * d.x; *p1 += v * d.y;
+    } else {
+        acc[sb] += v * d;
+    }
+}
+
 template <int K>
 __device__ __forceinline__ void fwd_edges_vec(int e0, int e1, const int32_t *__restrict__ idx,
                                               const float *__restrict__ val,
                                               const float *__restrict__ data,
                                               const uint8_t *__restrict__ sel, float *acc)
 {
-    constexpr int LPE = K / 4;          // lanes per edge
-    constexpr int EPS = kWave / LPE;    // edges per step
-    constexpr int STEPS = kWave / EPS;  // steps per 64-edge batch (== LPE)
+    using Lay = FwdLayout<K>;
+    constexpr int VEC = Lay::VEC, LPE = Lay::LPE, EPS = Lay::EPS;
+    constexpr int STEPS = kWave / EPS;  // steps per 64-edge batch
     constexpr int U = STEPS < 8 ? STEPS : 8;
+    using D = typename VecT<VEC>::D;
+    using SB = typename VecT<VEC>::S;
     const int lane = lane_id();
     const int sub = lane % LPE;
     const int slot = lane / LPE;
+    float *my_acc = acc + slot * kMaxDim;
     for (int base = e0; base < e1; base += kWave) {
         const int n = (e1 - base) < kWave ? (e1 - base) : kWave;
         int my_c = 0;
@@ -180,8 +235,8 @@ __device__ __forceinline__ void fwd_edges_vec(int e0, int e1, const int32_t *__r
 #pragma unroll
         for (int s0 = 0; s0 < STEPS; s0 += U) {
             if (s0 * EPS >= n) break;
-            f4 d[U];
-            uint32_t sb[U];
+            D d[U];
+            SB sb[U];
             float v[U];
 #pragma unroll
             for (int u = 0; u < U; ++u) {
@@ -189,30 +244,21 @@ __device__ __forceinline__ void fwd_edges_vec(int e0, int e1, const int32_t *__r
                 const int c = __shfl(my_c, t < kWave ? t : 0);
                 v[u] = __shfl(my_v, t < kWave ? t : 0);
                 if (t < n) {
-                    const size_t off = (size_t)c * K + sub * 4;
-                    d[u] = *reinterpret_cast<const f4 *>(data + off);
-                    sb[u] = *reinterpret_cast<const uint32_t *>(sel + off);
-                } else {
-                    v[u] = 0.f;
-                    d[u] = f4{0.f, 0.f, 0.f, 0.f};
-                    sb[u] = 0;
+                    const size_t off = (size_t)c * K + sub * VEC;
+                    d[u] = *reinterpret_cast<const D *>(data + off);
+                    sb[u] = *reinterpret_cast<const SB *>(sel + off);
                 }
             }
 #pragma unroll
             for (int u = 0; u < U; ++u) {
                 const int t = (s0 + u) * EPS + slot;
-                if (t < n) {
-                    lds_add(acc + (sb[u] & 0xff), v[u] * d[u].x);
-                    lds_add(acc + ((sb[u] >> 8) & 0xff), v[u] * d[u].y);
-                    lds_add(acc + ((sb[u] >> 16) & 0xff), v[u] * d[u].z);
-                    lds_add(acc + (sb[u] >> 24), v[u] * d[u].w);
-                }
+                if (t < n) rmw_acc<VEC>(my_acc, sb[u], v[u], d[u]);
             }
         }
     }
 }
 
-// Any k: one CBSR entry per lane.
+// Any k: one CBSR entry per lane, EPS = 64 / min(k, 64) row copies.
 __device__ __forceinline__ void fwd_edges_scalar(int e0, int e1, int k,
                                                  const int32_t *__restrict__ idx,
                                                  const float *__restrict__ val,
@@ -223,13 +269,14 @@ __device__ __forceinline__ void fwd_edges_scalar(int e0, int e1, int k,
     if (k <= kWave) {
         const int eps = kWave / k;
         const int slot = lane / k, l = lane % k;
+        float *my_acc = acc + slot * kMaxDim;
         for (int e = e0; e < e1; e += eps) {
             const int my = e + slot;
             if (slot < eps && my < e1) {
                 const int c = idx[my];
                 const float v = val[my];
                 const size_t off = (size_t)c * k + l;
-                lds_add(acc + sel[off], v * data[off]);
+                my_acc[sel[off]] += v * data[off];
             }
         }
     } else {
@@ -238,7 +285,7 @@ __device__ __forceinline__ void fwd_edges_scalar(int e0, int e1, int k,
             const float v = val[e];
             for (int l = lane; l < k; l += kWave) {
                 const size_t off = (size_t)c * k + l;
-                lds_add(acc + sel[off], v * data[off]);
+                acc[sel[off]] += v * data[off];
             }
         }
     }
@@ -256,44 +303,37 @@ __device__ __forceinline__ void fwd_edges(int e0, int e1, int k, const int32_t *
         fwd_edges_scalar(e0, e1, k, idx, val, data, sel, acc);
 }
 
-// acc (dim floats, dim % 4 == 0 padded) -> dst row, then zero acc.
-__device__ __forceinline__ void flush_store(float *acc, float *__restrict__ dst, int dim)
+// Row flushes: sum the `copies` LDS row copies, zero them, and store / add.
+enum FlushOp { kStore = 0, kAtomic = 1, kAdd = 2 };
+
+template <int OP>
+__device__ __forceinline__ void flush_row(float *acc, int copies, float *__restrict__ dst, int dim)
 {
     const int lane = lane_id();
     wave_sync_lds();
-    if ((dim & 3) == 0) {
+    if (OP == kStore && (dim & 3) == 0) {
         for (int c4 = lane; c4 < (dim >> 2); c4 += kWave) {
             f4 a = reinterpret_cast<f4 *>(acc)[c4];
-            reinterpret_cast<f4 *>(dst)[c4] = a;
             reinterpret_cast<f4 *>(acc)[c4] = f4{0.f, 0.f, 0.f, 0.f};
+            for (int cp = 1; cp < copies; ++cp) {
+                f4 *q = reinterpret_cast<f4 *>(acc + cp * kMaxDim) + c4;
+                a += *q;
+                *q = f4{0.f, 0.f, 0.f, 0.f};
+            }
+            reinterpret_cast<f4 *>(dst)[c4] = a;
         }
     } else {
-        for (int c = lane; c < dim; c += kWave) {
-            dst[c] = acc[c];
+        for (int c = lane; c < dim; c += kWave) {  // 256 contiguous bytes per instruction
+            float a = acc[c];
             acc[c] = 0.f;
+            for (int cp = 1; cp < copies; ++cp) {
+                a += acc[cp * kMaxDim + c];
+                acc[cp * kMaxDim + c] = 0.f;
+            }
+            if (OP == kStore) dst[c] = a;
+            else if (OP == kAtomic) gbl_add(dst + c, a);
+            else dst[c] += a;
         }
-    }
-    wave_sync_lds();
-}
-
-__device__ __forceinline__ void flush_atomic(float *acc, float *__restrict__ dst, int dim)
-{
-    const int lane = lane_id();
-    wave_sync_lds();
-    for (int c = lane; c < dim; c += kWave) {  // 256 contiguous bytes per instruction
-        gbl_add(dst + c, acc[c]);
-        acc[c] = 0.f;
-    }
-    wave_sync_lds();
-}
-
-__device__ __forceinline__ void flush_rmw(float *acc, float *__restrict__ dst, int dim)
-{
-    const int lane = lane_id();
-    wave_sync_lds();
-    for (int c = lane; c < dim; c += kWave) {
-        dst[c] += acc[c];
-        acc[c] = 0.f;
     }
     wave_sync_lds();
 }
@@ -315,17 +355,19 @@ __global__ __launch_bounds__(kBlock) void fwd_panel_kernel(
 {
     extern __shared__ __attribute__((aligned(16))) float lds[];
     const int dimp = (dim + 3) & ~3;
-    float *acc = lds + (threadIdx.x / kWave) * kMaxDim;  // selectors are uint8: never out of bounds
+    const int copies = fwd_copies<K>(k);
+    // selectors are uint8, so a full 256-float row per copy is never overrun
+    float *acc = lds + (threadIdx.x / kWave) * copies * kMaxDim;
     const int64_t w = (int64_t)blockIdx.x * kWavesPerBlock + threadIdx.x / kWave;
     if (w >= num_panels) return;
-    zero_lds(acc, kMaxDim);
+    zero_lds(acc, copies * kMaxDim);
     const int2 a = sched[w], b = sched[w + 1];
     const int i0 = a.x, j0 = a.y, i1 = b.x, j1 = b.y;
     int e = j0;
     for (int r = i0; r < i1; ++r) {
         const int re = indptr[r + 1];
         if (e < re) fwd_edges<K>(e, re, k, idx, val, data, sel, acc);
-        flush_store(acc, out + (size_t)r * dim, dim);
+        flush_row<kStore>(acc, copies, out + (size_t)r * dim, dim);
         e = re;
     }
     int has_carry = 0;
@@ -337,7 +379,7 @@ __global__ __launch_bounds__(kBlock) void fwd_panel_kernel(
         }
     }
     if (has_carry) {
-        flush_store(acc, carry + (size_t)w * dimp, dimp);
+        flush_row<kStore>(acc, copies, carry + (size_t)w * dimp, dimp);
         if (lane_id() == 0) carry_row[w] = i1;
     } else if (lane_id() == 0) {
         carry_row[w] = -1;
@@ -361,6 +403,7 @@ __global__ __launch_bounds__(kBlock) void carry_fixup_kernel(
 // warp4-driven forward (drop-in for the reference launcher).  A wave takes a
 // run of `run` consecutive chunks; rows entirely inside the run are added
 // with plain read-modify-write, rows crossing a run edge with global atomics.
+// Requires the chunks of a row to be consecutive (generate_meta.py order).
 template <int K>
 __global__ __launch_bounds__(kBlock) void fwd_warp4_kernel(
     const int4 *__restrict__ warp4, int num_warps, int run, const int32_t *__restrict__ idx,
@@ -368,12 +411,13 @@ __global__ __launch_bounds__(kBlock) void fwd_warp4_kernel(
     const uint8_t *__restrict__ sel, int dim, int k, float *__restrict__ out)
 {
     extern __shared__ __attribute__((aligned(16))) float lds[];
-    float *acc = lds + (threadIdx.x / kWave) * kMaxDim;  // selectors are uint8: never out of bounds
+    const int copies = fwd_copies<K>(k);
+    float *acc = lds + (threadIdx.x / kWave) * copies * kMaxDim;
     const int64_t w = (int64_t)blockIdx.x * kWavesPerBlock + threadIdx.x / kWave;
     const int64_t q0 = w * run;
     if (q0 >= num_warps) return;
     const int q1 = (int)((q0 + run) < num_warps ? (q0 + run) : num_warps);
-    zero_lds(acc, kMaxDim);
+    zero_lds(acc, copies * kMaxDim);
     const int head_row = q0 > 0 ? warp4[q0 - 1].x : -1;
     const int tail_row = q1 < num_warps ? warp4[q1].x : -1;
     int cur = -1;
@@ -382,8 +426,8 @@ __global__ __launch_bounds__(kBlock) void fwd_warp4_kernel(
         if (ch.x != cur) {
             if (cur >= 0) {
                 float *dst = out + (size_t)cur * dim;
-                if (cur == head_row) flush_atomic(acc, dst, dim);
-                else flush_rmw(acc, dst, dim);
+                if (cur == head_row) flush_row<kAtomic>(acc, copies, dst, dim);
+                else flush_row<kAdd>(acc, copies, dst, dim);
             }
             cur = ch.x;
         }
@@ -391,8 +435,8 @@ __global__ __launch_bounds__(kBlock) void fwd_warp4_kernel(
     }
     if (cur >= 0) {
         float *dst = out + (size_t)cur * dim;
-        if (cur == head_row || cur == tail_row) flush_atomic(acc, dst, dim);
-        else flush_rmw(acc, dst, dim);
+        if (cur == head_row || cur == tail_row) flush_row<kAtomic>(acc, copies, dst, dim);
+        else flush_row<kAdd>(acc, copies, dst, dim);
     }
 }
 
@@ -717,7 +761,10 @@ int dispatch_k(int k, Args &&...args)
     }
 }
 
-size_t fwd_lds_bytes(int dim) { (void)dim; return (size_t)kWavesPerBlock * kMaxDim * sizeof(float); }
+size_t row_lds_bytes() { return (size_t)kWavesPerBlock * kMaxDim * sizeof(float); }
+
+template <int K>
+size_t fwd_lds_bytes(int k) { return (size_t)kWavesPerBlock * fwd_copies<K>(k) * kMaxDim * sizeof(float); }
 
 template <int K>
 struct FwdPanel {
@@ -727,7 +774,7 @@ struct FwdPanel {
     {
         const int64_t blocks = ceil_div(P, kWavesPerBlock);
         hipLaunchKernelGGL(fwd_panel_kernel<K>, dim3((unsigned)blocks), dim3(kBlock),
-                           fwd_lds_bytes(dim), st, reinterpret_cast<const int2 *>(sched), P,
+                           fwd_lds_bytes<K>(k), st, reinterpret_cast<const int2 *>(sched), P,
                            indptr, idx, val, data, sel, V, dim, k, out, carry, carry_row);
         int rc = launch_status();
         if (rc) return rc;
@@ -746,7 +793,7 @@ struct FwdWarp4 {
         const int run = 16;
         const int64_t waves = ceil_div(W, run);
         hipLaunchKernelGGL(fwd_warp4_kernel<K>, dim3((unsigned)ceil_div(waves, kWavesPerBlock)),
-                           dim3(kBlock), fwd_lds_bytes(dim), st,
+                           dim3(kBlock), fwd_lds_bytes<K>(k), st,
                            reinterpret_cast<const int4 *>(warp4), W, run, idx, val, data, sel,
                            dim, k, out);
         return launch_status();
@@ -763,11 +810,11 @@ struct BwdPanel {
         const int64_t blocks = ceil_div(P, kWavesPerBlock);
         if (staged)
             hipLaunchKernelGGL((bwd_panel_kernel<K, true>), dim3((unsigned)blocks), dim3(kBlock),
-                               fwd_lds_bytes(dim), st, reinterpret_cast<const int2 *>(sched), P,
+                               row_lds_bytes(), st, reinterpret_cast<const int2 *>(sched), P,
                                indptr, idx, val, grad, sel, csc_pos, V, dim, k, dxs, Pbuf);
         else
             hipLaunchKernelGGL((bwd_panel_kernel<K, false>), dim3((unsigned)blocks), dim3(kBlock),
-                               fwd_lds_bytes(dim), st, reinterpret_cast<const int2 *>(sched), P,
+                               row_lds_bytes(), st, reinterpret_cast<const int2 *>(sched), P,
                                indptr, idx, val, grad, sel, csc_pos, V, dim, k, dxs, Pbuf);
         return launch_status();
     }
@@ -956,7 +1003,7 @@ int maxk_spmm_backward_warp4(const int32_t *warp4, const int32_t *idx, const flo
     const int run = 16;
     const int64_t waves = ceil_div(num_warps, run);
     hipLaunchKernelGGL(bwd_warp4_kernel, dim3((unsigned)ceil_div(waves, kWavesPerBlock)),
-                       dim3(kBlock), fwd_lds_bytes(feat_in), as_stream(stream),
+                       dim3(kBlock), row_lds_bytes(), as_stream(stream),
                        reinterpret_cast<const int4 *>(warp4), num_warps, run, idx, val, vin_data,
                        vin_selector, feat_in, dim_sparse, vout);
     return launch_status();
