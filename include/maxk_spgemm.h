@@ -92,6 +92,7 @@ int maxk_spgemm_forward(const int32_t *sched, int64_t num_panels, const int32_t 
 #define MAXK_BWD_AUTO 0
 #define MAXK_BWD_ATOMIC 1      /* push + global float atomics (reference's scheme) */
 #define MAXK_BWD_STAGED 2      /* push to per-edge staging rows + CSC segmented sum */
+#define MAXK_BWD_LOCAL 3       /* destination-owned LDS accumulation (maxk_sspmm_backward_local) */
 size_t maxk_backward_workspace_bytes(int algo, int64_t num_edges, int dim_k,
                                      int64_t csc_num_panels);
 int maxk_sspmm_backward(int algo, const int32_t *sched, int64_t num_panels,
@@ -101,6 +102,22 @@ int maxk_sspmm_backward(int algo, const int32_t *sched, int64_t num_panels,
                         const int32_t *csc_pos, const int32_t *csc_sched,
                         int64_t csc_num_panels, const int32_t *csc_indptr,
                         void *workspace, size_t workspace_bytes, void *stream);
+
+/* ---------------------------------------------------------------------------
+ * Backward SSpMM, LOCAL algorithm: destination-owned dXs in LDS, no atomics
+ * and no staging rows.  Needs a plan (built once per graph, ops.py
+ * MaxKGraph.local_plan): destinations split into `num_waves` ranges
+ * wave_dst_start[0..W] (<= dmax <= 256 each); each range's in-edges sorted by
+ * source row, packed as edge_rc = row | (dest - range_start) << 24 and
+ * edge_val, with wave_edge_off[0..W] offsets.  num_rows < 2^24; dim_k must
+ * divide 64; LDS per 4-wave block = maxk_backward_local_lds_bytes(dmax, k)
+ * <= 160 KiB.  Writes every element of dxs.
+ * ------------------------------------------------------------------------- */
+size_t maxk_backward_local_lds_bytes(int dmax, int dim_k);
+int maxk_sspmm_backward_local(const int32_t *wave_edge_off, const int32_t *wave_dst_start,
+                              int num_waves, int dmax, const int32_t *edge_rc,
+                              const float *edge_val, const float *grad, const uint8_t *cbsr_sel,
+                              int num_rows, int dim_origin, int dim_k, float *dxs, void *stream);
 
 /* ---------------------------------------------------------------------------
  * Exact drop-ins for the reference's extern "C" launchers

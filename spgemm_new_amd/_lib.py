@@ -25,6 +25,7 @@ MAXK_E_WORKSPACE = -3
 MAXK_BWD_AUTO = 0
 MAXK_BWD_ATOMIC = 1
 MAXK_BWD_STAGED = 2
+MAXK_BWD_LOCAL = 3
 DEFAULT_PANEL_COST = 2048
 DEFAULT_ROW_COST = 16
 
@@ -46,6 +47,8 @@ SIGNATURES = {
     "maxk_backward_workspace_bytes": (_S, [_I, _L, _I, _L]),
     "maxk_sspmm_backward": (_I, [_I, _P, _L, _P, _P, _P, _P, _P, _I, _L, _I, _I, _P, _P, _P, _L,
                                  _P, _P, _S, _P]),
+    "maxk_backward_local_lds_bytes": (_S, [_I, _I]),
+    "maxk_sspmm_backward_local": (_I, [_P, _P, _I, _I, _P, _P, _P, _P, _I, _I, _I, _P, _P]),
     "maxk_spmm_forward_warp4": (_I, [_P, _P, _P, _P, _P, _P, _I, _I, _I, _I, _I, _P]),
     "maxk_spmm_backward_warp4": (_I, [_P, _P, _P, _P, _P, _P, _I, _I, _I, _I, _I, _P]),
 }

@@ -730,6 +730,100 @@ __global__ __launch_bounds__(kBlock) void bwd_warp4_kernel(
 }
 
 // ---------------------------------------------------------------------------
+// Backward LOCAL: destination-owned accumulation (no atomics, no staging rows)
+//
+// Wave w owns destinations [dstart[w], dstart[w+1]) (D <= 256): their dXs
+// rows and selector rows live in the wave's LDS for the whole kernel.  Its
+// in-edges arrive as a list sorted by SOURCE row r, packed (r | c_local<<24,
+// val) by the plan builder (ops.py).  Every wave sweeps r upward at a similar
+// pace, so the gradient rows G[r] the chip is reading at any moment form a
+// narrow window that each XCD's L2 serves; each G row leaves HBM about once
+// per XCD instead of once per edge.  Per edge the K lanes of a group gather
+// G[r, sel[c, l]] (global, L2) and read-modify-write dXs[c, l] in LDS.
+// EPS = 64/K edges share one wave-instruction; a group whose destinations
+// collide is processed one edge at a time (plain LDS RMW stays race-free).
+// ---------------------------------------------------------------------------
+template <int K>
+__global__ __launch_bounds__(kBlock) void bwd_local_kernel(
+    const int32_t *__restrict__ woff, const int32_t *__restrict__ dstart, int num_waves,
+    int dmax, const int32_t *__restrict__ erc, const float *__restrict__ evl,
+    const float *__restrict__ grad, const uint8_t *__restrict__ sel, int dim,
+    float *__restrict__ dxs)
+{
+    constexpr int EPS = kWave / K;  // edges per wave-instruction
+    constexpr int U = 8;            // groups whose gathers are in flight together
+    extern __shared__ __attribute__((aligned(16))) float lds[];
+    const int wl = threadIdx.x / kWave;
+    const int region = (dmax * K * 5 + 15) & ~15;  // bytes: fp32 dXs block + u8 sel block
+    float *acc = reinterpret_cast<float *>(reinterpret_cast<char *>(lds) + wl * region);
+    uint8_t *sl = reinterpret_cast<uint8_t *>(acc + dmax * K);
+    const int w = blockIdx.x * kWavesPerBlock + wl;
+    if (w >= num_waves) return;
+    const int lane = lane_id();
+    const int d0 = dstart[w], D = dstart[w + 1] - d0;
+    const int nent = D * K;
+    for (int i = lane; i < nent; i += kWave) {
+        acc[i] = 0.f;
+        sl[i] = sel[(size_t)d0 * K + i];
+    }
+    wave_sync_lds();
+    const int grp = lane / K, l = lane % K;
+    const int e_beg = woff[w], e_end = woff[w + 1];
+    for (int base = e_beg; base < e_end; base += kWave) {
+        const int n = (e_end - base) < kWave ? (e_end - base) : kWave;
+        int my_rc = 0;
+        float my_v = 0.f;
+        if (lane < n) {
+            my_rc = __builtin_nontemporal_load(erc + base + lane);
+            my_v = __builtin_nontemporal_load(evl + base + lane);
+        }
+        for (int g0 = 0; g0 < n; g0 += EPS * U) {
+            float gv[U], vv[U];
+            int cc[U];
+#pragma unroll
+            for (int u = 0; u < U; ++u) {
+                const int t = g0 + u * EPS + grp;
+                const int rc = __shfl(my_rc, t < kWave ? t : 0);
+                vv[u] = __shfl(my_v, t < kWave ? t : 0);
+                cc[u] = (rc >> 24) & 0xff;
+                gv[u] = 0.f;
+                if (t < n) {
+                    const int r = rc & 0xffffff;
+                    const int col = sl[cc[u] * K + l];
+                    gv[u] = col < dim ? grad[(size_t)r * dim + col] : 0.f;
+                } else {
+                    vv[u] = 0.f;
+                    cc[u] = -1;
+                }
+            }
+#pragma unroll
+            for (int u = 0; u < U; ++u) {
+                if (g0 + u * EPS >= n) break;
+                bool clash = false;
+                if constexpr (EPS > 1) {
+#pragma unroll
+                    for (int j = 1; j < EPS; ++j) {
+                        const int other = __shfl(cc[u], lane >= j * K ? lane - j * K : lane);
+                        clash |= (lane >= j * K) && other == cc[u] && cc[u] >= 0;
+                    }
+                }
+                if (!__any(clash)) {
+                    if (cc[u] >= 0) acc[cc[u] * K + l] += vv[u] * gv[u];
+                } else {
+                    for (int gg = 0; gg < EPS; ++gg) {
+                        if (grp == gg && cc[u] >= 0) acc[cc[u] * K + l] += vv[u] * gv[u];
+                        wave_sync_lds();
+                    }
+                }
+            }
+        }
+    }
+    wave_sync_lds();
+    float *dst = dxs + (size_t)d0 * K;
+    for (int i = lane; i < nent; i += kWave) dst[i] = acc[i];
+}
+
+// ---------------------------------------------------------------------------
 // Host-side dispatch
 // ---------------------------------------------------------------------------
 inline hipStream_t as_stream(void *s) { return reinterpret_cast<hipStream_t>(s); }
@@ -833,6 +927,20 @@ struct BwdSegsum {
         if (rc) return rc;
         hipLaunchKernelGGL(carry_fixup_kernel, dim3((unsigned)blocks), dim3(kBlock), 0, st, CP,
                            carry, carry_row, dxs, k, k);
+        return launch_status();
+    }
+};
+
+template <int K>
+struct BwdLocal {
+    static int run(const int32_t *woff, const int32_t *dstart, int W, int dmax, const int32_t *erc,
+                   const float *evl, const float *grad, const uint8_t *sel, int dim, float *dxs,
+                   hipStream_t st)
+    {
+        const size_t region = (size_t)((dmax * K * 5 + 15) & ~15);
+        hipLaunchKernelGGL(bwd_local_kernel<K>, dim3((unsigned)ceil_div(W, kWavesPerBlock)),
+                           dim3(kBlock), region * kWavesPerBlock, st, woff, dstart, W, dmax, erc,
+                           evl, grad, sel, dim, dxs);
         return launch_status();
     }
 };
@@ -974,6 +1082,34 @@ int maxk_sspmm_backward(int algo, const int32_t *sched, int64_t num_panels,
     if (rc) return rc;
     return dispatch_k<BwdSegsum>(dim_k, csc_sched, csc_num_panels, csc_indptr, Pbuf, num_rows,
                                  dim_k, dxs, carry, carry_row, st);
+}
+
+size_t maxk_backward_local_lds_bytes(int dmax, int dim_k)
+{
+    return (size_t)kWavesPerBlock * (size_t)((dmax * dim_k * 5 + 15) & ~15);
+}
+
+int maxk_sspmm_backward_local(const int32_t *wave_edge_off, const int32_t *wave_dst_start,
+                              int num_waves, int dmax, const int32_t *edge_rc,
+                              const float *edge_val, const float *grad, const uint8_t *cbsr_sel,
+                              int num_rows, int dim_origin, int dim_k, float *dxs, void *stream)
+{
+    if (!wave_edge_off || !wave_dst_start || !dxs || num_waves < 1 || num_rows < 1 ||
+        num_rows >= (1 << 24) || dmax < 1 || dmax > 256)
+        return MAXK_E_ARG;
+    if (!dims_ok(dim_origin, dim_k) || (kWave % dim_k) != 0) return MAXK_E_DIM;
+    if (!edge_rc || !edge_val || !grad || !cbsr_sel) return MAXK_E_ARG;
+    if (maxk_backward_local_lds_bytes(dmax, dim_k) > 160 * 1024) return MAXK_E_WORKSPACE;
+    hipStream_t st = as_stream(stream);
+    switch (dim_k) {
+    case 1: return BwdLocal<1>::run(wave_edge_off, wave_dst_start, num_waves, dmax, edge_rc, edge_val, grad, cbsr_sel, dim_origin, dxs, st);
+    case 2: return BwdLocal<2>::run(wave_edge_off, wave_dst_start, num_waves, dmax, edge_rc, edge_val, grad, cbsr_sel, dim_origin, dxs, st);
+    case 4: return BwdLocal<4>::run(wave_edge_off, wave_dst_start, num_waves, dmax, edge_rc, edge_val, grad, cbsr_sel, dim_origin, dxs, st);
+    case 8: return BwdLocal<8>::run(wave_edge_off, wave_dst_start, num_waves, dmax, edge_rc, edge_val, grad, cbsr_sel, dim_origin, dxs, st);
+    case 16: return BwdLocal<16>::run(wave_edge_off, wave_dst_start, num_waves, dmax, edge_rc, edge_val, grad, cbsr_sel, dim_origin, dxs, st);
+    case 32: return BwdLocal<32>::run(wave_edge_off, wave_dst_start, num_waves, dmax, edge_rc, edge_val, grad, cbsr_sel, dim_origin, dxs, st);
+    default: return BwdLocal<64>::run(wave_edge_off, wave_dst_start, num_waves, dmax, edge_rc, edge_val, grad, cbsr_sel, dim_origin, dxs, st);
+    }
 }
 
 int maxk_spmm_forward_warp4(const int32_t *warp4, const int32_t *idx, const float *val,

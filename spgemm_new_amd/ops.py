@@ -41,6 +41,14 @@ def _stream(t):
     return _lib.stream_ptr(t.device)
 
 
+def _tensor_key(t):
+    return (t.data_ptr(), t.numel(), t._version)
+
+
+# LOCAL backward: target LDS bytes per wave (8 waves per CU share 160 KiB)
+LOCAL_WAVE_LDS_BYTES = 20 * 1024
+
+
 def _build_schedule(indptr: torch.Tensor, num_rows: int, num_edges: int, panel_cost: int,
                     row_cost: int):
     L = _lib.load()
@@ -93,6 +101,7 @@ class MaxKGraph:
             self.bwd_sched, self.bwd_num_panels = self.sched, self.num_panels
         self.csc_panel_cost = csc_panel_cost or panel_cost
         self._csc = None
+        self._local = {}
         self._ws = {}
 
     # ------------------------------------------------------------------ utils
@@ -117,6 +126,57 @@ class MaxKGraph:
                                        self.csc_panel_cost, self.row_cost)
             self._csc = (csc_pos, csc_indptr, sched, P)
         return self._csc
+
+    def local_plan(self, dim_k: int):
+        """Plan of the LOCAL backward (maxk_sspmm_backward_local), or None when
+        the shape does not suit it.  Destinations are cut into ranges of at
+        most dmax nodes balanced by in-degree; each range's in-edges are listed
+        in source-row order (stable sort of the CSR edges by owner range)."""
+        if dim_k in self._local:
+            plan = self._local[dim_k]
+            if plan is not None and plan["values_key"] != _tensor_key(self.values):
+                plan["edge_val"] = self.values[: self.num_edges][plan["perm"].long()].contiguous()
+                plan["values_key"] = _tensor_key(self.values)
+            return plan
+        plan = None
+        V, E = self.num_rows, self.num_edges
+        if E > 0 and V < (1 << 24) and 64 % dim_k == 0:
+            dmax = max(1, min(256, LOCAL_WAVE_LDS_BYTES // (5 * dim_k)))
+            _, csc_indptr, _, _ = self.csc()
+            w_min = -(-V // dmax)
+            tgt = torch.linspace(0, E, w_min + 1, device=self.device, dtype=torch.float64)
+            cut_e = torch.searchsorted(csc_indptr.double(), tgt, right=False).clamp_(0, V)
+            cut_d = torch.arange(0, V, dmax, device=self.device)
+            cuts = torch.unique(torch.cat([cut_e, cut_d, torch.tensor([0, V], device=self.device)]))
+            dstart = cuts.to(torch.int32).contiguous()
+            W = dstart.numel() - 1
+            idx = self.indices[:E].long()
+            owner = torch.searchsorted(dstart, self.indices[:E], right=True) - 1
+            rows = torch.repeat_interleave(torch.arange(V, device=self.device),
+                                           (self.indptr[1:] - self.indptr[:-1]).long())
+            perm = torch.argsort(owner, stable=True)
+            erc = (rows[perm] | ((idx[perm] - dstart.long()[owner[perm]]) << 24)).to(torch.int32)
+            woff = torch.zeros(W + 1, dtype=torch.int32, device=self.device)
+            woff[1:] = torch.cumsum(torch.bincount(owner, minlength=W), 0).to(torch.int32)
+            perm32 = perm.to(torch.int32)
+            del rows, owner, idx, perm
+            plan = {"dmax": dmax, "num_waves": W, "dstart": dstart, "woff": woff,
+                    "edge_rc": erc.contiguous(), "perm": perm32,
+                    "edge_val": self.values[:E][perm32.long()].contiguous(),
+                    "values_key": _tensor_key(self.values)}
+        self._local[dim_k] = plan
+        return plan
+
+    def local_fits(self, dim_k: int) -> bool:
+        """True when the LOCAL plan's waves are all co-resident (one sweep of G)."""
+        plan = self.local_plan(dim_k)
+        if plan is None:
+            return False
+        cus = torch.cuda.get_device_properties(self.device).multi_processor_count
+        L = _lib.load()
+        per_block = L.maxk_backward_local_lds_bytes(plan["dmax"], dim_k)
+        blocks_per_cu = max(1, (160 * 1024) // max(per_block, 1))
+        return plan["num_waves"] <= cus * blocks_per_cu * 4
 
     def nbytes_fwd(self, dim_k: int, dim_origin: int) -> int:
         """Algorithmic bytes of one forward call: 8E + 5kE + 4hV."""
@@ -184,10 +244,23 @@ def sspmm_backward(g: MaxKGraph, grad, sel, out=None, values=None, algo: int = _
         if tuple(out.shape) != (g.num_rows, k):
             raise RuntimeError("grad_input has the wrong shape")
     if algo == _lib.MAXK_BWD_AUTO:
-        algo = _lib.MAXK_BWD_STAGED
+        algo = _lib.MAXK_BWD_LOCAL if (values is g.values and g.local_fits(k)) else \
+            _lib.MAXK_BWD_STAGED
     if g.num_edges == 0:
         algo = _lib.MAXK_BWD_ATOMIC  # nothing to stage: the call just zeroes dXs
     L = _lib.load()
+    if algo == _lib.MAXK_BWD_LOCAL:
+        if values is not g.values:
+            raise RuntimeError("the LOCAL backward bakes the graph's edge values into its plan")
+        plan = g.local_plan(k)
+        if plan is None:
+            raise RuntimeError("LOCAL backward unsupported for this shape (k must divide 64)")
+        _lib.check(L.maxk_sspmm_backward_local(
+            plan["woff"].data_ptr(), plan["dstart"].data_ptr(), plan["num_waves"], plan["dmax"],
+            plan["edge_rc"].data_ptr(), plan["edge_val"].data_ptr(), grad.data_ptr(),
+            sel.data_ptr(), g.num_rows, dim_origin, k, out.data_ptr(), _stream(out)),
+            "maxk_sspmm_backward_local")
+        return out
     csc_pos = csc_indptr = csc_sched = None
     CP = 0
     ws = None

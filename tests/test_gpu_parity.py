@@ -65,11 +65,13 @@ def test_forward_overwrites_output(dev, oracle, g_small):
 
 
 # ---------------------------------------------------------------- backward
-@pytest.mark.parametrize("algo", [_lib.MAXK_BWD_ATOMIC, _lib.MAXK_BWD_STAGED])
+@pytest.mark.parametrize("algo", [_lib.MAXK_BWD_ATOMIC, _lib.MAXK_BWD_STAGED, _lib.MAXK_BWD_LOCAL])
 @pytest.mark.parametrize("k,h", [(32, 256), (8, 256), (16, 256), (64, 256), (4, 256),
                                  (128, 256), (5, 256), (24, 256), (16, 64), (8, 100)])
 def test_backward(dev, oracle, g_small, algo, k, h):
     indptr, indices, values = g_small
+    if algo == _lib.MAXK_BWD_LOCAL and 64 % k:
+        pytest.skip("LOCAL needs k | 64")
     v = len(indptr) - 1
     _, sel = random_cbsr(v, k, h, seed=50 + k)
     grad = np.random.default_rng(k).random((v, h), dtype=np.float32)
@@ -154,7 +156,7 @@ def _edge_graph(kind):
 
 
 @pytest.mark.parametrize("kind", ["empty_rows", "single_row_hub", "one_node", "last_row_only"])
-@pytest.mark.parametrize("algo", [_lib.MAXK_BWD_ATOMIC, _lib.MAXK_BWD_STAGED])
+@pytest.mark.parametrize("algo", [_lib.MAXK_BWD_ATOMIC, _lib.MAXK_BWD_STAGED, _lib.MAXK_BWD_LOCAL])
 def test_edge_cases(dev, oracle, kind, algo):
     indptr, indices = _edge_graph(kind)
     v, e = len(indptr) - 1, len(indices)
@@ -170,6 +172,36 @@ def test_edge_cases(dev, oracle, kind, algo):
     dx = g.backward(T(grad, dev), T(sel, dev), algo=algo)
     assert oracle.parity_error(dx.cpu().numpy(),
                                oracle.np_backward(indptr, indices, values, grad, sel)) <= TOL
+
+
+@pytest.mark.parametrize("k", [8, 16, 32, 64])
+@pytest.mark.parametrize("wave_lds", [5 * 64 * 3, 20 * 1024])
+def test_backward_local_collisions(dev, oracle, monkeypatch, k, wave_lds):
+    """Tiny destination ranges (dmax = 1..3) make same-destination edges share a
+    wave-instruction all the time (the serialised path); a hub column adds more."""
+    from spgemm_new_amd import ops
+    monkeypatch.setattr(ops, "LOCAL_WAVE_LDS_BYTES", wave_lds)
+    indptr, indices = small_csr(1200, seed=33)
+    v = len(indptr) - 1
+    indices = indices.copy()
+    indices[::3] = 7                                    # hub destination
+    rows = np.repeat(np.arange(v), np.diff(indptr))
+    order = np.lexsort((indices, rows))
+    indices = indices[order]
+    keep = np.ones(len(indices), bool)                  # drop duplicates within a row
+    keep[1:] = ~((rows[order][1:] == rows[order][:-1]) & (indices[1:] == indices[:-1]))
+    rows, indices = rows[order][keep], indices[keep]
+    indptr = np.zeros(v + 1, np.int32)
+    indptr[1:] = np.cumsum(np.bincount(rows, minlength=v))
+    values = np.random.default_rng(k).random(len(indices), dtype=np.float32)
+    _, sel = random_cbsr(v, k, 256, seed=k)
+    grad = np.random.default_rng(1).random((v, 256), dtype=np.float32)
+    g = S.MaxKGraph(T(indptr, dev), T(indices.astype(np.int32), dev), T(values, dev))
+    plan = g.local_plan(k)
+    assert plan["dmax"] == max(1, min(256, wave_lds // (5 * k)))
+    dx = g.backward(T(grad, dev), T(sel, dev), algo=_lib.MAXK_BWD_LOCAL)
+    ref = oracle.np_backward(indptr, indices, values, grad, sel)
+    assert oracle.parity_error(dx.cpu().numpy(), ref) <= TOL
 
 
 def test_offset_csr_view(dev, oracle, g_small):
