@@ -37,7 +37,7 @@ def parse():
     p.add_argument("--k", type=int, default=32)
     p.add_argument("--h", type=int, default=256)
     p.add_argument("--seed", type=int, default=123)
-    p.add_argument("--bwd-algo", default="auto", choices=["auto", "atomic", "staged"])
+    p.add_argument("--bwd-algo", default="auto", choices=["auto", "atomic", "staged", "local"])
     p.add_argument("--panel-cost", type=int, default=None)
     p.add_argument("--row-cost", type=int, default=None)
     p.add_argument("--no-cpu-baseline", action="store_true")
@@ -141,7 +141,7 @@ def main():
     log(f"[bench] graph {args.graph} V={V} E={E} built in {time.time() - t0:.1f}s")
 
     algo = {"auto": _lib.MAXK_BWD_AUTO, "atomic": _lib.MAXK_BWD_ATOMIC,
-            "staged": _lib.MAXK_BWD_STAGED}[args.bwd_algo]
+            "staged": _lib.MAXK_BWD_STAGED, "local": _lib.MAXK_BWD_LOCAL}[args.bwd_algo]
     kw = {}
     if args.panel_cost:
         kw["panel_cost"] = args.panel_cost
@@ -230,6 +230,7 @@ def main():
                               "unit": "GB/s", "frac": round(ach / HBM_PEAK_GBS, 4),
                               "traffic": None, "kernel": dom[0],
                               "algorithmic_bytes_per_launch": b_call}
+        result["config"]["bwd_algo"] = g.last_bwd_algo
         result["fwd_ms"] = round(fms, 4)
         result["bwd_ms"] = round(bms, 4)
         result["fwd_GBs"] = round(b_call / fms / 1e6, 1)

@@ -750,8 +750,9 @@ __global__ __launch_bounds__(kBlock) void bwd_local_kernel(
     const float *__restrict__ grad, const uint8_t *__restrict__ sel, int dim,
     float *__restrict__ dxs)
 {
-    constexpr int EPS = kWave / K;  // edges per wave-instruction
-    constexpr int U = 8;            // groups whose gathers are in flight together
+    constexpr int EPS = kWave / K;                 // edges per wave-instruction
+    constexpr int B = EPS * 32 < kWave ? EPS * 32 : kWave;  // edges per batch
+    constexpr int NG = B / EPS;                    // groups per batch (<= 32)
     extern __shared__ __attribute__((aligned(16))) float lds[];
     const int wl = threadIdx.x / kWave;
     const int region = (dmax * K * 5 + 15) & ~15;  // bytes: fp32 dXs block + u8 sel block
@@ -769,51 +770,72 @@ __global__ __launch_bounds__(kBlock) void bwd_local_kernel(
     wave_sync_lds();
     const int grp = lane / K, l = lane % K;
     const int e_beg = woff[w], e_end = woff[w + 1];
-    for (int base = e_beg; base < e_end; base += kWave) {
-        const int n = (e_end - base) < kWave ? (e_end - base) : kWave;
-        int my_rc = 0;
-        float my_v = 0.f;
-        if (lane < n) {
-            my_rc = __builtin_nontemporal_load(erc + base + lane);
-            my_v = __builtin_nontemporal_load(evl + base + lane);
+    // records of the next batch are prefetched while the current one gathers
+    int nx_rc = 0;
+    float nx_v = 0.f;
+    if (lane < B && e_beg + lane < e_end) {
+        nx_rc = __builtin_nontemporal_load(erc + e_beg + lane);
+        nx_v = __builtin_nontemporal_load(evl + e_beg + lane);
+    }
+    for (int base = e_beg; base < e_end; base += B) {
+        const int n = (e_end - base) < B ? (e_end - base) : B;
+        const int my_rc = nx_rc;
+        const float my_v = nx_v;
+        if (lane < B && base + B + lane < e_end) {
+            nx_rc = __builtin_nontemporal_load(erc + base + B + lane);
+            nx_v = __builtin_nontemporal_load(evl + base + B + lane);
         }
-        for (int g0 = 0; g0 < n; g0 += EPS * U) {
-            float gv[U], vv[U];
-            int cc[U];
+        float gv[NG], vv[NG];
+        int cc[NG];
+        uint32_t clash = 0;  // bit u: group u has two edges into one destination
 #pragma unroll
-            for (int u = 0; u < U; ++u) {
-                const int t = g0 + u * EPS + grp;
-                const int rc = __shfl(my_rc, t < kWave ? t : 0);
-                vv[u] = __shfl(my_v, t < kWave ? t : 0);
-                cc[u] = (rc >> 24) & 0xff;
-                gv[u] = 0.f;
-                if (t < n) {
-                    const int r = rc & 0xffffff;
-                    const int col = sl[cc[u] * K + l];
-                    gv[u] = col < dim ? grad[(size_t)r * dim + col] : 0.f;
-                } else {
-                    vv[u] = 0.f;
-                    cc[u] = -1;
+        for (int u = 0; u < NG; ++u) {
+            const int t = u * EPS + grp;
+            int rc;
+            if constexpr (EPS == 1) {
+                rc = __builtin_amdgcn_readlane(my_rc, u);
+                vv[u] = __builtin_bit_cast(float, __builtin_amdgcn_readlane(
+                    __builtin_bit_cast(int, my_v), u));
+            } else if constexpr (EPS == 2) {
+                const int ra = __builtin_amdgcn_readlane(my_rc, 2 * u);
+                const int rb = __builtin_amdgcn_readlane(my_rc, 2 * u + 1);
+                const float va = __builtin_bit_cast(float, __builtin_amdgcn_readlane(
+                    __builtin_bit_cast(int, my_v), 2 * u));
+                const float vb = __builtin_bit_cast(float, __builtin_amdgcn_readlane(
+                    __builtin_bit_cast(int, my_v), 2 * u + 1));
+                rc = grp ? rb : ra;
+                vv[u] = grp ? vb : va;
+                if ((2 * u + 1 < n) && ((ra >> 24) == (rb >> 24))) clash |= 1u << u;
+            } else {
+                rc = __shfl(my_rc, t);
+                vv[u] = __shfl(my_v, t);
+                bool c = false;
+#pragma unroll
+                for (int j = 1; j < EPS; ++j) {
+                    const int other = __shfl(rc, lane >= j * K ? lane - j * K : lane);
+                    c |= (lane >= j * K) && ((other >> 24) == (rc >> 24)) && (t < n);
                 }
+                if (__any(c)) clash |= 1u << u;
             }
+            cc[u] = (rc >> 24) & 0xff;
+            gv[u] = 0.f;
+            if (t < n) {
+                const int col = sl[cc[u] * K + l];
+                gv[u] = col < dim ? grad[(size_t)(rc & 0xffffff) * dim + col] : 0.f;
+            } else {
+                vv[u] = 0.f;
+                cc[u] = -1;
+            }
+        }
 #pragma unroll
-            for (int u = 0; u < U; ++u) {
-                if (g0 + u * EPS >= n) break;
-                bool clash = false;
-                if constexpr (EPS > 1) {
-#pragma unroll
-                    for (int j = 1; j < EPS; ++j) {
-                        const int other = __shfl(cc[u], lane >= j * K ? lane - j * K : lane);
-                        clash |= (lane >= j * K) && other == cc[u] && cc[u] >= 0;
-                    }
-                }
-                if (!__any(clash)) {
-                    if (cc[u] >= 0) acc[cc[u] * K + l] += vv[u] * gv[u];
-                } else {
-                    for (int gg = 0; gg < EPS; ++gg) {
-                        if (grp == gg && cc[u] >= 0) acc[cc[u] * K + l] += vv[u] * gv[u];
-                        wave_sync_lds();
-                    }
+        for (int u = 0; u < NG; ++u) {
+            if (u * EPS >= n) break;
+            if (!((clash >> u) & 1u)) {
+                if (cc[u] >= 0) acc[cc[u] * K + l] += vv[u] * gv[u];
+            } else {
+                for (int gg = 0; gg < EPS; ++gg) {
+                    if (grp == gg && cc[u] >= 0) acc[cc[u] * K + l] += vv[u] * gv[u];
+                    wave_sync_lds();
                 }
             }
         }

@@ -47,6 +47,7 @@ def _tensor_key(t):
 
 # LOCAL backward: target LDS bytes per wave (8 waves per CU share 160 KiB)
 LOCAL_WAVE_LDS_BYTES = 20 * 1024
+LOCAL_WAVES_PER_CU = 8
 
 
 def _build_schedule(indptr: torch.Tensor, num_rows: int, num_edges: int, panel_cost: int,
@@ -103,6 +104,7 @@ class MaxKGraph:
         self._csc = None
         self._local = {}
         self._ws = {}
+        self.last_bwd_algo = None
 
     # ------------------------------------------------------------------ utils
     def _workspace(self, key, nbytes: int) -> torch.Tensor:
@@ -143,11 +145,20 @@ class MaxKGraph:
         if E > 0 and V < (1 << 24) and 64 % dim_k == 0:
             dmax = max(1, min(256, LOCAL_WAVE_LDS_BYTES // (5 * dim_k)))
             _, csc_indptr, _, _ = self.csc()
-            w_min = -(-V // dmax)
-            tgt = torch.linspace(0, E, w_min + 1, device=self.device, dtype=torch.float64)
-            cut_e = torch.searchsorted(csc_indptr.double(), tgt, right=False).clamp_(0, V)
-            cut_d = torch.arange(0, V, dmax, device=self.device)
-            cuts = torch.unique(torch.cat([cut_e, cut_d, torch.tensor([0, V], device=self.device)]))
+            cus = torch.cuda.get_device_properties(self.device).multi_processor_count
+            w_tgt = max(-(-V // dmax), min(cus * LOCAL_WAVES_PER_CU, V))
+            tgt = torch.linspace(0, E, w_tgt + 1, device=self.device, dtype=torch.float64)
+            cuts = torch.searchsorted(csc_indptr.double(), tgt, right=False).clamp_(0, V)
+            cuts[0], cuts[-1] = 0, V
+            cuts = torch.unique(cuts)
+            # split ranges longer than dmax (hub-free but wide stretches of low in-degree)
+            span = cuts[1:] - cuts[:-1]
+            extra = (span - 1) // dmax
+            if int(extra.sum()) > 0:
+                base = torch.repeat_interleave(cuts[:-1], extra)
+                step = torch.arange(int(extra.sum()), device=self.device) - \
+                    torch.repeat_interleave(torch.cumsum(extra, 0) - extra, extra)
+                cuts = torch.unique(torch.cat([cuts, base + (step + 1) * dmax]))
             dstart = cuts.to(torch.int32).contiguous()
             W = dstart.numel() - 1
             idx = self.indices[:E].long()
@@ -244,8 +255,9 @@ def sspmm_backward(g: MaxKGraph, grad, sel, out=None, values=None, algo: int = _
         if tuple(out.shape) != (g.num_rows, k):
             raise RuntimeError("grad_input has the wrong shape")
     if algo == _lib.MAXK_BWD_AUTO:
-        algo = _lib.MAXK_BWD_LOCAL if (values is g.values and g.local_fits(k)) else \
-            _lib.MAXK_BWD_STAGED
+        # measured on MI355X (DESIGN.md "Backward"): STAGED is fastest on the
+        # Reddit/products shapes; LOCAL is L2-request-bound there.
+        algo = _lib.MAXK_BWD_STAGED
     if g.num_edges == 0:
         algo = _lib.MAXK_BWD_ATOMIC  # nothing to stage: the call just zeroes dXs
     L = _lib.load()
@@ -255,6 +267,7 @@ def sspmm_backward(g: MaxKGraph, grad, sel, out=None, values=None, algo: int = _
         plan = g.local_plan(k)
         if plan is None:
             raise RuntimeError("LOCAL backward unsupported for this shape (k must divide 64)")
+        g.last_bwd_algo = "local"
         _lib.check(L.maxk_sspmm_backward_local(
             plan["woff"].data_ptr(), plan["dstart"].data_ptr(), plan["num_waves"], plan["dmax"],
             plan["edge_rc"].data_ptr(), plan["edge_val"].data_ptr(), grad.data_ptr(),
@@ -268,6 +281,7 @@ def sspmm_backward(g: MaxKGraph, grad, sel, out=None, values=None, algo: int = _
         csc_pos, csc_indptr, csc_sched, CP = g.csc()
         nbytes = L.maxk_backward_workspace_bytes(algo, g.num_edges, k, CP)
         ws = g._workspace(("bwd", k), nbytes)
+    g.last_bwd_algo = {_lib.MAXK_BWD_ATOMIC: "atomic", _lib.MAXK_BWD_STAGED: "staged"}[algo]
     _lib.check(L.maxk_sspmm_backward(
         algo, g.bwd_sched.data_ptr(), g.bwd_num_panels, g.indptr.data_ptr(), g.indices.data_ptr(),
         values.data_ptr(), grad.data_ptr(), sel.data_ptr(), g.num_rows, g.num_edges, dim_origin, k,

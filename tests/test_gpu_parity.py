@@ -128,7 +128,7 @@ def test_main_cu_inputs(dev, oracle):
     assert oracle.parity_error(y.cpu().numpy(),
                                oracle.c_forward(w4, indices, values, data, sel, 256)) <= TOL
     # main.cu:103 times the backward with vin = the densified sparse input
-    for algo in (_lib.MAXK_BWD_ATOMIC, _lib.MAXK_BWD_STAGED):
+    for algo in (_lib.MAXK_BWD_ATOMIC, _lib.MAXK_BWD_STAGED, _lib.MAXK_BWD_LOCAL):
         dx = g.backward(T(dense, dev), T(sel, dev), algo=algo)
         assert oracle.parity_error(dx.cpu().numpy(),
                                    oracle.c_backward(w4, indices, values, dense, sel)) <= TOL

@@ -31,7 +31,8 @@ __global__ __launch_bounds__(256) void phase1(const int2 *__restrict__ panels, i
                                               const int *__restrict__ csc_pos,
                                               const float *__restrict__ G,
                                               const unsigned char *__restrict__ sel,
-                                              float *__restrict__ Pbuf, float *__restrict__ dxs)
+                                              float *__restrict__ Pbuf, float *__restrict__ dxs,
+                                              int split = 0)
 {
     __shared__ __attribute__((aligned(16))) float lds[4 * 256];
     const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
@@ -47,7 +48,7 @@ __global__ __launch_bounds__(256) void phase1(const int2 *__restrict__ panels, i
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
         __builtin_amdgcn_wave_barrier();
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-        if constexpr (MODE == 9) {   // atomic push, one entry per lane
+        if (MODE == 9 || (MODE == 10 && w < split)) {   // atomic push, one entry per lane
             constexpr int EPS = 64 / K;
             const int slot = lane / K, l = lane % K;
             for (int base = e0; base < e1; base += 64) {
@@ -80,7 +81,8 @@ __global__ __launch_bounds__(256) void phase1(const int2 *__restrict__ panels, i
                     for (int u = 0; u < U; ++u) {
                         const int t = (s0 + u) * EPS + slot;
                         const int c = __shfl(my_c, t < 64 ? t : 0);
-                        sb[u] = t < n ? *reinterpret_cast<const unsigned *>(sel + (size_t)c * K + sub * 4) : 0u;
+                        if constexpr (MODE == 4) sb[u] = (unsigned)c;
+                        else sb[u] = t < n ? *reinterpret_cast<const unsigned *>(sel + (size_t)c * K + sub * 4) : 0u;
                     }
 #pragma unroll
                     for (int u = 0; u < U; ++u) {
@@ -89,7 +91,7 @@ __global__ __launch_bounds__(256) void phase1(const int2 *__restrict__ panels, i
                         const float v = __shfl(my_v, t < 64 ? t : 0);
                         if (t < n) {
                             f4 o;
-                            if constexpr (MODE == 3) {
+                            if constexpr (MODE == 3 || MODE == 4) {
                                 o = f4{v, v * (float)(sb[u] & 255), v, v};
                             } else {
                                 o.x = v * gs[sb[u] & 0xff];
@@ -98,7 +100,7 @@ __global__ __launch_bounds__(256) void phase1(const int2 *__restrict__ panels, i
                                 o.w = v * gs[sb[u] >> 24];
                             }
                             f4 *dst = reinterpret_cast<f4 *>(Pbuf + (size_t)p * K + sub * 4);
-                            if constexpr (MODE == 0 || MODE == 3) __builtin_nontemporal_store(o, dst);
+                            if constexpr (MODE == 0 || MODE == 3 || MODE == 4 || MODE == 10) __builtin_nontemporal_store(o, dst);
                             else *dst = o;
                         }
                     }
@@ -227,6 +229,16 @@ void sweep(int V, const std::vector<int> &indptr, const std::vector<int> &idx, i
         hipLaunchKernelGGL((phase1<K, 9>), g1, b, 0, 0, d_p1, P1, d_ptr, d_idx, d_val, d_cpos, d_G, d_sel, d_P, d_dxs);
     }, reps);
     float q0 = P2RUN(0), q1 = P2RUN(1);
+    float t4 = P1RUN(4);
+    for (float f : {0.2f, 0.3f, 0.4f, 0.5f}) {
+        const int split = (int)(P1 * f);
+        float th = timeit([&] {
+            CK(hipMemsetAsync(d_dxs, 0, (size_t)V * K * 4));
+            hipLaunchKernelGGL((phase1<K, 10>), g1, b, 0, 0, d_p1, P1, d_ptr, d_idx, d_val, d_cpos, d_G, d_sel, d_P, d_dxs, split);
+        }, reps);
+        printf("   hybrid f=%.1f phase1 %.3f ms (+ phase2 ~%.3f) = %.3f ms\n", f, th, q0 * (1 - f), th + q0 * (1 - f));
+    }
+    printf("   p4 (pure scattered write, no sel gather, no LDS) %.3f ms\n", t4);
     printf("K=%d E=%lld  p0(nt scat) %.3f  p1(plain scat) %.3f  p2(seq) %.3f  p3(noLDS) %.3f  | q0(seq) %.3f  q1(gather) %.3f | atomic %.3f ms\n",
            K, E, t0, t1, t2, t3, q0, q1, tA);
     printf("   staged best: scat %.3f ms (%.0f GB/s), seq+gather %.3f ms (%.0f GB/s), atomic %.0f GB/s\n",
