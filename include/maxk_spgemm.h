@@ -18,13 +18,14 @@
  *    no host synchronisation, so calls can be captured into a hipGraph.
  *  - Return value: 0 on success; a negative MAXK_E* code for an invalid
  *    argument (nothing launched); a positive hipError_t for a launch failure.
- *  - Layouts (row-major, contiguous):
- *      CSR    indptr int32[V+1] (indptr[0] may be non-zero), indices int32[E],
- *             values fp32[E]
- *      CBSR   cbsr_data fp32[V,k], cbsr_sel uint8[V,k]  (k distinct columns
- *             < dim_origin per row; the selector is a uint8, so
+ *  - Layouts (row-major, contiguous).  A is num_rows x num_cols (square in
+ *    the single-GPU case; a row block with halo columns on a multi-GPU rank):
+ *      CSR    indptr int32[num_rows+1] (indptr[0] may be non-zero),
+ *             indices int32[E] (< num_cols), values fp32[E]
+ *      CBSR   cbsr_data fp32[num_cols,k], cbsr_sel uint8[num_cols,k] (k distinct
+ *             columns < dim_origin per row; the selector is a uint8, so
  *             dim_origin <= 256, as in the reference, spmm_maxk.cu:17)
- *      dense  out / grad fp32[V,dim_origin];  dxs fp32[V,k]
+ *      dense  out / grad fp32[num_rows,dim_origin];  dxs fp32[num_cols,k]
  */
 #ifndef MAXK_SPGEMM_H
 #define MAXK_SPGEMM_H
@@ -98,7 +99,7 @@ size_t maxk_backward_workspace_bytes(int algo, int64_t num_edges, int dim_k,
 int maxk_sspmm_backward(int algo, const int32_t *sched, int64_t num_panels,
                         const int32_t *indptr, const int32_t *indices, const float *values,
                         const float *grad, const uint8_t *cbsr_sel, int num_rows,
-                        int64_t num_edges, int dim_origin, int dim_k, float *dxs,
+                        int num_cols, int64_t num_edges, int dim_origin, int dim_k, float *dxs,
                         const int32_t *csc_pos, const int32_t *csc_sched,
                         int64_t csc_num_panels, const int32_t *csc_indptr,
                         void *workspace, size_t workspace_bytes, void *stream);

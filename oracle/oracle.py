@@ -193,7 +193,7 @@ def np_backward(indptr, indices, values, grad, sel) -> np.ndarray:
     v = len(indptr) - 1
     rows = np.repeat(np.arange(v), np.diff(indptr))
     cols = np.asarray(indices, dtype=np.int64)
-    agt = np.zeros((v, grad.shape[1]), dtype=np.float64)          # A^T G
+    agt = np.zeros((sel.shape[0], grad.shape[1]), dtype=np.float64)   # A^T G (A may be v x C)
     np.add.at(agt, cols, np.asarray(values, np.float64)[:, None] * np.asarray(grad, np.float64)[rows])
     return np.take_along_axis(agt, sel.astype(np.int64), axis=1)
 

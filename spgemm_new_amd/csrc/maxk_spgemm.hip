@@ -52,11 +52,6 @@ __device__ __forceinline__ void wave_sync_lds()
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 }
 
-__device__ __forceinline__ void lds_add(float *p, float v)
-{
-    __hip_atomic_fetch_add(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
-}
-
 __device__ __forceinline__ void gbl_add(float *p, float v)
 {
     // no-return global_atomic_add_f32 (agent scope: adders may sit on any XCD)
@@ -1068,21 +1063,27 @@ size_t maxk_backward_workspace_bytes(int algo, int64_t num_edges, int dim_k,
 int maxk_sspmm_backward(int algo, const int32_t *sched, int64_t num_panels,
                         const int32_t *indptr, const int32_t *indices, const float *values,
                         const float *grad, const uint8_t *cbsr_sel, int num_rows,
-                        int64_t num_edges, int dim_origin, int dim_k, float *dxs,
+                        int num_cols, int64_t num_edges, int dim_origin, int dim_k, float *dxs,
                         const int32_t *csc_pos, const int32_t *csc_sched,
                         int64_t csc_num_panels, const int32_t *csc_indptr, void *workspace,
                         size_t workspace_bytes, void *stream)
 {
-    if (!sched || !indptr || !dxs || num_panels < 1 || num_rows < 0) return MAXK_E_ARG;
+    if (!sched || !indptr || !dxs || num_panels < 1 || num_rows < 0 || num_cols < 0 ||
+        num_edges < 0)
+        return MAXK_E_ARG;
     if (!dims_ok(dim_origin, dim_k)) return MAXK_E_DIM;
     hipStream_t st = as_stream(stream);
-    if (num_rows == 0) return MAXK_OK;
+    if (num_cols == 0) return MAXK_OK;
+    if (num_rows == 0 || num_edges == 0) {  // no edge: dXs = 0
+        hipError_t e = hipMemsetAsync(dxs, 0, (size_t)num_cols * dim_k * sizeof(float), st);
+        return e == hipSuccess ? MAXK_OK : (int)e;
+    }
     if (!indices || !values || !grad || !cbsr_sel) return MAXK_E_ARG;
     const bool staged_ready = csc_pos && csc_sched && csc_indptr && csc_num_panels >= 1 &&
                               workspace;
     if (algo == MAXK_BWD_AUTO) algo = staged_ready ? MAXK_BWD_STAGED : MAXK_BWD_ATOMIC;
     if (algo == MAXK_BWD_ATOMIC) {
-        hipError_t e = hipMemsetAsync(dxs, 0, (size_t)num_rows * dim_k * sizeof(float), st);
+        hipError_t e = hipMemsetAsync(dxs, 0, (size_t)num_cols * dim_k * sizeof(float), st);
         if (e != hipSuccess) return (int)e;
         return dispatch_k<BwdPanel>(dim_k, false, sched, num_panels, indptr, indices, values, grad,
                                     cbsr_sel, (const int32_t *)nullptr, num_rows, dim_origin, dim_k,
@@ -1090,7 +1091,6 @@ int maxk_sspmm_backward(int algo, const int32_t *sched, int64_t num_panels,
     }
     if (algo != MAXK_BWD_STAGED || !staged_ready) return MAXK_E_ARG;
     // workspace: [P rows (E*k floats)] [carry (CP*k floats)] [carry_row (CP ints)]
-    if (num_edges < 0) return MAXK_E_ARG;
     if (workspace_bytes < maxk_backward_workspace_bytes(algo, num_edges, dim_k, csc_num_panels))
         return MAXK_E_WORKSPACE;
     const size_t pbytes = align_up((size_t)num_edges * dim_k * sizeof(float), 256);
@@ -1102,7 +1102,7 @@ int maxk_sspmm_backward(int algo, const int32_t *sched, int64_t num_panels,
     int rc = dispatch_k<BwdPanel>(dim_k, true, sched, num_panels, indptr, indices, values, grad,
                                   cbsr_sel, csc_pos, num_rows, dim_origin, dim_k, dxs, Pbuf, st);
     if (rc) return rc;
-    return dispatch_k<BwdSegsum>(dim_k, csc_sched, csc_num_panels, csc_indptr, Pbuf, num_rows,
+    return dispatch_k<BwdSegsum>(dim_k, csc_sched, csc_num_panels, csc_indptr, Pbuf, num_cols,
                                  dim_k, dxs, carry, carry_row, st);
 }
 

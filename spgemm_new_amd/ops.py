@@ -75,7 +75,7 @@ class MaxKGraph:
     def __init__(self, indptr: torch.Tensor, indices: torch.Tensor,
                  values: torch.Tensor | None = None, *, panel_cost: int = _lib.DEFAULT_PANEL_COST,
                  row_cost: int = _lib.DEFAULT_ROW_COST, bwd_panel_cost: int | None = None,
-                 csc_panel_cost: int | None = None):
+                 csc_panel_cost: int | None = None, num_cols: int | None = None):
         check_tensor(indptr, "indptr", torch.int32, dim=1)
         check_tensor(indices, "indices", torch.int32, dim=1)
         if values is None:
@@ -86,6 +86,8 @@ class MaxKGraph:
         if indptr.device != indices.device or values.device != indices.device:
             raise RuntimeError("graph tensors must be on the same device")
         self.num_rows = indptr.numel() - 1
+        # A may be rectangular (a multi-GPU rank's row block with halo columns)
+        self.num_cols = self.num_rows if num_cols is None else int(num_cols)
         self.num_edges = indices.numel()
         if self.num_edges == 0:  # the C ABI wants valid pointers even for an empty edge list
             indices = torch.zeros(1, dtype=torch.int32, device=indices.device)
@@ -121,10 +123,10 @@ class MaxKGraph:
             order = torch.argsort(idx, stable=True)
             csc_pos = torch.empty(self.num_edges, dtype=torch.int32, device=self.device)
             csc_pos[order] = torch.arange(self.num_edges, dtype=torch.int32, device=self.device)
-            counts = torch.bincount(idx, minlength=self.num_rows)[: self.num_rows]
-            csc_indptr = torch.zeros(self.num_rows + 1, dtype=torch.int32, device=self.device)
+            counts = torch.bincount(idx, minlength=self.num_cols)[: self.num_cols]
+            csc_indptr = torch.zeros(self.num_cols + 1, dtype=torch.int32, device=self.device)
             csc_indptr[1:] = torch.cumsum(counts, 0).to(torch.int32)
-            sched, P = _build_schedule(csc_indptr, self.num_rows, self.num_edges,
+            sched, P = _build_schedule(csc_indptr, self.num_cols, self.num_edges,
                                        self.csc_panel_cost, self.row_cost)
             self._csc = (csc_pos, csc_indptr, sched, P)
         return self._csc
@@ -141,8 +143,8 @@ class MaxKGraph:
                 plan["values_key"] = _tensor_key(self.values)
             return plan
         plan = None
-        V, E = self.num_rows, self.num_edges
-        if E > 0 and V < (1 << 24) and 64 % dim_k == 0:
+        V, E = self.num_cols, self.num_edges      # V: destinations (columns of A)
+        if E > 0 and self.num_rows < (1 << 24) and 64 % dim_k == 0:
             dmax = max(1, min(256, LOCAL_WAVE_LDS_BYTES // (5 * dim_k)))
             _, csc_indptr, _, _ = self.csc()
             cus = torch.cuda.get_device_properties(self.device).multi_processor_count
@@ -163,7 +165,7 @@ class MaxKGraph:
             W = dstart.numel() - 1
             idx = self.indices[:E].long()
             owner = torch.searchsorted(dstart, self.indices[:E], right=True) - 1
-            rows = torch.repeat_interleave(torch.arange(V, device=self.device),
+            rows = torch.repeat_interleave(torch.arange(self.num_rows, device=self.device),
                                            (self.indptr[1:] - self.indptr[:-1]).long())
             perm = torch.argsort(owner, stable=True)
             erc = (rows[perm] | ((idx[perm] - dstart.long()[owner[perm]]) << 24)).to(torch.int32)
@@ -212,8 +214,8 @@ def _check_cbsr(g: MaxKGraph, data, sel):
     check_tensor(sel, "sparse_selector", torch.uint8, dim=2)
     if data.shape != sel.shape:
         raise RuntimeError("input_data and sparse_selector must have the same shape")
-    if data.shape[0] != g.num_rows:
-        raise RuntimeError(f"CBSR has {data.shape[0]} rows, graph has {g.num_rows}")
+    if data.shape[0] != g.num_cols:
+        raise RuntimeError(f"CBSR has {data.shape[0]} rows, graph has {g.num_cols} columns")
     if data.device != g.device or sel.device != g.device:
         raise RuntimeError("CBSR tensors must be on the graph's device")
 
@@ -243,16 +245,17 @@ def spgemm_forward(g: MaxKGraph, data, sel, dim_origin: int = 256, out=None, val
 def sspmm_backward(g: MaxKGraph, grad, sel, out=None, values=None, algo: int = _lib.MAXK_BWD_AUTO):
     check_tensor(grad, "grad_output", torch.float32, dim=2)
     check_tensor(sel, "sparse_selector", torch.uint8, dim=2)
-    if grad.shape[0] != g.num_rows or sel.shape[0] != g.num_rows:
-        raise RuntimeError("grad_output / sparse_selector rows must equal the graph's rows")
+    if grad.shape[0] != g.num_rows or sel.shape[0] != g.num_cols:
+        raise RuntimeError("grad_output rows must equal the graph's rows and sparse_selector "
+                           "rows its columns")
     dim_origin, k = grad.shape[1], sel.shape[1]
     if values is None:
         values = g.values
     if out is None:
-        out = torch.empty((g.num_rows, k), dtype=torch.float32, device=g.device)
+        out = torch.empty((g.num_cols, k), dtype=torch.float32, device=g.device)
     else:
         check_tensor(out, "grad_input", torch.float32, dim=2)
-        if tuple(out.shape) != (g.num_rows, k):
+        if tuple(out.shape) != (g.num_cols, k):
             raise RuntimeError("grad_input has the wrong shape")
     if algo == _lib.MAXK_BWD_AUTO:
         # measured on MI355X (DESIGN.md "Backward"): STAGED is fastest on the
@@ -284,7 +287,8 @@ def sspmm_backward(g: MaxKGraph, grad, sel, out=None, values=None, algo: int = _
     g.last_bwd_algo = {_lib.MAXK_BWD_ATOMIC: "atomic", _lib.MAXK_BWD_STAGED: "staged"}[algo]
     _lib.check(L.maxk_sspmm_backward(
         algo, g.bwd_sched.data_ptr(), g.bwd_num_panels, g.indptr.data_ptr(), g.indices.data_ptr(),
-        values.data_ptr(), grad.data_ptr(), sel.data_ptr(), g.num_rows, g.num_edges, dim_origin, k,
+        values.data_ptr(), grad.data_ptr(), sel.data_ptr(), g.num_rows, g.num_cols, g.num_edges,
+        dim_origin, k,
         out.data_ptr(), _lib.ptr(csc_pos), _lib.ptr(csc_sched), CP, _lib.ptr(csc_indptr),
         _lib.ptr(ws), 0 if ws is None else ws.numel(), _stream(out)), "maxk_sspmm_backward")
     return out
