@@ -42,6 +42,8 @@ def parse():
     p.add_argument("--row-cost", type=int, default=None)
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--cpu-seconds", type=float, default=12.0)
+    p.add_argument("--partitioned", action="store_true",
+                   help="use the multi-GPU (row partition + halo exchange) path even at N=1")
     p.add_argument("--verbose", action="store_true")
     return p.parse_args()
 
@@ -123,9 +125,12 @@ def main():
     torch.cuda.set_device(local_rank)
     dev = torch.device("cuda", local_rank)
     dist = None
-    if world > 1:
+    partitioned = world > 1 or args.partitioned
+    if partitioned:
         import torch.distributed as dist
-        dist.init_process_group("nccl", device_id=dev)
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        os.environ.setdefault("MASTER_PORT", "29511")
+        dist.init_process_group("nccl", device_id=dev, rank=rank, world_size=world)
 
     V, E = CONFIGS[args.graph]
     h, k = args.h, args.k
@@ -148,7 +153,7 @@ def main():
     if args.row_cost:
         kw["row_cost"] = args.row_cost
 
-    if world > 1:
+    if partitioned:
         from spgemm_new_amd.distributed import PartitionedMaxK
         model = PartitionedMaxK(indptr, indices, values, rank, world, dev, **kw)
         data_l, sel_l = model.local_rows(data), model.local_rows(sel)
@@ -204,11 +209,15 @@ def main():
         "data": "synthetic (power-law degrees, uniform columns, seed 123; values/X/G U(0,1))",
         "config": {"workload": f"{args.graph} fwd SpGEMM + bwd SSpMM", "graph": args.graph,
                    "num_nodes": V, "num_edges": E, "hidden": h, "k": k,
-                   "parallelism": f"rowpart{world}" if world > 1 else "single",
+                   "parallelism": f"rowpart{world}" if partitioned else "single",
                    "bwd_algo": args.bwd_algo},
     }
 
-    if world == 1:
+    if partitioned:
+        p = model.plan
+        result["config"]["halo_nodes_rank0"] = p.num_halo
+        result["config"]["own_nodes_rank0"] = p.num_own
+    if not partitioned:
         # per-call timing with HIP events on the launch stream (the current stream)
         st = torch.cuda.current_stream()
         fw, bw = [], []
