@@ -100,6 +100,24 @@ def cpu_baseline(indptr, indices, values, x_masked, grad, mask, k, h, budget_s):
     }
 
 
+def workload_key(args, bwd_algo):
+    return f"{args.graph}_h{args.h}_k{args.k}_{bwd_algo}"
+
+
+def pmc_traffic(key, call):
+    """HBM bytes per launch of `call` measured by rocprofv3 PMC passes
+    (FETCH_SIZE x2 + WRITE_SIZE, MI355X_MICROARCH.md §HBM) for this exact
+    workload, from the committed profile summary (tools/profile.sh +
+    tools/summarize_profile.py); None when no such profile exists."""
+    path = os.path.join(ROOT, "profiles", "pmc_traffic.json")
+    try:
+        ent = json.load(open(path))[key]
+    except (OSError, KeyError, ValueError):
+        return None, None
+    v = ent.get(call)
+    return (int(v) if v else None), f"profiles/{ent['profile']}_summary.json"
+
+
 def _cpu_model():
     try:
         for line in open("/proc/cpuinfo"):
@@ -235,9 +253,10 @@ def main():
         b_call = 8 * E + 5 * k * E + 4 * h * V
         dom = ("sspmm_backward", bms) if bms >= fms else ("spgemm_forward", fms)
         ach = b_call / (dom[1] / 1e3) / 1e9
+        traffic, tsrc = pmc_traffic(workload_key(args, g.last_bwd_algo), dom[0])
         result["roofline"] = {"bound": "hbm", "achieved": round(ach, 1), "peak": HBM_PEAK_GBS,
                               "unit": "GB/s", "frac": round(ach / HBM_PEAK_GBS, 4),
-                              "traffic": None, "kernel": dom[0],
+                              "traffic": traffic, "traffic_source": tsrc, "kernel": dom[0],
                               "algorithmic_bytes_per_launch": b_call}
         result["config"]["bwd_algo"] = g.last_bwd_algo
         result["fwd_ms"] = round(fms, 4)

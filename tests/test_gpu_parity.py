@@ -309,3 +309,27 @@ def test_stream_capture_hipgraph(dev, oracle, g_small):
                                oracle.np_forward(indptr, indices, values, data, sel, h)) <= TOL
     assert oracle.parity_error(dx.cpu().numpy(),
                                oracle.np_backward(indptr, indices, values, grad, sel)) <= TOL
+
+
+def test_direct_kernel_interface(dev, oracle, tmp_path):
+    """direct_kernel_interface.py surface: graph files on disk, warp4 built on device,
+    cuSPARSE-style validation (rocSPARSE via torch), k sweep."""
+    from spgemm_new_amd.direct_kernel_interface import (DirectMaxKKernels, GraphDataLoader,
+                                                        test_direct_kernels)
+    from spgemm_new_amd.graphs import write_csr
+    indptr, indices = small_csr(1000, seed=31)
+    write_csr(str(tmp_path / "toy"), indptr, indices)
+    loader = GraphDataLoader(str(tmp_path))
+    assert loader.get_available_graphs() == ["toy"]
+    gd = loader.to_cuda_tensors(loader.load_graph("toy"))
+    kern = DirectMaxKKernels("toy")
+    assert kern.load_warp4_metadata() is False          # no .warp4 file on disk
+    assert kern.load_warp4_metadata(indptr=gd["indptr"]) is True
+    assert kern.num_warps == len(oracle.c_warp4(indptr))
+    x = torch.rand(1000, 256, device=dev)
+    assert kern.validate_against_cusparse(gd, x, 32)
+    y, t = kern.run_forward_kernel(gd, x, 16, timing=True)
+    assert y.shape == (1000, 256) and t > 0
+    res = kern.benchmark_all_k_values(gd, 256, (8, 32), num_runs=2)
+    assert set(res) == {8, 32}
+    assert test_direct_kernels(str(tmp_path))
