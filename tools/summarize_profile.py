@@ -70,7 +70,6 @@ def main(tag: str, root: str = ".", workload: str | None = None):
             tot = 0.0
             for n in names:
                 if n in k and "hbm_read_bytes_x2" in k[n] and "hbm_write_bytes" in k[n]:
-                    calls = k[n].get("calls", 1)
                     per = k[n]["hbm_read_bytes_x2"] + k[n]["hbm_write_bytes"]
                     # fixup runs once per forward and once per backward call
                     tot += per * (0.5 if n == "carry_fixup_kernel" else 1.0)
