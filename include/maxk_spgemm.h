@@ -110,15 +110,21 @@ int maxk_sspmm_backward(int algo, const int32_t *sched, int64_t num_panels,
  * MaxKGraph.local_plan): destinations split into `num_waves` ranges
  * wave_dst_start[0..W] (<= dmax <= 256 each); each range's in-edges sorted by
  * source row, packed as edge_rc = row | (dest - range_start) << 24 and
- * edge_val, with wave_edge_off[0..W] offsets.  num_rows < 2^24; dim_k must
- * divide 64; LDS per 4-wave block = maxk_backward_local_lds_bytes(dmax, k)
- * <= 160 KiB.  Writes every element of dxs.
+ * edge_val.  The source rows are cut into `num_segments` bands, one launch
+ * each, so the gradient rows in flight stay cache-resident:
+ * seg_edge_off[s * W + w] is the first edge of wave w in band s, and row
+ * s = num_segments holds each wave's end (for one band: the wave offsets
+ * without the last, then without the first).  Band 0 writes the owned dXs
+ * rows, later bands add to them.  num_rows < 2^24; dim_k must divide 64; LDS
+ * per 4-wave block = maxk_backward_local_lds_bytes(dmax, k) <= 160 KiB.
+ * Writes every element of dxs.
  * ------------------------------------------------------------------------- */
 size_t maxk_backward_local_lds_bytes(int dmax, int dim_k);
-int maxk_sspmm_backward_local(const int32_t *wave_edge_off, const int32_t *wave_dst_start,
-                              int num_waves, int dmax, const int32_t *edge_rc,
-                              const float *edge_val, const float *grad, const uint8_t *cbsr_sel,
-                              int num_rows, int dim_origin, int dim_k, float *dxs, void *stream);
+int maxk_sspmm_backward_local(const int32_t *seg_edge_off, int num_segments,
+                              const int32_t *wave_dst_start, int num_waves, int dmax,
+                              const int32_t *edge_rc, const float *edge_val, const float *grad,
+                              const uint8_t *cbsr_sel, int num_rows, int dim_origin, int dim_k,
+                              float *dxs, void *stream);
 
 /* ---------------------------------------------------------------------------
  * Exact drop-ins for the reference's extern "C" launchers

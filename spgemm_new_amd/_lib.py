@@ -48,7 +48,7 @@ SIGNATURES = {
     "maxk_sspmm_backward": (_I, [_I, _P, _L, _P, _P, _P, _P, _P, _I, _I, _L, _I, _I, _P, _P, _P,
                                  _L, _P, _P, _S, _P]),
     "maxk_backward_local_lds_bytes": (_S, [_I, _I]),
-    "maxk_sspmm_backward_local": (_I, [_P, _P, _I, _I, _P, _P, _P, _P, _I, _I, _I, _P, _P]),
+    "maxk_sspmm_backward_local": (_I, [_P, _I, _P, _I, _I, _P, _P, _P, _P, _I, _I, _I, _P, _P]),
     "maxk_spmm_forward_warp4": (_I, [_P, _P, _P, _P, _P, _P, _I, _I, _I, _I, _I, _P]),
     "maxk_spmm_backward_warp4": (_I, [_P, _P, _P, _P, _P, _P, _I, _I, _I, _I, _I, _P]),
 }

@@ -728,19 +728,26 @@ __global__ __launch_bounds__(kBlock) void bwd_warp4_kernel(
 // Backward LOCAL: destination-owned accumulation (no atomics, no staging rows)
 //
 // Wave w owns destinations [dstart[w], dstart[w+1]) (D <= 256): their dXs
-// rows and selector rows live in the wave's LDS for the whole kernel.  Its
-// in-edges arrive as a list sorted by SOURCE row r, packed (r | c_local<<24,
-// val) by the plan builder (ops.py).  Every wave sweeps r upward at a similar
-// pace, so the gradient rows G[r] the chip is reading at any moment form a
-// narrow window that each XCD's L2 serves; each G row leaves HBM about once
-// per XCD instead of once per edge.  Per edge the K lanes of a group gather
+// rows and selector rows live in the wave's LDS for the launch.  Its in-edges
+// arrive as a list sorted by SOURCE row r, packed (r | c_local<<24, val) by
+// the plan builder (ops.py).  The source rows are cut into bands, one launch
+// per band (first band stores dXs, later ones reload and add), so the
+// gradient rows G[r] the chip reads during a launch form a window of about
+// 32 MB that the Infinity Cache serves: measured 4.8 ms with a resident
+// window vs 10.8 ms when every wave sweeps all of G in one launch (Reddit
+// shape, uniform sources; tools/exp_local_window.py).  Per edge the K lanes of a group gather
 // G[r, sel[c, l]] (global, L2) and read-modify-write dXs[c, l] in LDS.
 // EPS = 64/K edges share one wave-instruction; a group whose destinations
 // collide is processed one edge at a time (plain LDS RMW stays race-free).
 // ---------------------------------------------------------------------------
+#ifndef LOCAL_U
+#define LOCAL_U 8
+#endif
+
 template <int K>
 __global__ __launch_bounds__(kBlock) void bwd_local_kernel(
-    const int32_t *__restrict__ woff, const int32_t *__restrict__ dstart, int num_waves,
+    const int32_t *__restrict__ seg_beg, const int32_t *__restrict__ seg_end, bool first,
+    const int32_t *__restrict__ dstart, int num_waves,
     int dmax, const int32_t *__restrict__ erc, const float *__restrict__ evl,
     const float *__restrict__ grad, const uint8_t *__restrict__ sel, int dim,
     float *__restrict__ dxs)
@@ -756,15 +763,17 @@ __global__ __launch_bounds__(kBlock) void bwd_local_kernel(
     const int w = blockIdx.x * kWavesPerBlock + wl;
     if (w >= num_waves) return;
     const int lane = lane_id();
+    const int e_beg = seg_beg[w], e_end = seg_end[w];
+    if (!first && e_beg == e_end) return;  // nothing to add in this band
     const int d0 = dstart[w], D = dstart[w + 1] - d0;
     const int nent = D * K;
+    float *dst = dxs + (size_t)d0 * K;
     for (int i = lane; i < nent; i += kWave) {
-        acc[i] = 0.f;
+        acc[i] = first ? 0.f : dst[i];
         sl[i] = sel[(size_t)d0 * K + i];
     }
     wave_sync_lds();
     const int grp = lane / K, l = lane % K;
-    const int e_beg = woff[w], e_end = woff[w + 1];
     // records of the next batch are prefetched while the current one gathers
     int nx_rc = 0;
     float nx_v = 0.f;
@@ -780,63 +789,64 @@ __global__ __launch_bounds__(kBlock) void bwd_local_kernel(
             nx_rc = __builtin_nontemporal_load(erc + base + B + lane);
             nx_v = __builtin_nontemporal_load(evl + base + B + lane);
         }
-        float gv[NG], vv[NG];
-        int cc[NG];
-        uint32_t clash = 0;  // bit u: group u has two edges into one destination
+        // U groups of gathers in flight per round (VGPR budget vs memory-level parallelism)
+        for (int g0 = 0; g0 < NG; g0 += LOCAL_U) {
+            if (g0 * EPS >= n) break;
+            float gv[LOCAL_U], vv[LOCAL_U];
+            int cc[LOCAL_U];
+            uint32_t clash = 0;  // bit u: group u has two edges into one destination
 #pragma unroll
-        for (int u = 0; u < NG; ++u) {
-            const int t = u * EPS + grp;
-            int rc;
-            if constexpr (EPS == 1) {
-                rc = __builtin_amdgcn_readlane(my_rc, u);
-                vv[u] = __builtin_bit_cast(float, __builtin_amdgcn_readlane(
-                    __builtin_bit_cast(int, my_v), u));
-            } else if constexpr (EPS == 2) {
-                const int ra = __builtin_amdgcn_readlane(my_rc, 2 * u);
-                const int rb = __builtin_amdgcn_readlane(my_rc, 2 * u + 1);
-                const float va = __builtin_bit_cast(float, __builtin_amdgcn_readlane(
-                    __builtin_bit_cast(int, my_v), 2 * u));
-                const float vb = __builtin_bit_cast(float, __builtin_amdgcn_readlane(
-                    __builtin_bit_cast(int, my_v), 2 * u + 1));
-                rc = grp ? rb : ra;
-                vv[u] = grp ? vb : va;
-                if ((2 * u + 1 < n) && ((ra >> 24) == (rb >> 24))) clash |= 1u << u;
-            } else {
-                rc = __shfl(my_rc, t);
-                vv[u] = __shfl(my_v, t);
-                bool c = false;
+            for (int u = 0; u < LOCAL_U; ++u) {
+                const int gi = g0 + u;
+                const int t = gi * EPS + grp;
+                int rc;
+                if constexpr (EPS == 1) {
+                    rc = __shfl(my_rc, gi);
+                    vv[u] = __shfl(my_v, gi);
+                } else if constexpr (EPS == 2) {
+                    const int ra = __shfl(my_rc, 2 * gi);
+                    const int rb = __shfl(my_rc, 2 * gi + 1);
+                    const float va = __shfl(my_v, 2 * gi);
+                    const float vb = __shfl(my_v, 2 * gi + 1);
+                    rc = grp ? rb : ra;
+                    vv[u] = grp ? vb : va;
+                    if ((2 * gi + 1 < n) && ((ra >> 24) == (rb >> 24))) clash |= 1u << u;
+                } else {
+                    rc = __shfl(my_rc, t);
+                    vv[u] = __shfl(my_v, t);
+                    bool c = false;
 #pragma unroll
-                for (int j = 1; j < EPS; ++j) {
-                    const int other = __shfl(rc, lane >= j * K ? lane - j * K : lane);
-                    c |= (lane >= j * K) && ((other >> 24) == (rc >> 24)) && (t < n);
+                    for (int j = 1; j < EPS; ++j) {
+                        const int other = __shfl(rc, lane >= j * K ? lane - j * K : lane);
+                        c |= (lane >= j * K) && ((other >> 24) == (rc >> 24)) && (t < n);
+                    }
+                    if (__any(c)) clash |= 1u << u;
                 }
-                if (__any(c)) clash |= 1u << u;
+                cc[u] = (rc >> 24) & 0xff;
+                gv[u] = 0.f;
+                if (t < n) {
+                    const int col = sl[cc[u] * K + l];
+                    gv[u] = col < dim ? grad[(size_t)(rc & 0xffffff) * dim + col] : 0.f;
+                } else {
+                    vv[u] = 0.f;
+                    cc[u] = -1;
+                }
             }
-            cc[u] = (rc >> 24) & 0xff;
-            gv[u] = 0.f;
-            if (t < n) {
-                const int col = sl[cc[u] * K + l];
-                gv[u] = col < dim ? grad[(size_t)(rc & 0xffffff) * dim + col] : 0.f;
-            } else {
-                vv[u] = 0.f;
-                cc[u] = -1;
-            }
-        }
 #pragma unroll
-        for (int u = 0; u < NG; ++u) {
-            if (u * EPS >= n) break;
-            if (!((clash >> u) & 1u)) {
-                if (cc[u] >= 0) acc[cc[u] * K + l] += vv[u] * gv[u];
-            } else {
-                for (int gg = 0; gg < EPS; ++gg) {
-                    if (grp == gg && cc[u] >= 0) acc[cc[u] * K + l] += vv[u] * gv[u];
-                    wave_sync_lds();
+            for (int u = 0; u < LOCAL_U; ++u) {
+                if ((g0 + u) * EPS >= n) break;
+                if (!((clash >> u) & 1u)) {
+                    if (cc[u] >= 0) acc[cc[u] * K + l] += vv[u] * gv[u];
+                } else {
+                    for (int gg = 0; gg < EPS; ++gg) {
+                        if (grp == gg && cc[u] >= 0) acc[cc[u] * K + l] += vv[u] * gv[u];
+                        wave_sync_lds();
+                    }
                 }
             }
         }
     }
     wave_sync_lds();
-    float *dst = dxs + (size_t)d0 * K;
     for (int i = lane; i < nent; i += kWave) dst[i] = acc[i];
 }
 
@@ -950,15 +960,20 @@ struct BwdSegsum {
 
 template <int K>
 struct BwdLocal {
-    static int run(const int32_t *woff, const int32_t *dstart, int W, int dmax, const int32_t *erc,
-                   const float *evl, const float *grad, const uint8_t *sel, int dim, float *dxs,
-                   hipStream_t st)
+    static int run(const int32_t *seg_off, int NS, const int32_t *dstart, int W, int dmax,
+                   const int32_t *erc, const float *evl, const float *grad, const uint8_t *sel,
+                   int dim, float *dxs, hipStream_t st)
     {
         const size_t region = (size_t)((dmax * K * 5 + 15) & ~15);
-        hipLaunchKernelGGL(bwd_local_kernel<K>, dim3((unsigned)ceil_div(W, kWavesPerBlock)),
-                           dim3(kBlock), region * kWavesPerBlock, st, woff, dstart, W, dmax, erc,
-                           evl, grad, sel, dim, dxs);
-        return launch_status();
+        for (int s = 0; s < NS; ++s) {
+            hipLaunchKernelGGL(bwd_local_kernel<K>, dim3((unsigned)ceil_div(W, kWavesPerBlock)),
+                               dim3(kBlock), region * kWavesPerBlock, st,
+                               seg_off + (size_t)s * W, seg_off + (size_t)(s + 1) * W, s == 0,
+                               dstart, W, dmax, erc, evl, grad, sel, dim, dxs);
+            const int rc = launch_status();
+            if (rc) return rc;
+        }
+        return MAXK_OK;
     }
 };
 
@@ -1111,27 +1126,31 @@ size_t maxk_backward_local_lds_bytes(int dmax, int dim_k)
     return (size_t)kWavesPerBlock * (size_t)((dmax * dim_k * 5 + 15) & ~15);
 }
 
-int maxk_sspmm_backward_local(const int32_t *wave_edge_off, const int32_t *wave_dst_start,
-                              int num_waves, int dmax, const int32_t *edge_rc,
-                              const float *edge_val, const float *grad, const uint8_t *cbsr_sel,
-                              int num_rows, int dim_origin, int dim_k, float *dxs, void *stream)
+int maxk_sspmm_backward_local(const int32_t *seg_edge_off, int num_segments,
+                              const int32_t *wave_dst_start, int num_waves, int dmax,
+                              const int32_t *edge_rc, const float *edge_val, const float *grad,
+                              const uint8_t *cbsr_sel, int num_rows, int dim_origin, int dim_k,
+                              float *dxs, void *stream)
 {
-    if (!wave_edge_off || !wave_dst_start || !dxs || num_waves < 1 || num_rows < 1 ||
-        num_rows >= (1 << 24) || dmax < 1 || dmax > 256)
+    if (!seg_edge_off || !wave_dst_start || !dxs || num_waves < 1 || num_segments < 1 ||
+        num_rows < 1 || num_rows >= (1 << 24) || dmax < 1 || dmax > 256)
         return MAXK_E_ARG;
     if (!dims_ok(dim_origin, dim_k) || (kWave % dim_k) != 0) return MAXK_E_DIM;
     if (!edge_rc || !edge_val || !grad || !cbsr_sel) return MAXK_E_ARG;
     if (maxk_backward_local_lds_bytes(dmax, dim_k) > 160 * 1024) return MAXK_E_WORKSPACE;
     hipStream_t st = as_stream(stream);
+#define LOCAL_ARGS seg_edge_off, num_segments, wave_dst_start, num_waves, dmax, edge_rc, edge_val, \
+                   grad, cbsr_sel, dim_origin, dxs, st
     switch (dim_k) {
-    case 1: return BwdLocal<1>::run(wave_edge_off, wave_dst_start, num_waves, dmax, edge_rc, edge_val, grad, cbsr_sel, dim_origin, dxs, st);
-    case 2: return BwdLocal<2>::run(wave_edge_off, wave_dst_start, num_waves, dmax, edge_rc, edge_val, grad, cbsr_sel, dim_origin, dxs, st);
-    case 4: return BwdLocal<4>::run(wave_edge_off, wave_dst_start, num_waves, dmax, edge_rc, edge_val, grad, cbsr_sel, dim_origin, dxs, st);
-    case 8: return BwdLocal<8>::run(wave_edge_off, wave_dst_start, num_waves, dmax, edge_rc, edge_val, grad, cbsr_sel, dim_origin, dxs, st);
-    case 16: return BwdLocal<16>::run(wave_edge_off, wave_dst_start, num_waves, dmax, edge_rc, edge_val, grad, cbsr_sel, dim_origin, dxs, st);
-    case 32: return BwdLocal<32>::run(wave_edge_off, wave_dst_start, num_waves, dmax, edge_rc, edge_val, grad, cbsr_sel, dim_origin, dxs, st);
-    default: return BwdLocal<64>::run(wave_edge_off, wave_dst_start, num_waves, dmax, edge_rc, edge_val, grad, cbsr_sel, dim_origin, dxs, st);
+    case 1: return BwdLocal<1>::run(LOCAL_ARGS);
+    case 2: return BwdLocal<2>::run(LOCAL_ARGS);
+    case 4: return BwdLocal<4>::run(LOCAL_ARGS);
+    case 8: return BwdLocal<8>::run(LOCAL_ARGS);
+    case 16: return BwdLocal<16>::run(LOCAL_ARGS);
+    case 32: return BwdLocal<32>::run(LOCAL_ARGS);
+    default: return BwdLocal<64>::run(LOCAL_ARGS);
     }
+#undef LOCAL_ARGS
 }
 
 int maxk_spmm_forward_warp4(const int32_t *warp4, const int32_t *idx, const float *val,

@@ -15,6 +15,8 @@ ops once per graph (plumbing, outside the hot path).
 """
 from __future__ import annotations
 
+import os
+
 import torch
 
 from . import _lib
@@ -46,8 +48,11 @@ def _tensor_key(t):
 
 
 # LOCAL backward: target LDS bytes per wave (8 waves per CU share 160 KiB)
-LOCAL_WAVE_LDS_BYTES = 20 * 1024
-LOCAL_WAVES_PER_CU = 8
+LOCAL_WAVE_LDS_BYTES = int(os.environ.get("MAXK_LOCAL_WAVE_LDS", 10 * 1024))
+LOCAL_WAVES_PER_CU = int(os.environ.get("MAXK_LOCAL_WAVES_PER_CU", 16))
+# LOCAL backward: gradient-row bytes per source band (one launch each); about 32 MB keeps a
+# band's G rows resident in the Infinity Cache (tools/exp_local_window.py)
+LOCAL_BAND_BYTES = int(os.environ.get("MAXK_LOCAL_BAND_BYTES", 32 << 20))
 
 
 def _build_schedule(indptr: torch.Tensor, num_rows: int, num_edges: int, panel_cost: int,
@@ -106,6 +111,7 @@ class MaxKGraph:
         self._csc = None
         self._local = {}
         self._ws = {}
+        self._bwd_choice = {}
         self.last_bwd_algo = None
 
     # ------------------------------------------------------------------ utils
@@ -174,11 +180,42 @@ class MaxKGraph:
             perm32 = perm.to(torch.int32)
             del rows, owner, idx, perm
             plan = {"dmax": dmax, "num_waves": W, "dstart": dstart, "woff": woff,
-                    "edge_rc": erc.contiguous(), "perm": perm32,
+                    "edge_rc": erc.contiguous(), "perm": perm32, "bands": {},
                     "edge_val": self.values[:E][perm32.long()].contiguous(),
                     "values_key": _tensor_key(self.values)}
         self._local[dim_k] = plan
         return plan
+
+    def local_bands(self, plan, dim_origin: int):
+        """(seg_edge_off, num_segments) of the LOCAL plan for gradient rows of
+        dim_origin floats: source rows cut into equal bands of about
+        LOCAL_BAND_BYTES of G; seg_edge_off[s*W + w] = first edge of wave w in
+        band s (a wave's edges are sorted by source row), row NS = wave ends."""
+        ns = max(1, -(-self.num_rows * dim_origin * 4 // max(LOCAL_BAND_BYTES, 1)))
+        ns = min(ns, self.num_rows)
+        hit = plan["bands"].get(ns)
+        if hit is not None:
+            return hit
+        W, woff = plan["num_waves"], plan["woff"]
+        if ns == 1:
+            seg = torch.cat([woff[:-1], woff[1:]])
+        else:
+            n = int(woff[-1])
+            owner = torch.repeat_interleave(torch.arange(W, device=self.device),
+                                            (woff[1:] - woff[:-1]).long(), output_size=n)
+            key = owner * self.num_rows + (plan["edge_rc"].long() & 0xFFFFFF)
+            del owner
+            cuts = torch.div(torch.arange(ns + 1, device=self.device) * self.num_rows, ns,
+                             rounding_mode="floor")
+            q = torch.arange(W, device=self.device)[None, :] * self.num_rows + cuts[:, None]
+            seg = torch.searchsorted(key, q.reshape(-1)).to(torch.int32)
+            seg = seg.view(ns + 1, W)
+            seg[-1] = woff[1:]
+            seg = seg.reshape(-1)
+            del key, q
+        hit = (seg.contiguous(), ns)
+        plan["bands"][ns] = hit
+        return hit
 
     def local_fits(self, dim_k: int) -> bool:
         """True when the LOCAL plan's waves are all co-resident (one sweep of G)."""
@@ -190,6 +227,37 @@ class MaxKGraph:
         per_block = L.maxk_backward_local_lds_bytes(plan["dmax"], dim_k)
         blocks_per_cu = max(1, (160 * 1024) // max(per_block, 1))
         return plan["num_waves"] <= cus * blocks_per_cu * 4
+
+    def autotune_backward(self, grad, sel, out, values=None) -> int:
+        """MAXK_BWD_AUTO: the fastest algorithm for this graph and k, measured once
+        (each candidate run twice, the second timed with HIP events on the
+        current stream) and cached.  Candidates: STAGED, ATOMIC, and LOCAL when
+        its plan exists.  During stream capture, or before any measurement,
+        STAGED is used (allocation-free once its workspace exists)."""
+        k = sel.shape[1]
+        key = (k, grad.shape[1])
+        if key in self._bwd_choice:
+            return self._bwd_choice[key]
+        if self.num_edges == 0 or torch.cuda.is_current_stream_capturing():
+            return _lib.MAXK_BWD_STAGED
+        cands = [_lib.MAXK_BWD_STAGED, _lib.MAXK_BWD_ATOMIC]
+        if (values is None or values is self.values) and self.local_plan(k) is not None:
+            cands.append(_lib.MAXK_BWD_LOCAL)
+        best, best_ms = None, float("inf")
+        for a in cands:
+            sspmm_backward(self, grad, sel, out, values, a)
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record()
+            sspmm_backward(self, grad, sel, out, values, a)
+            e1.record()
+            e1.synchronize()
+            ms = e0.elapsed_time(e1)
+            if ms < best_ms:
+                best, best_ms = a, ms
+        self._bwd_choice[key] = best
+        self.bwd_timings = getattr(self, "bwd_timings", {})
+        self.bwd_timings[key] = best_ms
+        return best
 
     def nbytes_fwd(self, dim_k: int, dim_origin: int) -> int:
         """Algorithmic bytes of one forward call: 8E + 5kE + 4hV."""
@@ -258,9 +326,7 @@ def sspmm_backward(g: MaxKGraph, grad, sel, out=None, values=None, algo: int = _
         if tuple(out.shape) != (g.num_cols, k):
             raise RuntimeError("grad_input has the wrong shape")
     if algo == _lib.MAXK_BWD_AUTO:
-        # measured on MI355X (DESIGN.md "Backward"): STAGED is fastest on the
-        # Reddit/products shapes; LOCAL is L2-request-bound there.
-        algo = _lib.MAXK_BWD_STAGED
+        algo = g.autotune_backward(grad, sel, out, values)
     if g.num_edges == 0:
         algo = _lib.MAXK_BWD_ATOMIC  # nothing to stage: the call just zeroes dXs
     L = _lib.load()
@@ -271,8 +337,9 @@ def sspmm_backward(g: MaxKGraph, grad, sel, out=None, values=None, algo: int = _
         if plan is None:
             raise RuntimeError("LOCAL backward unsupported for this shape (k must divide 64)")
         g.last_bwd_algo = "local"
+        seg, ns = g.local_bands(plan, dim_origin)
         _lib.check(L.maxk_sspmm_backward_local(
-            plan["woff"].data_ptr(), plan["dstart"].data_ptr(), plan["num_waves"], plan["dmax"],
+            seg.data_ptr(), ns, plan["dstart"].data_ptr(), plan["num_waves"], plan["dmax"],
             plan["edge_rc"].data_ptr(), plan["edge_val"].data_ptr(), grad.data_ptr(),
             sel.data_ptr(), g.num_rows, dim_origin, k, out.data_ptr(), _stream(out)),
             "maxk_sspmm_backward_local")

@@ -204,6 +204,29 @@ def test_backward_local_collisions(dev, oracle, monkeypatch, k, wave_lds):
     assert oracle.parity_error(dx.cpu().numpy(), ref) <= TOL
 
 
+@pytest.mark.parametrize("band_bytes", [1, 1024 * 50, 1024 * 300, 1 << 30])
+@pytest.mark.parametrize("k", [8, 32])
+def test_backward_local_bands(dev, oracle, monkeypatch, band_bytes, k):
+    """Source bands (one launch each; band 0 stores dXs, later bands add):
+    one row per band, a few bands, one band.  Waves with no edges in a band
+    skip it; the result is the same sum."""
+    from spgemm_new_amd import ops
+    monkeypatch.setattr(ops, "LOCAL_BAND_BYTES", band_bytes)
+    indptr, indices = small_csr(700, seed=5)
+    v = len(indptr) - 1
+    values = np.random.default_rng(3).random(len(indices), dtype=np.float32)
+    _, sel = random_cbsr(v, k, 256, seed=9)
+    grad = np.random.default_rng(2).random((v, 256), dtype=np.float32)
+    g = S.MaxKGraph(T(indptr, dev), T(indices, dev), T(values, dev))
+    dx = torch.full((v, k), float("nan"), device=dev)
+    g.backward(T(grad, dev), T(sel, dev), out=dx, algo=_lib.MAXK_BWD_LOCAL)
+    seg, ns = g.local_bands(g.local_plan(k), 256)
+    assert ns == min(v, max(1, -(-v * 1024 // band_bytes)))
+    assert seg.numel() == (ns + 1) * g.local_plan(k)["num_waves"]
+    ref = oracle.np_backward(indptr, indices, values, grad, sel)
+    assert oracle.parity_error(dx.cpu().numpy(), ref) <= TOL
+
+
 def test_offset_csr_view(dev, oracle, g_small):
     """indptr[0] != 0 (a row slice of a bigger CSR) is honoured."""
     indptr, indices, values = g_small
