@@ -744,35 +744,105 @@ __global__ __launch_bounds__(kBlock) void bwd_warp4_kernel(
 #define LOCAL_U 8
 #endif
 
+// Offset (in floats) of G[row, col] -> element pointer; 32-bit byte offsets
+// (global_load saddr form) when the whole gradient array is below 4 GiB.
+template <bool WIDE>
+__device__ __forceinline__ const float *g_at(const float *grad, uint32_t row_off, uint32_t col)
+{
+    if constexpr (WIDE)
+        return grad + ((uint64_t)row_off + col);
+    else
+        return reinterpret_cast<const float *>(reinterpret_cast<const char *>(grad) +
+                                               ((row_off + col) << 2));
+}
+
+// One round of the LOCAL loop for K in {32, 64}: R = 16 edge records held in
+// SGPRs (wave-uniform loads), NG = R/EPS gathers issued back to back, then the
+// NG LDS read-modify-writes.  Row offsets, destination slots and the clash
+// test are scalar; per lane only the half-select (EPS = 2), the selector byte
+// and the gather remain.  All R records are valid (the tail round of a wave's
+// list takes the generic loop).
+template <int K, bool WIDE>
+__device__ __forceinline__ void local_round(const int32_t *__restrict__ rec_rc,
+                                            const float *__restrict__ rec_v,
+                                            const float *__restrict__ grad, uint32_t dim,
+                                            const uint8_t *sl, float *acc, int grp, int l)
+{
+    constexpr int EPS = kWave / K;
+    constexpr int R = 16;
+    constexpr int NG = R / EPS;
+    float gv[NG], vv[NG];
+    int ai[NG];
+    uint32_t ro[NG], col[NG];
+    uint32_t clash = 0;
+    const bool hi = EPS == 2 && grp != 0;
+    // scalar part: records -> (destination slot, row offset, value) per half,
+    // pinned in SGPRs (otherwise the half-select is hoisted above the
+    // arithmetic and every lane pays a v_mul_lo_u32); per lane a half-select
+    // is a ^ ((a ^ b) & m) with the xor scalar: two VALU ops
+    int32_t rcs[R];
+    uint32_t vbits[R];
+#pragma unroll
+    for (int i = 0; i < R; ++i) {
+        rcs[i] = rec_rc[i];
+        vbits[i] = __builtin_bit_cast(uint32_t, rec_v[i]);
+    }
+    // materialise all records here (two s_load_dwordx16, one wait)
+    asm volatile("" : "+s"(rcs[0]), "+s"(rcs[1]), "+s"(rcs[2]), "+s"(rcs[3]), "+s"(rcs[4]),
+                 "+s"(rcs[5]), "+s"(rcs[6]), "+s"(rcs[7]), "+s"(rcs[8]), "+s"(rcs[9]),
+                 "+s"(rcs[10]), "+s"(rcs[11]), "+s"(rcs[12]), "+s"(rcs[13]), "+s"(rcs[14]),
+                 "+s"(rcs[15]));
+    const uint32_t m = hi ? 0xffffffffu : 0u;
+#pragma unroll
+    for (int u = 0; u < NG; ++u) {
+        const int ra = rcs[u * EPS];
+        const int rb = EPS == 2 ? rcs[u * EPS + 1] : ra;
+        uint32_t sa = ((uint32_t)ra >> 24) * K, sb = ((uint32_t)rb >> 24) * K;
+        uint32_t oa = (uint32_t)(ra & 0xffffff) * dim, ob = (uint32_t)(rb & 0xffffff) * dim;
+        uint32_t va = vbits[u * EPS], vb = EPS == 2 ? vbits[u * EPS + 1] : va;
+        if (EPS == 2 && sa == sb) clash |= 1u << u;
+        uint32_t xs = sa ^ sb, xo = oa ^ ob, xv = va ^ vb;
+        asm volatile("" : "+s"(sa), "+s"(oa), "+s"(va), "+s"(xs), "+s"(xo), "+s"(xv));
+        if constexpr (EPS == 2) {
+            ai[u] = (int)(sa ^ (xs & m)) + l;
+            ro[u] = oa ^ (xo & m);
+            vv[u] = __builtin_bit_cast(float, va ^ (xv & m));
+        } else {
+            ai[u] = (int)sa + l;
+            ro[u] = oa;
+            vv[u] = __builtin_bit_cast(float, va);
+        }
+    }
+    // selector bytes for all groups, then all gathers back to back
+#pragma unroll
+    for (int u = 0; u < NG; ++u) col[u] = sl[ai[u]];
+#pragma unroll
+    for (int u = 0; u < NG; ++u) gv[u] = *g_at<WIDE>(grad, ro[u], col[u]);
+#pragma unroll
+    for (int u = 0; u < NG; ++u) {
+        if (!((clash >> u) & 1u)) {
+            acc[ai[u]] = fmaf(vv[u], gv[u], acc[ai[u]]);
+        } else {  // both halves target one destination: one half at a time
+            for (int gg = 0; gg < EPS; ++gg) {
+                if (grp == gg) acc[ai[u]] = fmaf(vv[u], gv[u], acc[ai[u]]);
+                wave_sync_lds();
+            }
+        }
+    }
+}
+
+// The generic LOCAL loop (any K dividing 64): records shuffled out of VGPRs.
 template <int K>
-__global__ __launch_bounds__(kBlock) void bwd_local_kernel(
-    const int32_t *__restrict__ seg_beg, const int32_t *__restrict__ seg_end, bool first,
-    const int32_t *__restrict__ dstart, int num_waves,
-    int dmax, const int32_t *__restrict__ erc, const float *__restrict__ evl,
-    const float *__restrict__ grad, const uint8_t *__restrict__ sel, int dim,
-    float *__restrict__ dxs)
+__device__ __forceinline__ void local_edges_shfl(int e_beg, int e_end,
+                                                 const int32_t *__restrict__ erc,
+                                                 const float *__restrict__ evl,
+                                                 const float *__restrict__ grad, int dim,
+                                                 const uint8_t *sl, float *acc)
 {
     constexpr int EPS = kWave / K;                 // edges per wave-instruction
     constexpr int B = EPS * 32 < kWave ? EPS * 32 : kWave;  // edges per batch
     constexpr int NG = B / EPS;                    // groups per batch (<= 32)
-    extern __shared__ __attribute__((aligned(16))) float lds[];
-    const int wl = threadIdx.x / kWave;
-    const int region = (dmax * K * 5 + 15) & ~15;  // bytes: fp32 dXs block + u8 sel block
-    float *acc = reinterpret_cast<float *>(reinterpret_cast<char *>(lds) + wl * region);
-    uint8_t *sl = reinterpret_cast<uint8_t *>(acc + dmax * K);
-    const int w = blockIdx.x * kWavesPerBlock + wl;
-    if (w >= num_waves) return;
     const int lane = lane_id();
-    const int e_beg = seg_beg[w], e_end = seg_end[w];
-    if (!first && e_beg == e_end) return;  // nothing to add in this band
-    const int d0 = dstart[w], D = dstart[w + 1] - d0;
-    const int nent = D * K;
-    float *dst = dxs + (size_t)d0 * K;
-    for (int i = lane; i < nent; i += kWave) {
-        acc[i] = first ? 0.f : dst[i];
-        sl[i] = sel[(size_t)d0 * K + i];
-    }
-    wave_sync_lds();
     const int grp = lane / K, l = lane % K;
     // records of the next batch are prefetched while the current one gathers
     int nx_rc = 0;
@@ -799,34 +869,19 @@ __global__ __launch_bounds__(kBlock) void bwd_local_kernel(
             for (int u = 0; u < LOCAL_U; ++u) {
                 const int gi = g0 + u;
                 const int t = gi * EPS + grp;
-                int rc;
-                if constexpr (EPS == 1) {
-                    rc = __shfl(my_rc, gi);
-                    vv[u] = __shfl(my_v, gi);
-                } else if constexpr (EPS == 2) {
-                    const int ra = __shfl(my_rc, 2 * gi);
-                    const int rb = __shfl(my_rc, 2 * gi + 1);
-                    const float va = __shfl(my_v, 2 * gi);
-                    const float vb = __shfl(my_v, 2 * gi + 1);
-                    rc = grp ? rb : ra;
-                    vv[u] = grp ? vb : va;
-                    if ((2 * gi + 1 < n) && ((ra >> 24) == (rb >> 24))) clash |= 1u << u;
-                } else {
-                    rc = __shfl(my_rc, t);
-                    vv[u] = __shfl(my_v, t);
-                    bool c = false;
+                int rc = __shfl(my_rc, t);
+                vv[u] = __shfl(my_v, t);
+                bool c = false;
 #pragma unroll
-                    for (int j = 1; j < EPS; ++j) {
-                        const int other = __shfl(rc, lane >= j * K ? lane - j * K : lane);
-                        c |= (lane >= j * K) && ((other >> 24) == (rc >> 24)) && (t < n);
-                    }
-                    if (__any(c)) clash |= 1u << u;
+                for (int j = 1; j < EPS; ++j) {
+                    const int other = __shfl(rc, lane >= j * K ? lane - j * K : lane);
+                    c |= (lane >= j * K) && ((other >> 24) == (rc >> 24)) && (t < n);
                 }
+                if (__any(c)) clash |= 1u << u;
                 cc[u] = (rc >> 24) & 0xff;
                 gv[u] = 0.f;
                 if (t < n) {
-                    const int col = sl[cc[u] * K + l];
-                    gv[u] = col < dim ? grad[(size_t)(rc & 0xffffff) * dim + col] : 0.f;
+                    gv[u] = grad[(size_t)(rc & 0xffffff) * dim + sl[cc[u] * K + l]];
                 } else {
                     vv[u] = 0.f;
                     cc[u] = -1;
@@ -846,8 +901,61 @@ __global__ __launch_bounds__(kBlock) void bwd_local_kernel(
             }
         }
     }
+}
+
+template <int K, bool WIDE>
+__device__ __forceinline__ void local_edges_scalar(int e_beg, int e_end,
+                                                   const int32_t *__restrict__ erc,
+                                                   const float *__restrict__ evl,
+                                                   const float *__restrict__ grad, int dim,
+                                                   const uint8_t *sl, float *acc)
+{
+    constexpr int R = 16;
+    const int lane = lane_id();
+    const int grp = lane / K, l = lane % K;
+    const int full_end = e_beg + ((e_end - e_beg) / R) * R;
+    for (int base = e_beg; base < full_end; base += R)
+        local_round<K, WIDE>(erc + base, evl + base, grad, (uint32_t)dim, sl, acc, grp, l);
+    if (full_end < e_end) local_edges_shfl<K>(full_end, e_end, erc, evl, grad, dim, sl, acc);
+}
+
+template <int K, bool WIDE>
+__global__ __launch_bounds__(kBlock) void bwd_local_kernel(
+    const int32_t *__restrict__ seg_beg, const int32_t *__restrict__ seg_end, bool first,
+    const int32_t *__restrict__ dstart, int num_waves,
+    int dmax, const int32_t *__restrict__ erc, const float *__restrict__ evl,
+    const float *__restrict__ grad, const uint8_t *__restrict__ sel, int dim,
+    float *__restrict__ dxs)
+{
+    extern __shared__ __attribute__((aligned(16))) float lds[];
+    const int wl = __builtin_amdgcn_readfirstlane(threadIdx.x / kWave);
+    const int region = (dmax * K * 5 + 15) & ~15;  // bytes: fp32 dXs block + u8 sel block
+    float *acc = reinterpret_cast<float *>(reinterpret_cast<char *>(lds) + wl * region);
+    uint8_t *sl = reinterpret_cast<uint8_t *>(acc + dmax * K);
+    const int w = blockIdx.x * kWavesPerBlock + wl;
+    if (w >= num_waves) return;
+    const int lane = lane_id();
+    const int e_beg = __builtin_amdgcn_readfirstlane(seg_beg[w]);
+    const int e_end = __builtin_amdgcn_readfirstlane(seg_end[w]);
+    if (!first && e_beg == e_end) return;  // nothing to add in this band
+    const int d0 = dstart[w], D = dstart[w + 1] - d0;
+    const int nent = D * K;
+    float *dst = dxs + (size_t)d0 * K;
+    const uint8_t *srow = sel + (size_t)d0 * K;
+    // selector bytes are clamped into the row for the gathers; entries that
+    // were out of range are written as 0 below (they receive no contribution)
+    for (int i = lane; i < nent; i += kWave) {
+        acc[i] = first ? 0.f : dst[i];
+        const int c = srow[i];
+        sl[i] = (uint8_t)(c < dim ? c : dim - 1);
+    }
     wave_sync_lds();
-    for (int i = lane; i < nent; i += kWave) dst[i] = acc[i];
+    if constexpr (kWave / K <= 2)
+        local_edges_scalar<K, WIDE>(e_beg, e_end, erc, evl, grad, dim, sl, acc);
+    else
+        local_edges_shfl<K>(e_beg, e_end, erc, evl, grad, dim, sl, acc);
+    wave_sync_lds();
+    for (int i = lane; i < nent; i += kWave) dst[i] = srow[i] < dim ? acc[i] : 0.f;
 }
 
 // ---------------------------------------------------------------------------
@@ -962,11 +1070,13 @@ template <int K>
 struct BwdLocal {
     static int run(const int32_t *seg_off, int NS, const int32_t *dstart, int W, int dmax,
                    const int32_t *erc, const float *evl, const float *grad, const uint8_t *sel,
-                   int dim, float *dxs, hipStream_t st)
+                   int num_rows, int dim, float *dxs, hipStream_t st)
     {
         const size_t region = (size_t)((dmax * K * 5 + 15) & ~15);
+        const bool wide = (uint64_t)num_rows * (uint64_t)dim * 4u >= (1ull << 32);
         for (int s = 0; s < NS; ++s) {
-            hipLaunchKernelGGL(bwd_local_kernel<K>, dim3((unsigned)ceil_div(W, kWavesPerBlock)),
+            auto kern = wide ? bwd_local_kernel<K, true> : bwd_local_kernel<K, false>;
+            hipLaunchKernelGGL(kern, dim3((unsigned)ceil_div(W, kWavesPerBlock)),
                                dim3(kBlock), region * kWavesPerBlock, st,
                                seg_off + (size_t)s * W, seg_off + (size_t)(s + 1) * W, s == 0,
                                dstart, W, dmax, erc, evl, grad, sel, dim, dxs);
@@ -1140,7 +1250,7 @@ int maxk_sspmm_backward_local(const int32_t *seg_edge_off, int num_segments,
     if (maxk_backward_local_lds_bytes(dmax, dim_k) > 160 * 1024) return MAXK_E_WORKSPACE;
     hipStream_t st = as_stream(stream);
 #define LOCAL_ARGS seg_edge_off, num_segments, wave_dst_start, num_waves, dmax, edge_rc, edge_val, \
-                   grad, cbsr_sel, dim_origin, dxs, st
+                   grad, cbsr_sel, num_rows, dim_origin, dxs, st
     switch (dim_k) {
     case 1: return BwdLocal<1>::run(LOCAL_ARGS);
     case 2: return BwdLocal<2>::run(LOCAL_ARGS);
