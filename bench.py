@@ -104,18 +104,31 @@ def workload_key(args, bwd_algo):
     return f"{args.graph}_h{args.h}_k{args.k}_{bwd_algo}"
 
 
-def pmc_traffic(key, call):
-    """HBM bytes per launch of `call` measured by rocprofv3 PMC passes
-    (FETCH_SIZE x2 + WRITE_SIZE, MI355X_MICROARCH.md §HBM) for this exact
-    workload, from the committed profile summary (tools/profile.sh +
-    tools/summarize_profile.py); None when no such profile exists."""
+def pmc_traffic(key, call, algo=None, bands=1):
+    """HBM bytes of one hot-path call (`spgemm_forward` / `sspmm_backward`)
+    measured by rocprofv3 PMC passes (FETCH_SIZE x2 + WRITE_SIZE,
+    MI355X_MICROARCH.md §HBM) for this exact workload, from the committed
+    profile summary (tools/profile.sh + tools/summarize_profile.py): per-kernel
+    bytes per launch times the launches the call makes (the LOCAL backward
+    launches once per source band).  None when no such profile exists."""
     path = os.path.join(ROOT, "profiles", "pmc_traffic.json")
     try:
         ent = json.load(open(path))[key]
-    except (OSError, KeyError, ValueError):
+        k = ent["kernels"]
+    except (OSError, KeyError, ValueError, TypeError):
         return None, None
-    v = ent.get(call)
-    return (int(v) if v else None), f"profiles/{ent['profile']}_summary.json"
+    fix = k.get("carry_fixup_kernel", 0.0)
+    if call == "spgemm_forward":
+        parts = [k.get("fwd_panel_kernel"), fix]
+    elif algo == "local":
+        parts = [None if "bwd_local_kernel" not in k else k["bwd_local_kernel"] * bands]
+    elif algo == "staged":
+        parts = [k.get("bwd_panel_kernel"), k.get("bwd_segsum_kernel"), fix]
+    else:
+        parts = [k.get("bwd_panel_kernel")]
+    if any(p is None for p in parts):
+        return None, None
+    return int(sum(parts)), f"profiles/{ent['profile']}_summary.json"
 
 
 def _cpu_model():
@@ -253,11 +266,16 @@ def main():
         b_call = 8 * E + 5 * k * E + 4 * h * V
         dom = ("sspmm_backward", bms) if bms >= fms else ("spgemm_forward", fms)
         ach = b_call / (dom[1] / 1e3) / 1e9
-        traffic, tsrc = pmc_traffic(workload_key(args, g.last_bwd_algo), dom[0])
+        bands = 1
+        if g.last_bwd_algo == "local":
+            bands = g.local_bands(g.local_plan(k), h)[1]
+        traffic, tsrc = pmc_traffic(workload_key(args, g.last_bwd_algo), dom[0],
+                                    g.last_bwd_algo, bands)
         result["roofline"] = {"bound": "hbm", "achieved": round(ach, 1), "peak": HBM_PEAK_GBS,
                               "unit": "GB/s", "frac": round(ach / HBM_PEAK_GBS, 4),
                               "traffic": traffic, "traffic_source": tsrc, "kernel": dom[0],
-                              "algorithmic_bytes_per_launch": b_call}
+                              "algorithmic_bytes_per_launch": b_call,
+                              "launches_per_call": bands if dom[0] == "sspmm_backward" else 1}
         result["config"]["bwd_algo"] = g.last_bwd_algo
         result["fwd_ms"] = round(fms, 4)
         result["bwd_ms"] = round(bms, 4)

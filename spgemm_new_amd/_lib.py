@@ -14,7 +14,8 @@ import os
 import torch  # noqa: F401  -- must be imported first so its HIP runtime is the one we bind to
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "lib", "libmaxk_spgemm.so")
+# MAXK_LIB overrides the library path (variant builds in development tools)
+LIB_PATH = os.environ.get("MAXK_LIB") or os.path.join(_HERE, "lib", "libmaxk_spgemm.so")
 SOURCES = [os.path.join(_HERE, "csrc", "maxk_spgemm.hip")]
 HEADER = os.path.join(os.path.dirname(_HERE), "include", "maxk_spgemm.h")
 

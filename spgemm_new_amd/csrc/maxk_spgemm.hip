@@ -743,6 +743,9 @@ __global__ __launch_bounds__(kBlock) void bwd_warp4_kernel(
 #ifndef LOCAL_U
 #define LOCAL_U 8
 #endif
+#ifndef LOCAL_R
+#define LOCAL_R 16  // edge records per SGPR round (k = 32, 64)
+#endif
 
 // Offset (in floats) of G[row, col] -> element pointer; 32-bit byte offsets
 // (global_load saddr form) when the whole gradient array is below 4 GiB.
@@ -769,7 +772,7 @@ __device__ __forceinline__ void local_round(const int32_t *__restrict__ rec_rc,
                                             const uint8_t *sl, float *acc, int grp, int l)
 {
     constexpr int EPS = kWave / K;
-    constexpr int R = 16;
+    constexpr int R = LOCAL_R;
     constexpr int NG = R / EPS;
     float gv[NG], vv[NG];
     int ai[NG];
@@ -788,10 +791,14 @@ __device__ __forceinline__ void local_round(const int32_t *__restrict__ rec_rc,
         vbits[i] = __builtin_bit_cast(uint32_t, rec_v[i]);
     }
     // materialise all records here (two s_load_dwordx16, one wait)
-    asm volatile("" : "+s"(rcs[0]), "+s"(rcs[1]), "+s"(rcs[2]), "+s"(rcs[3]), "+s"(rcs[4]),
-                 "+s"(rcs[5]), "+s"(rcs[6]), "+s"(rcs[7]), "+s"(rcs[8]), "+s"(rcs[9]),
-                 "+s"(rcs[10]), "+s"(rcs[11]), "+s"(rcs[12]), "+s"(rcs[13]), "+s"(rcs[14]),
-                 "+s"(rcs[15]));
+    static_assert(R % 16 == 0, "records are pinned 16 at a time");
+#pragma unroll
+    for (int c = 0; c < R; c += 16) {
+        int32_t *q = rcs + c;
+        asm volatile("" : "+s"(q[0]), "+s"(q[1]), "+s"(q[2]), "+s"(q[3]), "+s"(q[4]), "+s"(q[5]),
+                     "+s"(q[6]), "+s"(q[7]), "+s"(q[8]), "+s"(q[9]), "+s"(q[10]), "+s"(q[11]),
+                     "+s"(q[12]), "+s"(q[13]), "+s"(q[14]), "+s"(q[15]));
+    }
     const uint32_t m = hi ? 0xffffffffu : 0u;
 #pragma unroll
     for (int u = 0; u < NG; ++u) {
@@ -910,7 +917,7 @@ __device__ __forceinline__ void local_edges_scalar(int e_beg, int e_end,
                                                    const float *__restrict__ grad, int dim,
                                                    const uint8_t *sl, float *acc)
 {
-    constexpr int R = 16;
+    constexpr int R = LOCAL_R;
     const int lane = lane_id();
     const int grp = lane / K, l = lane % K;
     const int full_end = e_beg + ((e_end - e_beg) / R) * R;

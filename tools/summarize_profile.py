@@ -61,23 +61,15 @@ def main(tag: str, root: str = ".", workload: str | None = None):
             row["l2_hit_rate"] = row["TCC_HIT_sum"] / t if t else None
         out["kernels"][n] = row
     json.dump(out, open(os.path.join(dst, f"{tag}_summary.json"), "w"), indent=1)
-    if workload:  # per-launch HBM traffic per hot-path call, read by bench.py
+    if workload:  # per-launch HBM traffic of each kernel, read by bench.py
         idx_path = os.path.join(dst, "pmc_traffic.json")
         idx = json.load(open(idx_path)) if os.path.exists(idx_path) else {}
         k = out["kernels"]
 
-        def call_bytes(names):
-            tot = 0.0
-            for n in names:
-                if n in k and "hbm_read_bytes_x2" in k[n] and "hbm_write_bytes" in k[n]:
-                    per = k[n]["hbm_read_bytes_x2"] + k[n]["hbm_write_bytes"]
-                    # fixup runs once per forward and once per backward call
-                    tot += per * (0.5 if n == "carry_fixup_kernel" else 1.0)
-            return tot
-        idx[workload] = {"profile": tag,
-                         "spgemm_forward": call_bytes(["fwd_panel_kernel", "carry_fixup_kernel"]),
-                         "sspmm_backward": call_bytes(["bwd_panel_kernel", "bwd_segsum_kernel",
-                                                       "carry_fixup_kernel", "bwd_local_kernel"])}
+        per_launch = {n: r["hbm_read_bytes_x2"] + r["hbm_write_bytes"] for n, r in k.items()
+                      if "hbm_read_bytes_x2" in r and "hbm_write_bytes" in r}
+        # bench.py composes a call's traffic from these (launches per call known there)
+        idx[workload] = {"profile": tag, "kernels": per_launch}
         json.dump(idx, open(idx_path, "w"), indent=1)
     with open(os.path.join(dst, f"{tag}_summary.md"), "w") as fh:
         fh.write(f"# rocprofv3 summary `{tag}`\n\nSource: `tools/profile.sh {tag}` "
