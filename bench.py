@@ -146,7 +146,7 @@ def main():
     import spgemm_new_amd as S
     from spgemm_new_amd import _lib
     from spgemm_new_amd.graphs import CONFIGS, synthetic_csr_gpu
-    from spgemm_new_amd.models import cbsr_topk
+    from spgemm_new_amd.ops import topk_cbsr
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
@@ -173,7 +173,7 @@ def main():
     values = torch.rand(E, generator=gen, device=dev)          # main.cu:83-84 U(0,1)
     X = torch.rand((V, h), generator=gen, device=dev)
     G = torch.rand((V, h), generator=gen, device=dev)
-    data, sel = cbsr_topk(X, k)
+    data, sel = topk_cbsr(X, k, order="column")  # HIP CBSR producer
     log(f"[bench] graph {args.graph} V={V} E={E} built in {time.time() - t0:.1f}s")
 
     algo = {"auto": _lib.MAXK_BWD_AUTO, "atomic": _lib.MAXK_BWD_ATOMIC,
@@ -281,6 +281,21 @@ def main():
         result["bwd_ms"] = round(bms, 4)
         result["fwd_GBs"] = round(b_call / fms / 1e6, 1)
         result["bwd_GBs"] = round(b_call / bms / 1e6, 1)
+        # reported separately: CBSR producer and dense-gradient scatter
+        from spgemm_new_amd.ops import cbsr_scatter
+
+        def ev_ms(fn, reps=5):
+            fn()
+            a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            a.record(st)
+            for _ in range(reps):
+                fn()
+            b.record(st)
+            b.synchronize()
+            return a.elapsed_time(b) / reps
+        dx_tmp = torch.empty((V, k), device=dev)
+        result["topk_ms"] = round(ev_ms(lambda: topk_cbsr(X, k, order="column")), 4)
+        result["scatter_ms"] = round(ev_ms(lambda: cbsr_scatter(dx_tmp, sel, h)), 4)
         if not args.no_cpu_baseline and rank == 0:
             mask = torch.zeros((V, h), device=dev)
             mask.scatter_(1, sel.long(), 1.0)

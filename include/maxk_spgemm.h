@@ -127,6 +127,30 @@ int maxk_sspmm_backward_local(const int32_t *seg_edge_off, int num_segments,
                               float *dxs, void *stream);
 
 /* ---------------------------------------------------------------------------
+ * CBSR producer (MaxK top-k) and dense-gradient scatter.
+ * Replace torch.topk in the CBSR producers (direct_kernel_interface.py:58-85,
+ * kernels/spmm_bindings.cpp:163-184, utils/models.py:72) and the host scatter
+ * loop of SpGEMMFunction.backward (utils/models.py:136-141).
+ *   maxk_topk_cbsr: per row of x (num_rows x dim, row stride ld floats,
+ *   dim <= 256) the k largest entries -> cbsr_data[r, j] = x[r, cbsr_sel[r, j]]
+ *   (num_rows x k, fp32 / uint8).  NaN counts as the largest value, -0 == +0,
+ *   ties at the k-th value go to the lower column.  order: COLUMN = ascending
+ *   column, VALUE = descending value (torch.topk's sorted order).  dense_out
+ *   (nullable, num_rows x dim): the MaxK forward (selected kept, rest 0).
+ *   maxk_cbsr_scatter: out[r, :] = 0 except out[r, cbsr_sel[r, j]] = vals[r, j].
+ *   maxk_cbsr_mask: out[r, :] = 0 except out[r, c] = src[r, c] for c in
+ *   cbsr_sel[r, :] (src, out: num_rows x dim) -- the MaxK backward.
+ * ------------------------------------------------------------------------- */
+#define MAXK_TOPK_ORDER_COLUMN 0
+#define MAXK_TOPK_ORDER_VALUE 1
+int maxk_topk_cbsr(const float *x, int num_rows, int dim, int64_t ld, int k, int order,
+                   float *cbsr_data, uint8_t *cbsr_sel, float *dense_out, void *stream);
+int maxk_cbsr_scatter(const float *vals, const uint8_t *cbsr_sel, int num_rows, int k, int dim,
+                      float *out, void *stream);
+int maxk_cbsr_mask(const float *src, const uint8_t *cbsr_sel, int num_rows, int k, int dim,
+                   float *out, void *stream);
+
+/* ---------------------------------------------------------------------------
  * Exact drop-ins for the reference's extern "C" launchers
  * (cuda_kernel_wrappers.cu:38-56 and :58-76), minus the CUDA launch geometry
  * (grid/block/shared_size), which the implementation chooses.  They consume

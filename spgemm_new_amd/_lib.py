@@ -27,6 +27,8 @@ MAXK_BWD_AUTO = 0
 MAXK_BWD_ATOMIC = 1
 MAXK_BWD_STAGED = 2
 MAXK_BWD_LOCAL = 3
+MAXK_TOPK_ORDER_COLUMN = 0
+MAXK_TOPK_ORDER_VALUE = 1
 DEFAULT_PANEL_COST = 2048
 DEFAULT_ROW_COST = 16
 
@@ -50,6 +52,9 @@ SIGNATURES = {
                                  _L, _P, _P, _S, _P]),
     "maxk_backward_local_lds_bytes": (_S, [_I, _I]),
     "maxk_sspmm_backward_local": (_I, [_P, _I, _P, _I, _I, _P, _P, _P, _P, _I, _I, _I, _P, _P]),
+    "maxk_topk_cbsr": (_I, [_P, _I, _I, _L, _I, _I, _P, _P, _P, _P]),
+    "maxk_cbsr_scatter": (_I, [_P, _P, _I, _I, _I, _P, _P]),
+    "maxk_cbsr_mask": (_I, [_P, _P, _I, _I, _I, _P, _P]),
     "maxk_spmm_forward_warp4": (_I, [_P, _P, _P, _P, _P, _P, _I, _I, _I, _I, _I, _P]),
     "maxk_spmm_backward_warp4": (_I, [_P, _P, _P, _P, _P, _P, _I, _I, _I, _I, _I, _P]),
 }

@@ -1,0 +1,259 @@
+// maxk_topk.hip -- MI355X (gfx950) CBSR producer and dense-gradient scatter.
+//
+// The MaxK nonlinearity keeps the k largest entries of each feature row
+// (reference: utils/models.py:28-59 MaxK, and the CBSR producers
+// direct_kernel_interface.py:58-85 / kernels/spmm_bindings.cpp:163-184, all
+// torch.topk(X, k, dim=1)).  The SpGEMM consumes them as CBSR: data[r, j] =
+// X[r, sel[r, j]], sel uint8.  SpGEMMFunction's backward scatters the
+// k-column gradient back to a dense row (utils/models.py:136-141).
+//
+// topk_kernel: one wave64 per row (dim <= 256: each lane holds 4 entries,
+// loaded as one float4 when the row allows).  Entries map to order-preserving
+// u32 keys (NaN = the largest key, as torch.topk treats NaN; -0 == +0).  The
+// k-th largest key T comes from a 32-step bitwise search: per step, four
+// v_cmp produce lane masks and s_bcnt1 counts them (no LDS, no sort).
+// Selected = key > T, plus the lowest-column entries with key == T until k
+// are taken (ties go to the lower column).  Output order:
+//   column order: ascending column (prefix counts with v_mbcnt);
+//   value order:  descending value, ties by lower column -- torch.topk's
+//                 sorted order -- by ranking each selected entry against the
+//                 row's k selected (key, column) pairs staged in LDS.
+// An optional dense output receives the MaxK forward (selected entries kept,
+// the rest 0), utils/models.py:44-50.
+//
+// scatter_kernel: out[r, :] = 0 except out[r, sel[r, j]] = vals[r, j] (or
+// src[r, sel[r, j]] for the masked copy) -- the row is assembled in LDS and
+// leaves as one coalesced store per lane.
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "../../include/maxk_spgemm.h"
+
+namespace {
+
+constexpr int kWave = 64;
+constexpr int kWavesPerBlock = 4;
+constexpr int kBlock = kWave * kWavesPerBlock;
+constexpr int kMaxDim = 256;
+
+__device__ __forceinline__ void wave_sync_lds()
+{
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+__device__ __forceinline__ uint32_t float_key(float x)
+{
+    if (x != x) return 0xffffffffu;      // NaN: largest
+    if (x == 0.f) x = 0.f;               // -0 -> +0
+    const uint32_t u = __builtin_bit_cast(uint32_t, x);
+    return (u & 0x80000000u) ? ~u : (u | 0x80000000u);
+}
+
+__device__ __forceinline__ int popc64(uint64_t m) { return __builtin_popcountll(m); }
+
+// lanes below this one whose bit is set in m
+__device__ __forceinline__ int prefix_count(uint64_t m)
+{
+    return __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32),
+                                     __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0));
+}
+
+template <bool VALUE_ORDER>
+__global__ __launch_bounds__(kBlock) void topk_kernel(const float *__restrict__ x, int num_rows,
+                                                      int dim, int64_t ld, int k,
+                                                      float *__restrict__ data,
+                                                      uint8_t *__restrict__ sel,
+                                                      float *__restrict__ dense)
+{
+    __shared__ uint64_t stage[kWavesPerBlock][kMaxDim];  // value order: (key << 32 | ~col)
+    const int lane = threadIdx.x & (kWave - 1);
+    const int wl = threadIdx.x / kWave;
+    const int64_t nwaves = (int64_t)gridDim.x * kWavesPerBlock;
+    const bool vec = (dim & 3) == 0 && (ld & 3) == 0;
+    for (int64_t r = (int64_t)blockIdx.x * kWavesPerBlock + wl; r < num_rows; r += nwaves) {
+        const float *row = x + r * ld;
+        float v[4];
+        uint32_t key[4];
+        if (vec && 4 * lane < dim) {
+            const float4 q = *reinterpret_cast<const float4 *>(row + 4 * lane);
+            v[0] = q.x; v[1] = q.y; v[2] = q.z; v[3] = q.w;
+        } else {
+#pragma unroll
+            for (int j = 0; j < 4; ++j) v[j] = (4 * lane + j < dim) ? row[4 * lane + j] : 0.f;
+        }
+#pragma unroll
+        for (int j = 0; j < 4; ++j) key[j] = (4 * lane + j < dim) ? float_key(v[j]) : 0u;
+        // largest T with #{key >= T} >= k (every valid key is >= 0x007fffff > 0)
+        uint32_t T = 0;
+        for (int b = 31; b >= 0; --b) {
+            const uint32_t cand = T | (1u << b);
+            int cnt = 0;
+#pragma unroll
+            for (int j = 0; j < 4; ++j) cnt += popc64(__ballot(key[j] >= cand));
+            if (cnt >= k) T = cand;
+        }
+        uint64_t gt[4], eq[4];
+        int n_gt = 0;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            gt[j] = __ballot(key[j] > T);
+            eq[j] = __ballot(key[j] == T && 4 * lane + j < dim);
+            n_gt += popc64(gt[j]);
+        }
+        const int need = k - n_gt;  // ties to take, lowest column first
+        int eq_before = 0;          // ties at lower columns than this lane's first entry
+#pragma unroll
+        for (int j = 0; j < 4; ++j) eq_before += prefix_count(eq[j]);
+        bool take[4];
+        int mine = 0;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            const bool t = (eq[j] >> lane) & 1;
+            take[j] = ((gt[j] >> lane) & 1) || (t && eq_before < need);
+            eq_before += t;
+        }
+        // column-order position: selected entries at lower columns
+        uint64_t sm[4];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) sm[j] = __ballot(take[j]);
+        int pos = 0;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) pos += prefix_count(sm[j]);
+        float *drow = data + r * (int64_t)k;
+        uint8_t *srow = sel + r * (int64_t)k;
+        if constexpr (!VALUE_ORDER) {
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                if (take[j]) {
+                    drow[pos + mine] = v[j];
+                    srow[pos + mine] = (uint8_t)(4 * lane + j);
+                    ++mine;
+                }
+            }
+        } else {
+            uint64_t *st = stage[wl];
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                if (take[j]) {
+                    st[pos + mine] = ((uint64_t)key[j] << 32) | (uint32_t)~(uint32_t)(4 * lane + j);
+                    ++mine;
+                }
+            }
+            wave_sync_lds();
+            // rank = #selected entries ordered before this one (key desc, column asc)
+            mine = 0;
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                if (take[j]) {
+                    const uint64_t me = st[pos + mine];
+                    int rank = 0;
+                    for (int t = 0; t < k; ++t) rank += st[t] > me;
+                    drow[rank] = v[j];
+                    srow[rank] = (uint8_t)(4 * lane + j);
+                    ++mine;
+                }
+            }
+            wave_sync_lds();
+        }
+        if (dense) {
+            float *orow = dense + r * (int64_t)dim;
+#pragma unroll
+            for (int j = 0; j < 4; ++j)
+                if (4 * lane + j < dim) orow[4 * lane + j] = take[j] ? v[j] : 0.f;
+        }
+    }
+}
+
+// DENSE_SRC: vals is a dense [num_rows, dim] array read at the selected
+// columns (MaxK backward: grad masked to the top-k), else [num_rows, k].
+template <bool DENSE_SRC>
+__global__ __launch_bounds__(kBlock) void scatter_kernel(const float *__restrict__ vals,
+                                                         const uint8_t *__restrict__ sel,
+                                                         int num_rows, int k, int dim,
+                                                         float *__restrict__ out)
+{
+    __shared__ float rowbuf[kWavesPerBlock][kMaxDim];
+    const int lane = threadIdx.x & (kWave - 1);
+    const int wl = threadIdx.x / kWave;
+    float *rb = rowbuf[wl];
+    const int64_t nwaves = (int64_t)gridDim.x * kWavesPerBlock;
+    for (int64_t r = (int64_t)blockIdx.x * kWavesPerBlock + wl; r < num_rows; r += nwaves) {
+        for (int i = lane; i < dim; i += kWave) rb[i] = 0.f;
+        wave_sync_lds();
+        for (int j = lane; j < k; j += kWave) {
+            const int c = sel[r * (int64_t)k + j];
+            if (c < dim) rb[c] = DENSE_SRC ? vals[r * (int64_t)dim + c] : vals[r * (int64_t)k + j];
+        }
+        wave_sync_lds();
+        float *orow = out + r * (int64_t)dim;
+        if ((dim & 3) == 0) {
+            if (4 * lane < dim)
+                reinterpret_cast<float4 *>(orow)[lane] = reinterpret_cast<const float4 *>(rb)[lane];
+        } else {
+            for (int i = lane; i < dim; i += kWave) orow[i] = rb[i];
+        }
+        wave_sync_lds();
+    }
+}
+
+inline int launch_status()
+{
+    const hipError_t e = hipGetLastError();
+    return e == hipSuccess ? MAXK_OK : (int)e;
+}
+
+inline unsigned grid_for(int num_rows)
+{
+    // enough waves to fill 256 CUs x 8 waves; rows beyond are grid-strided
+    const int64_t blocks = ((int64_t)num_rows + kWavesPerBlock - 1) / kWavesPerBlock;
+    return (unsigned)(blocks < 2048 ? blocks : 2048);
+}
+
+}  // namespace
+
+extern "C" {
+
+int maxk_topk_cbsr(const float *x, int num_rows, int dim, int64_t ld, int k, int order,
+                   float *cbsr_data, uint8_t *cbsr_sel, float *dense_out, void *stream)
+{
+    if (num_rows < 0 || (num_rows > 0 && (!x || !cbsr_data || !cbsr_sel))) return MAXK_E_ARG;
+    if (dim < 1 || dim > kMaxDim || k < 1 || k > dim || ld < dim) return MAXK_E_DIM;
+    if (order != MAXK_TOPK_ORDER_COLUMN && order != MAXK_TOPK_ORDER_VALUE) return MAXK_E_ARG;
+    if (num_rows == 0) return MAXK_OK;
+    hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+    if (order == MAXK_TOPK_ORDER_VALUE)
+        hipLaunchKernelGGL(topk_kernel<true>, dim3(grid_for(num_rows)), dim3(kBlock), 0, st, x,
+                           num_rows, dim, ld, k, cbsr_data, cbsr_sel, dense_out);
+    else
+        hipLaunchKernelGGL(topk_kernel<false>, dim3(grid_for(num_rows)), dim3(kBlock), 0, st, x,
+                           num_rows, dim, ld, k, cbsr_data, cbsr_sel, dense_out);
+    return launch_status();
+}
+
+int maxk_cbsr_scatter(const float *vals, const uint8_t *cbsr_sel, int num_rows, int k, int dim,
+                      float *out, void *stream)
+{
+    if (num_rows < 0 || (num_rows > 0 && (!vals || !cbsr_sel || !out))) return MAXK_E_ARG;
+    if (dim < 1 || dim > kMaxDim || k < 1 || k > dim) return MAXK_E_DIM;
+    if (num_rows == 0) return MAXK_OK;
+    hipLaunchKernelGGL(scatter_kernel<false>, dim3(grid_for(num_rows)), dim3(kBlock), 0,
+                       reinterpret_cast<hipStream_t>(stream), vals, cbsr_sel, num_rows, k, dim,
+                       out);
+    return launch_status();
+}
+
+int maxk_cbsr_mask(const float *src, const uint8_t *cbsr_sel, int num_rows, int k, int dim,
+                   float *out, void *stream)
+{
+    if (num_rows < 0 || (num_rows > 0 && (!src || !cbsr_sel || !out))) return MAXK_E_ARG;
+    if (dim < 1 || dim > kMaxDim || k < 1 || k > dim) return MAXK_E_DIM;
+    if (num_rows == 0) return MAXK_OK;
+    hipLaunchKernelGGL(scatter_kernel<true>, dim3(grid_for(num_rows)), dim3(kBlock), 0,
+                       reinterpret_cast<hipStream_t>(stream), src, cbsr_sel, num_rows, k, dim,
+                       out);
+    return launch_status();
+}
+
+}  // extern "C"

@@ -21,7 +21,7 @@ import numpy as np
 import torch
 
 from . import _lib
-from .ops import MaxKGraph, check_tensor, warp4_build
+from .ops import MaxKGraph, check_tensor, topk_cbsr, warp4_build
 
 FULL_DIM = 256  # cuda_kernel_bindings.cpp:70
 
@@ -134,7 +134,11 @@ def cuda_topk_maxk_float(input, k: int):
     check_tensor(input, "Input", dim=2)
     if not (0 < k <= input.size(1)):
         raise RuntimeError("Invalid k value")
-    vals, idx = torch.topk(input.float() if input.dtype != torch.float32 else input, k, dim=1)
+    x = input.float() if input.dtype != torch.float32 else input
+    if x.size(1) <= 256:
+        vals, idx = topk_cbsr(x.contiguous(), k, order="value")  # HIP producer
+        return vals, idx.to(torch.int32)
+    vals, idx = torch.topk(x, k, dim=1)  # dim > 256: outside the kernels' range
     return vals.contiguous(), idx.to(torch.int32).contiguous()
 
 

@@ -3,12 +3,13 @@
 ``MaxK.apply(x, k)`` and ``SpGEMMFunction.apply(features, (indptr, indices,
 values), maxk)`` have the reference's names, arguments and return values, so
 the training loop (maxk_gnn_integrated.py, SAGE.forward utils/models.py:230)
-calls them unchanged.  The hot path is the HIP SpGEMM / SSpMM; the CBSR
-producer is torch.topk (SURVEY.md §8f1 lists a fused HIP top-k as next).
+calls them unchanged.  Every step runs in the HIP library: the top-k CBSR
+producer (maxk_topk_cbsr, replacing torch.topk), the SpGEMM / SSpMM, and the
+sparse->dense gradient scatter / MaxK mask (maxk_cbsr_scatter / _mask).
 
 Fixed relative to the reference: the kernel path actually runs,
 there is no per-layer debug copy, and the sparse->dense gradient scatter is a
-single on-device scatter instead of a V*k Python loop (utils/models.py:136-141).
+single device kernel instead of a V*k Python loop (utils/models.py:136-141).
 No fallback: if the HIP library is missing the call raises.
 """
 from __future__ import annotations
@@ -17,6 +18,7 @@ import torch
 from torch.autograd import Function
 
 from .graph_cache import graph_for
+from .ops import cbsr_mask, cbsr_scatter, topk_cbsr
 
 
 class MaxK(Function):
@@ -24,6 +26,14 @@ class MaxK(Function):
 
     @staticmethod
     def forward(ctx, input, k=1):
+        ctx.hip = input.is_cuda and input.dtype == torch.float32 and input.dim() == 2 \
+            and input.size(1) <= 256
+        if ctx.hip:
+            _, sel, out = topk_cbsr(input.contiguous(), k, dense=True)
+            ctx.save_for_backward(sel)
+            return out
+        # other dtypes / widths are outside the kernels' domain: the reference's
+        # own formulation (utils/models.py:44-50) on the tensor's device
         _, indices = input.topk(k, dim=1)
         mask = torch.zeros_like(input)
         mask.scatter_(1, indices, 1)
@@ -32,14 +42,16 @@ class MaxK(Function):
 
     @staticmethod
     def backward(ctx, grad_output):
-        (mask,) = ctx.saved_tensors
-        return grad_output * mask, None
+        (saved,) = ctx.saved_tensors
+        if ctx.hip:
+            return cbsr_mask(grad_output.contiguous(), saved), None
+        return grad_output * saved, None
 
 
-def cbsr_topk(features: torch.Tensor, maxk: int):
-    """(data fp32[V,k], sel uint8[V,k]) = top-k of each row (direct_kernel_interface.py:79-83)."""
-    vals, idx = torch.topk(features, maxk, dim=1)
-    return vals.contiguous(), idx.to(torch.uint8).contiguous()
+def cbsr_topk(features: torch.Tensor, maxk: int, order: str = "value"):
+    """(data fp32[V,k], sel uint8[V,k]) = top-k of each row (direct_kernel_interface.py:79-83),
+    by the HIP producer; order="value" is torch.topk's sorted order."""
+    return topk_cbsr(features.contiguous(), maxk, order=order)
 
 
 class SpGEMMFunction(Function):
@@ -51,7 +63,7 @@ class SpGEMMFunction(Function):
         if features.dim() != 2:
             raise RuntimeError("features must be 2D")
         x = features.contiguous()
-        data, sel = cbsr_topk(x, maxk)
+        data, sel = topk_cbsr(x, maxk, order="column")
         g = graph_for(indptr.contiguous(), indices.contiguous(), values.contiguous())
         out = g.forward(data, sel, dim_origin=x.size(1))
         ctx.graph = g
@@ -65,7 +77,4 @@ class SpGEMMFunction(Function):
         g = ctx.graph
         sel = ctx.sparse_selector
         dxs = g.backward(grad_output.contiguous(), sel)
-        grad_input = torch.zeros(ctx.features_shape, dtype=grad_output.dtype,
-                                 device=grad_output.device)
-        grad_input.scatter_(1, sel.long(), dxs)
-        return grad_input, None, None
+        return cbsr_scatter(dxs, sel, ctx.features_shape[1]), None, None

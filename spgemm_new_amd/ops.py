@@ -21,7 +21,8 @@ import torch
 
 from . import _lib
 
-__all__ = ["MaxKGraph", "check_tensor", "spgemm_forward", "sspmm_backward", "warp4_build"]
+__all__ = ["MaxKGraph", "check_tensor", "spgemm_forward", "sspmm_backward", "warp4_build",
+           "topk_cbsr", "cbsr_scatter", "cbsr_mask"]
 
 
 def check_tensor(t, name: str, dtype=None, cuda: bool = True, dim: int | None = None):
@@ -377,3 +378,73 @@ def warp4_build(indptr: torch.Tensor, warp_max_nz: int = 64) -> torch.Tensor:
     _lib.check(L.maxk_warp4_build(indptr.data_ptr(), V, warp_max_nz, scratch.data_ptr(),
                                   warp4.data_ptr(), W, ctypes.byref(n), st), "maxk_warp4_build")
     return warp4[: 4 * W]
+
+
+# ----------------------------------------------------------------- CBSR producer
+_TOPK_ORDERS = {"column": _lib.MAXK_TOPK_ORDER_COLUMN, "value": _lib.MAXK_TOPK_ORDER_VALUE}
+
+
+def topk_cbsr(x: torch.Tensor, k: int, order: str = "column", dense: bool = False,
+              data: torch.Tensor | None = None, sel: torch.Tensor | None = None):
+    """CBSR of the row-wise top-k of x (fp32[V, h], h <= 256): (data fp32[V,k],
+    sel uint8[V,k]) with data[r, j] = x[r, sel[r, j]]; with dense=True also the
+    MaxK forward (top-k kept, rest 0).  Replaces torch.topk in the reference's
+    producers (direct_kernel_interface.py:79-83, spmm_bindings.cpp:163-184,
+    utils/models.py:44-50).  order="column": ascending column; "value":
+    descending value as torch.topk(sorted=True), ties to the lower column.
+    NaN ranks as the largest value."""
+    check_tensor(x, "input", torch.float32, dim=2)
+    V, h = x.shape
+    if not 1 <= k <= h or h > 256:
+        raise RuntimeError(f"top-k needs 1 <= k <= dim <= 256 (k={k}, dim={h})")
+    if order not in _TOPK_ORDERS:
+        raise RuntimeError(f"order must be one of {sorted(_TOPK_ORDERS)}")
+    if data is None:
+        data = torch.empty((V, k), dtype=torch.float32, device=x.device)
+    if sel is None:
+        sel = torch.empty((V, k), dtype=torch.uint8, device=x.device)
+    check_tensor(data, "cbsr_data", torch.float32, dim=2)
+    check_tensor(sel, "cbsr_sel", torch.uint8, dim=2)
+    if tuple(data.shape) != (V, k) or tuple(sel.shape) != (V, k):
+        raise RuntimeError("cbsr_data / cbsr_sel must be [V, k]")
+    out = torch.empty_like(x) if dense else None
+    L = _lib.load()
+    _lib.check(L.maxk_topk_cbsr(x.data_ptr(), V, h, h, k, _TOPK_ORDERS[order], data.data_ptr(),
+                                sel.data_ptr(), _lib.ptr(out), _stream(x)), "maxk_topk_cbsr")
+    return (data, sel, out) if dense else (data, sel)
+
+
+def cbsr_scatter(vals: torch.Tensor, sel: torch.Tensor, dim: int,
+                 out: torch.Tensor | None = None) -> torch.Tensor:
+    """Dense fp32[V, dim] with out[r, sel[r, j]] = vals[r, j], 0 elsewhere: the
+    sparse->dense gradient of SpGEMMFunction.backward (utils/models.py:136-141)."""
+    check_tensor(vals, "vals", torch.float32, dim=2)
+    check_tensor(sel, "sparse_selector", torch.uint8, dim=2)
+    if vals.shape != sel.shape:
+        raise RuntimeError("vals and sparse_selector must have the same shape")
+    V, k = sel.shape
+    if out is None:
+        out = torch.empty((V, dim), dtype=torch.float32, device=vals.device)
+    check_tensor(out, "output", torch.float32, dim=2)
+    if tuple(out.shape) != (V, dim):
+        raise RuntimeError("output must be [V, dim]")
+    L = _lib.load()
+    _lib.check(L.maxk_cbsr_scatter(vals.data_ptr(), sel.data_ptr(), V, k, dim, out.data_ptr(),
+                                   _stream(vals)), "maxk_cbsr_scatter")
+    return out
+
+
+def cbsr_mask(src: torch.Tensor, sel: torch.Tensor, out: torch.Tensor | None = None) -> torch.Tensor:
+    """src masked to the selected columns (the MaxK backward, utils/models.py:52-59)."""
+    check_tensor(src, "grad_output", torch.float32, dim=2)
+    check_tensor(sel, "sparse_selector", torch.uint8, dim=2)
+    V, dim = src.shape
+    if sel.shape[0] != V:
+        raise RuntimeError("sparse_selector rows must match grad_output rows")
+    if out is None:
+        out = torch.empty_like(src)
+    check_tensor(out, "output", torch.float32, dim=2)
+    L = _lib.load()
+    _lib.check(L.maxk_cbsr_mask(src.data_ptr(), sel.data_ptr(), V, sel.shape[1], dim,
+                                out.data_ptr(), _stream(src)), "maxk_cbsr_mask")
+    return out

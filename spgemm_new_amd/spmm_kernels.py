@@ -15,7 +15,7 @@ import time
 import torch
 
 from .graph_cache import graph_for
-from .ops import check_tensor
+from .ops import check_tensor, topk_cbsr
 
 
 def _sel_u8(sparse_selector):
@@ -96,7 +96,10 @@ def prepare_cbsr_format(features, maxk: int):
     check_tensor(features, "Features", dim=2)
     if not (0 < maxk <= features.size(1)):
         raise RuntimeError("Invalid maxk value")
-    vals, idx = torch.topk(features, maxk, dim=1)
+    if features.dtype == torch.float32 and features.size(1) <= 256:
+        vals, idx = topk_cbsr(features.contiguous(), maxk, order="value")  # HIP producer
+        return vals, idx.to(torch.int32)
+    vals, idx = torch.topk(features, maxk, dim=1)  # dim > 256: outside the kernels' range
     return vals.contiguous(), idx.to(torch.int32).contiguous()
 
 
@@ -105,6 +108,8 @@ def topk_nonlinearity(input, k: int):
     check_tensor(input, "Input", dim=2)
     if not (0 < k <= input.size(1)):
         raise RuntimeError("Invalid k value")
+    if input.dtype == torch.float32 and input.size(1) <= 256:
+        return topk_cbsr(input.contiguous(), k, dense=True)[2]  # HIP producer, dense form
     vals, idx = torch.topk(input, k, dim=1)
     out = torch.zeros_like(input)
     out.scatter_(1, idx, vals)
