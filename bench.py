@@ -45,6 +45,9 @@ def parse():
     p.add_argument("--partitioned", action="store_true",
                    help="use the multi-GPU (row partition + halo exchange) path even at N=1")
     p.add_argument("--verbose", action="store_true")
+    p.add_argument("--relations", type=int, default=1,
+                   help="R > 1: BASELINE config 5, the fused R-relation forward "
+                        "(use with --graph proteins) vs R single-relation forwards")
     return p.parse_args()
 
 
@@ -141,6 +144,59 @@ def _cpu_model():
     return "unknown"
 
 
+def bench_multi(args, S, indptr, indices, data, sel, V, E, h, k, dev, world):
+    """BASELINE config 5 (ogbn-proteins, R edge-feature relations): the fused
+    multi-relation forward Y[q] = A_q . X^ (one CSR + CBSR gather shared by R
+    relations) timed against R single-relation forwards.  Bytes per fused call
+    (SURVEY.md §8d): E*(4 + 4R + 5k) + R*4hV; unfused: R*(8E + 5kE + 4hV)."""
+    R = args.relations
+    gen = torch.Generator(device=dev)
+    gen.manual_seed(args.seed + 7)
+    vals = torch.rand((E, R), generator=gen, device=dev)
+    cols = [vals[:, q].contiguous() for q in range(R)]
+    g = S.MaxKGraph(indptr, indices, cols[0])
+    y = torch.empty((R, V, h), device=dev)
+
+    def fused():
+        g.forward_multi(data, sel, vals, h, out=y)
+
+    def unfused():
+        for q in range(R):
+            g.forward(data, sel, h, out=y[q], values=cols[q])
+
+    def timed(fn):
+        for _ in range(args.warmup):
+            fn()
+        st = torch.cuda.current_stream()
+        a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        a.record(st)
+        for _ in range(args.steps):
+            fn()
+        b.record(st)
+        b.synchronize()
+        return a.elapsed_time(b) / args.steps
+    t_f, t_u = timed(fused), timed(unfused)
+    b_fused = E * (4 + 4 * R + 5 * k) + R * 4 * h * V
+    b_unf = R * (8 * E + 5 * k * E + 4 * h * V)
+    val = b_fused / (t_f / 1e3) / 1e9
+    result = {
+        "metric": f"fused {R}-relation SpGEMM forward GB/s, {args.graph} h={h} k={k}",
+        "value": round(val, 2), "unit": "GB/s", "n_gpus": world, "steps": args.steps,
+        "warmup": args.warmup, "ms_per_step": round(t_f, 4), "higher_is_better": True,
+        "scaling": "strong", "vs_baseline": None, "dtype": "fp32",
+        "data": "synthetic (power-law degrees, uniform columns, seed 123; values/X U(0,1))",
+        "config": {"workload": f"{args.graph} fused multi-relation forward", "graph": args.graph,
+                   "num_nodes": V, "num_edges": E, "hidden": h, "k": k, "relations": R,
+                   "parallelism": "single"},
+        "roofline": {"bound": "hbm", "achieved": round(val, 1), "peak": HBM_PEAK_GBS,
+                     "unit": "GB/s", "frac": round(val / HBM_PEAK_GBS, 4), "traffic": None,
+                     "kernel": "spgemm_forward_multi", "algorithmic_bytes_per_launch": b_fused},
+        "unfused_ms": round(t_u, 4), "fused_speedup": round(t_u / t_f, 3),
+        "unfused_bytes": b_unf,
+    }
+    print(json.dumps(result), flush=True)
+
+
 def main():
     args = parse()
     import spgemm_new_amd as S
@@ -183,6 +239,9 @@ def main():
         kw["panel_cost"] = args.panel_cost
     if args.row_cost:
         kw["row_cost"] = args.row_cost
+
+    if args.relations > 1:
+        return bench_multi(args, S, indptr, indices, data, sel, V, E, h, k, dev, world)
 
     if partitioned:
         from spgemm_new_amd.distributed import PartitionedMaxK

@@ -85,6 +85,24 @@ int maxk_spgemm_forward(const int32_t *sched, int64_t num_panels, const int32_t 
                         size_t workspace_bytes, void *stream);
 
 /* ---------------------------------------------------------------------------
+ * Fused multi-relation forward (ogbn-proteins, BASELINE config 5; no
+ * reference function -- the reference sums proteins' 8 edge features into
+ * node features, utils/proteins_loader.py:41-44).  Y[q] = A_q . scatter(CBSR)
+ * for q < num_rel <= 16 relations sharing one CSR and one CBSR; values is
+ * fp32[num_edges, num_rel] (row-major), out is fp32[num_rel, num_rows,
+ * dim_origin].  Equals num_rel calls of maxk_spgemm_forward with values[:, q]
+ * (up to fp32 summation order).  dim_k must be a power of two in [4, 256].
+ * Same schedule as maxk_spgemm_forward; workspace from
+ * maxk_forward_multi_workspace_bytes.
+ * ------------------------------------------------------------------------- */
+size_t maxk_forward_multi_workspace_bytes(int64_t num_panels, int dim_origin, int num_rel);
+int maxk_spgemm_forward_multi(const int32_t *sched, int64_t num_panels, const int32_t *indptr,
+                              const int32_t *indices, const float *values, int num_rel,
+                              const float *cbsr_data, const uint8_t *cbsr_sel, int num_rows,
+                              int dim_origin, int dim_k, float *out, void *workspace,
+                              size_t workspace_bytes, void *stream);
+
+/* ---------------------------------------------------------------------------
  * Backward SSpMM  dXs[c,l] = sum_{e: idx[e]=c} val[e] * G[row(e), sel[c,l]]
  * (spmm_maxk_backward.cu:15-115, K2).  Writes every element of dxs (no
  * pre-zeroing needed).  Workspace: maxk_backward_workspace_bytes(...).

@@ -381,18 +381,147 @@ __global__ __launch_bounds__(kBlock) void fwd_panel_kernel(
     }
 }
 
-// Adds each panel's carry row into the output (after the owner stored it).
+// Adds each panel's carry row(s) into the output (after the owner stored it):
+// nrel relations, carry rows carry_stride apart, output relations rel_stride apart.
 __global__ __launch_bounds__(kBlock) void carry_fixup_kernel(
     int64_t num_panels, const float *__restrict__ carry, const int32_t *__restrict__ carry_row,
-    float *__restrict__ out, int dim, int carry_stride)
+    float *__restrict__ out, int dim, int carry_stride, int nrel = 1, size_t rel_stride = 0)
 {
     const int64_t w = (int64_t)blockIdx.x * kWavesPerBlock + threadIdx.x / kWave;
     if (w >= num_panels) return;
     const int r = carry_row[w];
     if (r < 0) return;
-    const float *src = carry + (size_t)w * carry_stride;
-    float *dst = out + (size_t)r * dim;
-    for (int c = lane_id(); c < dim; c += kWave) gbl_add(dst + c, src[c]);
+    for (int q = 0; q < nrel; ++q) {
+        const float *src = carry + ((size_t)w * nrel + q) * carry_stride;
+        float *dst = out + q * rel_stride + (size_t)r * dim;
+        for (int c = lane_id(); c < dim; c += kWave) gbl_add(dst + c, src[c]);
+    }
+}
+
+// ---------------------------------------------------------------------------
+// Fused multi-relation forward (ogbn-proteins, config 5):
+// Y_q = A_q . X^ for q < R relations sharing one CSR and one CBSR, edge values
+// val[e * R + q].  Parity: R independent calls of the single-relation forward.
+// One edge per wave-step: the CBSR row is gathered once (LPE lanes x VEC
+// entries, as FwdLayout) and reused by RP = 64 / LPE relations at once (lane
+// group q), ceil(R / RP) passes.  Each relation owns one LDS row of MROW
+// floats; the 4-float skew between relation rows puts the same selected
+// column of different relations in different banks.  No row copies are
+// needed: the lanes of one relation in one step touch distinct columns.
+// ---------------------------------------------------------------------------
+constexpr int kMultiRow = kMaxDim + 4;
+constexpr int kMaxRel = 16;
+
+template <int K>
+__device__ __forceinline__ void fwd_multi_edges(int e0, int e1, int R,
+                                                const int32_t *__restrict__ idx,
+                                                const float *__restrict__ val,
+                                                const float *__restrict__ data,
+                                                const uint8_t *__restrict__ sel, float *acc)
+{
+    using Lay = FwdLayout<K>;
+    constexpr int VEC = Lay::VEC, LPE = Lay::LPE, RP = kWave / LPE;
+    constexpr int U = 8;
+    using D = typename VecT<VEC>::D;
+    using SB = typename VecT<VEC>::S;
+    const int lane = lane_id();
+    const int sub = lane % LPE, grp = lane / LPE;
+    const int passes = (R + RP - 1) / RP;
+    for (int base = e0; base < e1; base += kWave) {
+        const int n = (e1 - base) < kWave ? (e1 - base) : kWave;
+        const int my_c = lane < n ? __builtin_nontemporal_load(idx + base + lane) : 0;
+        for (int s0 = 0; s0 < n; s0 += U) {
+            D d[U];
+            SB sb[U];
+#pragma unroll
+            for (int u = 0; u < U; ++u) {
+                if (s0 + u >= n) break;
+                const int c = __builtin_amdgcn_readlane(my_c, s0 + u);
+                const size_t off = (size_t)c * K + sub * VEC;
+                d[u] = *reinterpret_cast<const D *>(data + off);
+                sb[u] = *reinterpret_cast<const SB *>(sel + off);
+            }
+            for (int p = 0; p < passes; ++p) {
+                const int q = p * RP + grp;
+                float v[U];
+#pragma unroll
+                for (int u = 0; u < U; ++u) {
+                    if (s0 + u >= n) break;
+                    v[u] = q < R ? val[(size_t)(base + s0 + u) * R + q] : 0.f;
+                }
+                if (q < R) {
+#pragma unroll
+                    for (int u = 0; u < U; ++u) {
+                        if (s0 + u >= n) break;
+                        rmw_acc<VEC>(acc + q * kMultiRow, sb[u], v[u], d[u]);
+                    }
+                }
+            }
+        }
+    }
+}
+
+// Store the R accumulator rows to dst + q * rel_stride and zero them.
+__device__ __forceinline__ void flush_multi(float *acc, int R, float *__restrict__ dst,
+                                            size_t rel_stride, int dim)
+{
+    const int lane = lane_id();
+    wave_sync_lds();
+    if ((dim & 3) == 0) {
+        const int d4 = dim >> 2;
+        for (int i = lane; i < R * d4; i += kWave) {
+            const int q = i / d4, c4 = i - q * d4;
+            f4 *src = reinterpret_cast<f4 *>(acc + q * kMultiRow) + c4;
+            reinterpret_cast<f4 *>(dst + q * rel_stride)[c4] = *src;
+            *src = f4{0.f, 0.f, 0.f, 0.f};
+        }
+    } else {
+        for (int i = lane; i < R * dim; i += kWave) {
+            const int q = i / dim, c = i - q * dim;
+            dst[q * rel_stride + c] = acc[q * kMultiRow + c];
+            acc[q * kMultiRow + c] = 0.f;
+        }
+    }
+    wave_sync_lds();
+}
+
+template <int K>
+__global__ __launch_bounds__(kBlock) void fwd_multi_panel_kernel(
+    const int2 *__restrict__ sched, int64_t num_panels, const int32_t *__restrict__ indptr,
+    const int32_t *__restrict__ idx, const float *__restrict__ val, int R,
+    const float *__restrict__ data, const uint8_t *__restrict__ sel, int num_rows, int dim,
+    float *__restrict__ out, float *__restrict__ carry, int32_t *__restrict__ carry_row)
+{
+    extern __shared__ __attribute__((aligned(16))) float lds[];
+    const int dimp = (dim + 3) & ~3;
+    float *acc = lds + (threadIdx.x / kWave) * R * kMultiRow;
+    const int64_t w = (int64_t)blockIdx.x * kWavesPerBlock + threadIdx.x / kWave;
+    if (w >= num_panels) return;
+    zero_lds(acc, R * kMultiRow);
+    const size_t rs = (size_t)num_rows * dim;  // relation stride of the output
+    const int2 a = sched[w], b = sched[w + 1];
+    const int i0 = a.x, j0 = a.y, i1 = b.x, j1 = b.y;
+    int e = j0;
+    for (int r = i0; r < i1; ++r) {
+        const int re = indptr[r + 1];
+        if (e < re) fwd_multi_edges<K>(e, re, R, idx, val, data, sel, acc);
+        flush_multi(acc, R, out + (size_t)r * dim, rs, dim);
+        e = re;
+    }
+    int has_carry = 0;
+    if (i1 < num_rows) {
+        const int eb = e > indptr[i1] ? e : indptr[i1];
+        if (eb < j1) {
+            fwd_multi_edges<K>(eb, j1, R, idx, val, data, sel, acc);
+            has_carry = 1;
+        }
+    }
+    if (has_carry) {
+        flush_multi(acc, R, carry + (size_t)w * R * dimp, dimp, dimp);
+        if (lane_id() == 0) carry_row[w] = i1;
+    } else if (lane_id() == 0) {
+        carry_row[w] = -1;
+    }
 }
 
 // warp4-driven forward (drop-in for the reference launcher).  A wave takes a
@@ -1021,6 +1150,29 @@ struct FwdPanel {
 };
 
 template <int K>
+struct FwdMulti {
+    static int run(const int32_t *sched, int64_t P, const int32_t *indptr, const int32_t *idx,
+                   const float *val, int R, const float *data, const uint8_t *sel, int V,
+                   int dim, float *out, float *carry, int32_t *carry_row, hipStream_t st)
+    {
+        if constexpr (K == 0) {
+            return MAXK_E_DIM;  // the fused kernel is compiled for k = 4, 8, ..., 256
+        } else {
+            const int64_t blocks = ceil_div(P, kWavesPerBlock);
+            const size_t lds = (size_t)kWavesPerBlock * R * kMultiRow * sizeof(float);
+            hipLaunchKernelGGL(fwd_multi_panel_kernel<K>, dim3((unsigned)blocks), dim3(kBlock), lds,
+                               st, reinterpret_cast<const int2 *>(sched), P, indptr, idx, val, R,
+                               data, sel, V, dim, out, carry, carry_row);
+            int rc = launch_status();
+            if (rc) return rc;
+            hipLaunchKernelGGL(carry_fixup_kernel, dim3((unsigned)blocks), dim3(kBlock), 0, st, P,
+                               carry, carry_row, out, dim, (dim + 3) & ~3, R, (size_t)V * dim);
+            return launch_status();
+        }
+    }
+};
+
+template <int K>
 struct FwdWarp4 {
     static int run(const int32_t *warp4, int W, const int32_t *idx, const float *val,
                    const float *data, const uint8_t *sel, int dim, int k, float *out,
@@ -1180,6 +1332,37 @@ int maxk_spgemm_forward(const int32_t *sched, int64_t num_panels, const int32_t 
         static_cast<char *>(workspace) + align_up((size_t)num_panels * dimp * sizeof(float), 256));
     return dispatch_k<FwdPanel>(dim_k, sched, num_panels, indptr, indices, values, cbsr_data,
                                 cbsr_sel, num_rows, dim_origin, dim_k, out, carry, carry_row,
+                                as_stream(stream));
+}
+
+size_t maxk_forward_multi_workspace_bytes(int64_t num_panels, int dim_origin, int num_rel)
+{
+    const size_t dimp = (size_t)((dim_origin + 3) & ~3);
+    return align_up((size_t)num_panels * num_rel * dimp * sizeof(float), 256) +
+           align_up((size_t)num_panels * sizeof(int32_t), 256);
+}
+
+int maxk_spgemm_forward_multi(const int32_t *sched, int64_t num_panels, const int32_t *indptr,
+                              const int32_t *indices, const float *values, int num_rel,
+                              const float *cbsr_data, const uint8_t *cbsr_sel, int num_rows,
+                              int dim_origin, int dim_k, float *out, void *workspace,
+                              size_t workspace_bytes, void *stream)
+{
+    if (!sched || !indptr || !out || num_panels < 1 || num_rows < 0) return MAXK_E_ARG;
+    if (num_rel < 1 || num_rel > kMaxRel) return MAXK_E_ARG;
+    if (!dims_ok(dim_origin, dim_k)) return MAXK_E_DIM;
+    if (num_rows == 0) return MAXK_OK;
+    if (!indices || !values || !cbsr_data || !cbsr_sel) return MAXK_E_ARG;
+    if (!workspace ||
+        workspace_bytes < maxk_forward_multi_workspace_bytes(num_panels, dim_origin, num_rel))
+        return MAXK_E_WORKSPACE;
+    const size_t dimp = (size_t)((dim_origin + 3) & ~3);
+    float *carry = static_cast<float *>(workspace);
+    int32_t *carry_row = reinterpret_cast<int32_t *>(
+        static_cast<char *>(workspace) +
+        align_up((size_t)num_panels * num_rel * dimp * sizeof(float), 256));
+    return dispatch_k<FwdMulti>(dim_k, sched, num_panels, indptr, indices, values, num_rel,
+                                cbsr_data, cbsr_sel, num_rows, dim_origin, out, carry, carry_row,
                                 as_stream(stream));
 }
 

@@ -21,7 +21,8 @@ import torch
 
 from . import _lib
 
-__all__ = ["MaxKGraph", "check_tensor", "spgemm_forward", "sspmm_backward", "warp4_build",
+__all__ = ["MaxKGraph", "check_tensor", "spgemm_forward", "spgemm_forward_multi",
+           "sspmm_backward", "warp4_build",
            "topk_cbsr", "cbsr_scatter", "cbsr_mask"]
 
 
@@ -272,6 +273,15 @@ class MaxKGraph:
         """Y = A . scatter(CBSR)  (spmm_maxk.cu:17-106).  Returns fp32[V, dim_origin]."""
         return spgemm_forward(self, cbsr_data, cbsr_sel, dim_origin, out, values)
 
+    def forward_multi(self, cbsr_data: torch.Tensor, cbsr_sel: torch.Tensor,
+                      values: torch.Tensor, dim_origin: int = 256,
+                      out: torch.Tensor | None = None) -> torch.Tensor:
+        """Fused multi-relation forward (BASELINE config 5, ogbn-proteins):
+        Y[q] = A_q . scatter(CBSR) with A_q's values = values[:, q]
+        (fp32[E, R], R <= 16).  Returns fp32[R, V, dim_origin]; equals R
+        forward() calls with values[:, q].contiguous()."""
+        return spgemm_forward_multi(self, cbsr_data, cbsr_sel, values, dim_origin, out)
+
     def backward(self, grad: torch.Tensor, cbsr_sel: torch.Tensor, out: torch.Tensor | None = None,
                  values: torch.Tensor | None = None, algo: int = _lib.MAXK_BWD_AUTO) -> torch.Tensor:
         """dXs = (A^T G) sampled at sel  (spmm_maxk_backward.cu:15-115).  Returns fp32[V, k]."""
@@ -308,6 +318,34 @@ def spgemm_forward(g: MaxKGraph, data, sel, dim_origin: int = 256, out=None, val
                                      g.indices.data_ptr(), values.data_ptr(), data.data_ptr(),
                                      sel.data_ptr(), g.num_rows, dim_origin, k, out.data_ptr(),
                                      ws.data_ptr(), ws.numel(), _stream(out)), "maxk_spgemm_forward")
+    return out
+
+
+def spgemm_forward_multi(g: MaxKGraph, data, sel, values, dim_origin: int = 256, out=None):
+    _check_cbsr(g, data, sel)
+    k = data.shape[1]
+    check_tensor(values, "values", torch.float32, dim=2)
+    if values.shape[0] != g.num_edges:
+        raise RuntimeError("values must be [num_edges, num_relations]")
+    R = values.shape[1]
+    if not 1 <= R <= 16:
+        raise RuntimeError("1 <= num_relations <= 16")
+    if k & (k - 1) or not 4 <= k <= 256:
+        raise RuntimeError("the fused multi-relation forward needs k a power of two in [4, 256]")
+    if out is None:
+        out = torch.empty((R, g.num_rows, dim_origin), dtype=torch.float32, device=g.device)
+    else:
+        check_tensor(out, "output", torch.float32, dim=3)
+        if tuple(out.shape) != (R, g.num_rows, dim_origin):
+            raise RuntimeError("output must be [R, V, dim_origin]")
+    vals = values if g.num_edges > 0 else torch.zeros((1, R), device=g.device)
+    L = _lib.load()
+    nbytes = L.maxk_forward_multi_workspace_bytes(g.num_panels, dim_origin, R)
+    ws = g._workspace(("fwd_multi", dim_origin, R), nbytes)
+    _lib.check(L.maxk_spgemm_forward_multi(
+        g.sched.data_ptr(), g.num_panels, g.indptr.data_ptr(), g.indices.data_ptr(),
+        vals.data_ptr(), R, data.data_ptr(), sel.data_ptr(), g.num_rows, dim_origin, k,
+        out.data_ptr(), ws.data_ptr(), ws.numel(), _stream(out)), "maxk_spgemm_forward_multi")
     return out
 
 

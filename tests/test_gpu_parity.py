@@ -356,3 +356,50 @@ def test_direct_kernel_interface(dev, oracle, tmp_path):
     res = kern.benchmark_all_k_values(gd, 256, (8, 32), num_runs=2)
     assert set(res) == {8, 32}
     assert test_direct_kernels(str(tmp_path))
+
+
+@pytest.mark.parametrize("k", [8, 16, 32, 64])
+@pytest.mark.parametrize("R", [1, 3, 8, 16])
+def test_forward_multi_relation(dev, oracle, k, R):
+    """Fused R-relation forward (config 5) == R independent single-relation
+    forwards (SURVEY.md §8 a10 parity definition) == the fp64 oracle."""
+    indptr, indices = small_csr(900, seed=21)
+    v, e = len(indptr) - 1, len(indices)
+    vals = np.random.default_rng(R).random((e, R), dtype=np.float32)
+    data, sel = random_cbsr(v, k, 256, seed=k + R)
+    g = S.MaxKGraph(T(indptr, dev), T(indices, dev), panel_cost=300)
+    y = g.forward_multi(T(data, dev), T(sel, dev), T(vals, dev), 256)
+    assert y.shape == (R, v, 256)
+    for q in range(R):
+        ref = oracle.np_forward(indptr, indices, vals[:, q], data, sel, 256)
+        assert oracle.parity_error(y[q].cpu().numpy(), ref) <= TOL
+        single = g.forward(T(data, dev), T(sel, dev), 256,
+                           values=T(np.ascontiguousarray(vals[:, q]), dev))
+        assert torch.allclose(y[q], single, rtol=1e-5, atol=1e-5)
+
+
+def test_forward_multi_errors(dev):
+    indptr, indices = small_csr(50, seed=2)
+    g = S.MaxKGraph(T(indptr, dev), T(indices, dev))
+    data, sel = random_cbsr(50, 12, 256, seed=1)
+    with pytest.raises(RuntimeError, match="power of two"):
+        g.forward_multi(T(data, dev), T(sel, dev), torch.rand((len(indices), 2), device=dev))
+    data, sel = random_cbsr(50, 8, 256, seed=1)
+    with pytest.raises(RuntimeError, match="num_relations"):
+        g.forward_multi(T(data, dev), T(sel, dev), torch.rand((len(indices), 17), device=dev))
+    with pytest.raises(RuntimeError, match="num_edges"):
+        g.forward_multi(T(data, dev), T(sel, dev), torch.rand((3, 2), device=dev))
+
+
+@pytest.mark.parametrize("kind", ["single_row_hub", "empty_rows", "last_row_only"])
+def test_forward_multi_edge_cases(dev, oracle, kind):
+    indptr, indices = _edge_graph(kind)
+    v, e, R, k = len(indptr) - 1, len(indices), 8, 32
+    vals = np.random.default_rng(4).random((e, R), dtype=np.float32)
+    data, sel = random_cbsr(v, k, 256, seed=3)
+    g = S.MaxKGraph(T(indptr, dev), T(indices, dev), panel_cost=100)
+    out = torch.full((R, v, 256), float("nan"), device=dev)
+    g.forward_multi(T(data, dev), T(sel, dev), T(vals, dev), 256, out=out)
+    for q in range(R):
+        ref = oracle.np_forward(indptr, indices, vals[:, q], data, sel, 256)
+        assert oracle.parity_error(out[q].cpu().numpy(), ref) <= TOL
