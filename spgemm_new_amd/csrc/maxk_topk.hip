@@ -72,10 +72,8 @@ __global__ __launch_bounds__(kBlock) void topk_kernel(const float *__restrict__ 
     const int wl = threadIdx.x / kWave;
     const int64_t nwaves = (int64_t)gridDim.x * kWavesPerBlock;
     const bool vec = (dim & 3) == 0 && (ld & 3) == 0;
-    for (int64_t r = (int64_t)blockIdx.x * kWavesPerBlock + wl; r < num_rows; r += nwaves) {
-        const float *row = x + r * ld;
-        float v[4];
-        uint32_t key[4];
+    auto load_row = [&](int64_t rr, float *v) {
+        const float *row = x + rr * ld;
         if (vec && 4 * lane < dim) {
             const float4 q = *reinterpret_cast<const float4 *>(row + 4 * lane);
             v[0] = q.x; v[1] = q.y; v[2] = q.z; v[3] = q.w;
@@ -83,16 +81,30 @@ __global__ __launch_bounds__(kBlock) void topk_kernel(const float *__restrict__ 
 #pragma unroll
             for (int j = 0; j < 4; ++j) v[j] = (4 * lane + j < dim) ? row[4 * lane + j] : 0.f;
         }
+    };
+    int64_t r = (int64_t)blockIdx.x * kWavesPerBlock + wl;
+    float nx[4] = {0.f, 0.f, 0.f, 0.f};
+    if (r < num_rows) load_row(r, nx);
+    for (; r < num_rows; r += nwaves) {
+        float v[4];
+        uint32_t key[4];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) v[j] = nx[j];
+        if (r + nwaves < num_rows) load_row(r + nwaves, nx);  // next row in flight
 #pragma unroll
         for (int j = 0; j < 4; ++j) key[j] = (4 * lane + j < dim) ? float_key(v[j]) : 0u;
-        // largest T with #{key >= T} >= k (every valid key is >= 0x007fffff > 0)
+        // largest T with #{key >= T} >= k (every valid key is >= 0x007fffff > 0);
+        // stops early once exactly k keys are >= T: then they are the selection
         uint32_t T = 0;
         for (int b = 31; b >= 0; --b) {
             const uint32_t cand = T | (1u << b);
             int cnt = 0;
 #pragma unroll
             for (int j = 0; j < 4; ++j) cnt += popc64(__ballot(key[j] >= cand));
-            if (cnt >= k) T = cand;
+            if (cnt >= k) {
+                T = cand;
+                if (cnt == k) break;
+            }
         }
         uint64_t gt[4], eq[4];
         int n_gt = 0;
