@@ -240,7 +240,9 @@ __device__ __forceinline__ void fwd_edges_vec(int e0, int e1, const int32_t *__r
                 v[u] = __shfl(my_v, t < kWave ? t : 0);
                 if (t < n) {
                     const size_t off = (size_t)c * K + sub * VEC;
-                    d[u] = *reinterpret_cast<const D *>(data + off);
+                    // data rows non-temporal (measured 3.45 -> 3.18 ms on Reddit k=32);
+                    // selector words plain (nt 4-B loads measured slower)
+                    d[u] = __builtin_nontemporal_load(reinterpret_cast<const D *>(data + off));
                     sb[u] = *reinterpret_cast<const SB *>(sel + off);
                 }
             }

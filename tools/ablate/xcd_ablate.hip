@@ -38,7 +38,7 @@ __device__ __forceinline__ void edges(int e0, int e1, const int *__restrict__ id
             const float v = __shfl(my_v, t);
             if (t < n) {
                 const size_t off = (size_t)c * K + sub * 4;
-                const f4 d = *reinterpret_cast<const f4 *>(data + off);
+                const f4 d = __builtin_nontemporal_load(reinterpret_cast<const f4 *>(data + off));
                 const unsigned sb = *reinterpret_cast<const unsigned *>(sel + off);
                 my[sb & 255] += v * d.x; my[(sb >> 8) & 255] += v * d.y;
                 my[(sb >> 16) & 255] += v * d.z; my[sb >> 24] += v * d.w;
@@ -99,6 +99,43 @@ __global__ __launch_bounds__(256) void fwd(const int2 *__restrict__ panels, int 
         }
         edges(e0, e1, idx, val, data, sel, acc, lane);
         flush(acc, dst, lane);
+    }
+}
+
+// Sequential classes: one launch per class x, every block on class x; launch 0
+// stores rows, later launches add (plain RMW of owned rows).
+__global__ __launch_bounds__(256) void fwd_seq(const int2 *__restrict__ panels, int P, int x, int NC,
+                                               const int *__restrict__ bnd,
+                                               const int *__restrict__ idx, const float *__restrict__ val,
+                                               const float *__restrict__ data,
+                                               const unsigned char *__restrict__ sel,
+                                               float *__restrict__ out)
+{
+    __shared__ __attribute__((aligned(16))) float lds[4 * EPS * 256];
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    float *acc = lds + wv * EPS * 256;
+    for (int i = lane; i < EPS * 256; i += 64) acc[i] = 0.f;
+    const int pidx = blockIdx.x * 4 + wv;
+    if (pidx >= P) return;
+    const int2 pr = panels[pidx];
+    for (int r = pr.x; r < pr.y; ++r) {
+        const int e0 = bnd[(size_t)r * (NC + 1) + x], e1 = bnd[(size_t)r * (NC + 1) + x + 1];
+        edges(e0, e1, idx, val, data, sel, acc, lane);
+        float *dst = out + (size_t)r * 256;
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        f4 a = reinterpret_cast<f4 *>(acc)[lane];
+        reinterpret_cast<f4 *>(acc)[lane] = f4{0, 0, 0, 0};
+        for (int cp = 1; cp < EPS; ++cp) {
+            a += reinterpret_cast<f4 *>(acc + cp * 256)[lane];
+            reinterpret_cast<f4 *>(acc + cp * 256)[lane] = f4{0, 0, 0, 0};
+        }
+        if (x > 0) a += reinterpret_cast<f4 *>(dst)[lane];
+        reinterpret_cast<f4 *>(dst)[lane] = a;
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
     }
 }
 
@@ -173,6 +210,35 @@ void run_cls(int V, const std::vector<int> &indptr, const std::vector<int> &idx,
     hipFree(d_bnd); hipFree(d_p); hipFree(d_y8);
 }
 
+void run_seq(int NC, int V, const std::vector<int> &indptr, const std::vector<int> &idx, int *d_idx,
+             float *d_val, float *d_data, unsigned char *d_sel, int reps, double bytes, float *d_y)
+{
+    std::vector<int> bnd((size_t)V * (NC + 1));
+    for (int r = 0; r < V; ++r)
+        for (int x = 0; x <= NC; ++x) {
+            const long long cut = (long long)V * x / NC;
+            bnd[(size_t)r * (NC + 1) + x] = (int)(std::lower_bound(idx.begin() + indptr[r], idx.begin() + indptr[r + 1], (int)cut) - idx.begin());
+        }
+    std::vector<int2> panels;
+    int r0 = 0;
+    long long acc = 0;
+    for (int r = 0; r < V; ++r) {
+        acc += (indptr[r + 1] - indptr[r]) / NC + 16;
+        if (acc >= 2048) { panels.push_back(make_int2(r0, r + 1)); r0 = r + 1; acc = 0; }
+    }
+    if (r0 < V) panels.push_back(make_int2(r0, V));
+    int *d_bnd = up(bnd);
+    int2 *d_p = up(panels);
+    const int P = (int)panels.size();
+    float t = timeit([&] {
+        for (int x = 0; x < NC; ++x)
+            hipLaunchKernelGGL(fwd_seq, dim3((P + 3) / 4), dim3(256), 0, 0, d_p, P, x, NC, d_bnd, d_idx, d_val, d_data, d_sel, d_y);
+    }, reps);
+    printf("seq NC=%d: %.3f ms (%.0f GB/s eff)\n", NC, t, bytes / t / 1e6);
+    fflush(stdout);
+    hipFree(d_bnd); hipFree(d_p);
+}
+
 int main(int argc, char **argv)
 {
     const int V = argc > 1 ? atoi(argv[1]) : 232965;
@@ -213,8 +279,8 @@ int main(int argc, char **argv)
     float tb = timeit([&] { hipLaunchKernelGGL((fwd<0>), dim3((P + 3) / 4), dim3(256), 0, 0, d_p, P, d_ptr, (const int *)nullptr, d_idx, d_val, d_data, d_sel, d_y, V); }, reps);
     printf("V=%d E=%lld base: %.3f ms (%.0f GB/s eff)\n", V, E, tb, bytes / tb / 1e6);
     fflush(stdout);
+    for (int nc : {1, 2, 3, 4, 8}) run_seq(nc, V, indptr, idx, d_idx, d_val, d_data, d_sel, reps, bytes, d_y);
     run_cls<8>(V, indptr, idx, d_idx, d_val, d_data, d_sel, reps, bytes, d_y);
-    run_cls<16>(V, indptr, idx, d_idx, d_val, d_data, d_sel, reps, bytes, d_y);
     run_cls<4>(V, indptr, idx, d_idx, d_val, d_data, d_sel, reps, bytes, d_y);
     return 0;
 }
