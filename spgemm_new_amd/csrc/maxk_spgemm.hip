@@ -435,21 +435,25 @@ __device__ __forceinline__ void fwd_multi_edges(int e0, int e1, int R,
         for (int s0 = 0; s0 < n; s0 += U) {
             D d[U];
             SB sb[U];
+            float v[U];
+            // CBSR gathers and the first pass's edge values in flight together
 #pragma unroll
             for (int u = 0; u < U; ++u) {
                 if (s0 + u >= n) break;
                 const int c = __builtin_amdgcn_readlane(my_c, s0 + u);
                 const size_t off = (size_t)c * K + sub * VEC;
-                d[u] = *reinterpret_cast<const D *>(data + off);
+                d[u] = __builtin_nontemporal_load(reinterpret_cast<const D *>(data + off));
                 sb[u] = *reinterpret_cast<const SB *>(sel + off);
+                v[u] = grp < R ? val[(size_t)(base + s0 + u) * R + grp] : 0.f;
             }
             for (int p = 0; p < passes; ++p) {
                 const int q = p * RP + grp;
-                float v[U];
+                if (p > 0) {
 #pragma unroll
-                for (int u = 0; u < U; ++u) {
-                    if (s0 + u >= n) break;
-                    v[u] = q < R ? val[(size_t)(base + s0 + u) * R + q] : 0.f;
+                    for (int u = 0; u < U; ++u) {
+                        if (s0 + u >= n) break;
+                        v[u] = q < R ? val[(size_t)(base + s0 + u) * R + q] : 0.f;
+                    }
                 }
                 if (q < R) {
 #pragma unroll
@@ -485,6 +489,203 @@ __device__ __forceinline__ void flush_multi(float *acc, int R, float *__restrict
         }
     }
     wave_sync_lds();
+}
+
+// Relation-vector form for R = 4*R4 relations (R4 in {1, 2, 4}, so that
+// L = K*R4 divides or is a multiple of 64): the accumulator is laid out
+// [col][R] so one lane owns (selected entry j, relation quad rq) and updates
+// four relations with one ds_read_b128 + ds_write_b128 per edge; the edge's
+// four values arrive as one float4.  L = K*R4 lanes per edge: EPS = 64/L
+// edges per step with private row copies when L < 64, else L/64 passes.
+// Lanes of one step write distinct words (an edge's selected columns are
+// distinct; different edges use different copies).
+template <int K, int R4>
+struct Rel4 {
+    static_assert((R4 & (R4 - 1)) == 0, "R4 must be a power of two");
+    static constexpr int R = 4 * R4;
+    static constexpr int L = K * R4;
+    static constexpr int EPS = L >= kWave ? 1 : kWave / L;
+    static constexpr int PASSES = L >= kWave ? L / kWave : 1;
+    static constexpr int U = PASSES >= 8 ? 1 : 8 / PASSES;
+    // floats per column record: an odd number of float4 quads, so the 4-bank
+    // group of a b128 access (= col * S/4 mod 16) takes all 16 values; with
+    // S = 8 (R = 8) only 8 groups were used: 19 conflict cycles per
+    // ds_*_b128 measured on proteins (SQ_LDS_BANK_CONFLICT / SQ_INSTS_LDS)
+    static constexpr int S = (R4 & 1) ? R : R + 4;
+    static constexpr int ROW = kMaxDim * S;  // floats per accumulator copy
+};
+
+// One round of U edges (EPS == 1: every lane works on the same edge): the
+// edge's column index is wave-uniform, so the CBSR row and edge-value row
+// pointers are scalar and every load is saddr + a constant lane offset.
+template <int K, int R4, bool FULL>
+__device__ __forceinline__ void rel4_round_uniform(int my_c, int base, int s0, int n,
+                                                   const float *__restrict__ val,
+                                                   const float *__restrict__ data,
+                                                   const uint8_t *__restrict__ sel, float *my)
+{
+    using C = Rel4<K, R4>;
+    constexpr int R = C::R, PASSES = C::PASSES, U = C::U;
+    const int lane = lane_id();
+    float d[U][PASSES];
+    uint32_t col[U][PASSES];
+    f4 v[U][PASSES];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+        if (!FULL && s0 + u >= n) break;
+        const int c = __builtin_amdgcn_readlane(my_c, s0 + u);
+        const float *drow = data + (size_t)c * K;
+        const uint8_t *srow = sel + (size_t)c * K;
+        // per-lane float4 of the edge's values (scalar loads + per-lane
+        // select measured slower: 8.37 vs 7.33 ms on proteins R=8)
+        const f4 *vrow = reinterpret_cast<const f4 *>(val + (size_t)(base + s0 + u) * R);
+#pragma unroll
+        for (int p = 0; p < PASSES; ++p) {
+            const int item = lane + p * kWave;
+            const int j = item % K, rq = item / K;
+            d[u][p] = drow[j];
+            col[u][p] = srow[j];
+            v[u][p] = vrow[rq];
+        }
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+        if (!FULL && s0 + u >= n) break;
+#pragma unroll
+        for (int p = 0; p < PASSES; ++p) {
+            const int rq = (lane + p * kWave) / K;
+            f4 *a = reinterpret_cast<f4 *>(my + col[u][p] * C::S + 4 * rq);
+            *a += d[u][p] * v[u][p];
+        }
+    }
+}
+
+template <int K, int R4>
+__device__ __forceinline__ void fwd_rel4_edges(int e0, int e1, const int32_t *__restrict__ idx,
+                                               const float *__restrict__ val,
+                                               const float *__restrict__ data,
+                                               const uint8_t *__restrict__ sel, float *acc)
+{
+    using C = Rel4<K, R4>;
+    constexpr int R = C::R, L = C::L, EPS = C::EPS, PASSES = C::PASSES, U = C::U;
+    const int lane = lane_id();
+    const int slot = EPS > 1 ? lane / L : 0;
+    float *my = acc + slot * C::ROW;
+    for (int base = e0; base < e1; base += kWave) {
+        const int n = __builtin_amdgcn_readfirstlane((e1 - base) < kWave ? (e1 - base) : kWave);
+        const int my_c = lane < n ? __builtin_nontemporal_load(idx + base + lane) : 0;
+        if constexpr (EPS == 1) {
+            int s0 = 0;
+            for (; s0 + U <= n; s0 += U)
+                rel4_round_uniform<K, R4, true>(my_c, base, s0, n, val, data, sel, my);
+            if (s0 < n) rel4_round_uniform<K, R4, false>(my_c, base, s0, n, val, data, sel, my);
+        } else {
+            for (int s0 = 0; s0 < n; s0 += U * EPS) {
+                float d[U][PASSES];
+                uint32_t col[U][PASSES];
+                f4 v[U][PASSES];
+                bool ok[U];
+#pragma unroll
+                for (int u = 0; u < U; ++u) {
+                    const int t = s0 + u * EPS + slot;
+                    ok[u] = t < n;
+                    const int c = __shfl(my_c, t < kWave ? t : 0);
+#pragma unroll
+                    for (int p = 0; p < PASSES; ++p) {
+                        const int item = lane % L;
+                        const int j = item % K, rq = item / K;
+                        if (ok[u]) {
+                            const size_t off = (size_t)c * K + j;
+                            d[u][p] = data[off];
+                            col[u][p] = sel[off];
+                            v[u][p] = *reinterpret_cast<const f4 *>(val + (size_t)(base + t) * R + 4 * rq);
+                        }
+                    }
+                }
+#pragma unroll
+                for (int u = 0; u < U; ++u) {
+                    if (!ok[u]) continue;
+#pragma unroll
+                    for (int p = 0; p < PASSES; ++p) {
+                        const int rq = (lane % L) / K;
+                        f4 *a = reinterpret_cast<f4 *>(my + col[u][p] * C::S + 4 * rq);
+                        *a += d[u][p] * v[u][p];
+                    }
+                }
+            }
+        }
+    }
+}
+
+// Sum the row copies of the [col][R] accumulator, store relation q's row to
+// dst + q * rel_stride, zero the copies.
+template <int K, int R4>
+__device__ __forceinline__ void flush_rel4(float *acc, float *__restrict__ dst, size_t rel_stride,
+                                           int dim)
+{
+    using C = Rel4<K, R4>;
+    constexpr int R = C::R;
+    const int lane = lane_id();
+    wave_sync_lds();
+    const int d4 = (dim + 3) >> 2;
+    for (int i = lane; i < R * d4; i += kWave) {
+        const int q = i / d4, c4 = i - q * d4;
+        f4 s = f4{0.f, 0.f, 0.f, 0.f};
+        for (int cp = 0; cp < C::EPS; ++cp) {
+            constexpr int S = C::S;
+            float *b = acc + cp * C::ROW + (4 * c4) * S + q;
+            s.x += b[0]; s.y += b[S]; s.z += b[2 * S]; s.w += b[3 * S];
+            b[0] = 0.f; b[S] = 0.f; b[2 * S] = 0.f; b[3 * S] = 0.f;
+        }
+        float *o = dst + q * rel_stride + 4 * c4;
+        if ((dim & 3) == 0) {
+            *reinterpret_cast<f4 *>(o) = s;
+        } else {
+            const float sv[4] = {s.x, s.y, s.z, s.w};
+            for (int t = 0; t < 4 && 4 * c4 + t < dim; ++t) o[t] = sv[t];
+        }
+    }
+    wave_sync_lds();
+}
+
+template <int K, int R4>
+__global__ __launch_bounds__(kBlock) void fwd_rel4_panel_kernel(
+    const int2 *__restrict__ sched, int64_t num_panels, const int32_t *__restrict__ indptr,
+    const int32_t *__restrict__ idx, const float *__restrict__ val,
+    const float *__restrict__ data, const uint8_t *__restrict__ sel, int num_rows, int dim,
+    float *__restrict__ out, float *__restrict__ carry, int32_t *__restrict__ carry_row)
+{
+    using C = Rel4<K, R4>;
+    extern __shared__ __attribute__((aligned(16))) float lds[];
+    const int dimp = (dim + 3) & ~3;
+    float *acc = lds + (threadIdx.x / kWave) * C::EPS * C::ROW;
+    const int64_t w = (int64_t)blockIdx.x * kWavesPerBlock + threadIdx.x / kWave;
+    if (w >= num_panels) return;
+    zero_lds(acc, C::EPS * C::ROW);
+    const size_t rs = (size_t)num_rows * dim;
+    const int2 a = sched[w], b = sched[w + 1];
+    const int i0 = a.x, j0 = a.y, i1 = b.x, j1 = b.y;
+    int e = j0;
+    for (int r = i0; r < i1; ++r) {
+        const int re = indptr[r + 1];
+        if (e < re) fwd_rel4_edges<K, R4>(e, re, idx, val, data, sel, acc);
+        flush_rel4<K, R4>(acc, out + (size_t)r * dim, rs, dim);
+        e = re;
+    }
+    int has_carry = 0;
+    if (i1 < num_rows) {
+        const int eb = e > indptr[i1] ? e : indptr[i1];
+        if (eb < j1) {
+            fwd_rel4_edges<K, R4>(eb, j1, idx, val, data, sel, acc);
+            has_carry = 1;
+        }
+    }
+    if (has_carry) {
+        flush_rel4<K, R4>(acc, carry + (size_t)w * C::R * dimp, dimp, dimp);
+        if (lane_id() == 0) carry_row[w] = i1;
+    } else if (lane_id() == 0) {
+        carry_row[w] = -1;
+    }
 }
 
 template <int K>
@@ -1153,6 +1354,20 @@ struct FwdPanel {
 
 template <int K>
 struct FwdMulti {
+    template <int R4>
+    static int launch_rel4(const int2 *sc, int64_t P, const int32_t *indptr, const int32_t *idx,
+                           const float *val, const float *data, const uint8_t *sel, int V,
+                           int dim, float *out, float *carry, int32_t *carry_row, hipStream_t st)
+    {
+        using C = Rel4<K, R4>;
+        const size_t lds = (size_t)kWavesPerBlock * C::EPS * C::ROW * sizeof(float);
+        if (lds > 160 * 1024) return -1;  // nothing launched; the caller falls back
+        hipLaunchKernelGGL((fwd_rel4_panel_kernel<K, R4>), dim3((unsigned)ceil_div(P, kWavesPerBlock)),
+                           dim3(kBlock), lds, st, sc, P, indptr, idx, val, data, sel, V, dim, out,
+                           carry, carry_row);
+        return launch_status();
+    }
+
     static int run(const int32_t *sched, int64_t P, const int32_t *indptr, const int32_t *idx,
                    const float *val, int R, const float *data, const uint8_t *sel, int V,
                    int dim, float *out, float *carry, int32_t *carry_row, hipStream_t st)
@@ -1161,11 +1376,26 @@ struct FwdMulti {
             return MAXK_E_DIM;  // the fused kernel is compiled for k = 4, 8, ..., 256
         } else {
             const int64_t blocks = ceil_div(P, kWavesPerBlock);
-            const size_t lds = (size_t)kWavesPerBlock * R * kMultiRow * sizeof(float);
-            hipLaunchKernelGGL(fwd_multi_panel_kernel<K>, dim3((unsigned)blocks), dim3(kBlock), lds,
-                               st, reinterpret_cast<const int2 *>(sched), P, indptr, idx, val, R,
-                               data, sel, V, dim, out, carry, carry_row);
-            int rc = launch_status();
+            const int2 *sc = reinterpret_cast<const int2 *>(sched);
+            int rc = MAXK_OK;
+            bool done = false;
+            if ((R & 3) == 0 && (reinterpret_cast<uintptr_t>(val) & 15) == 0) {
+                done = true;
+                switch (R / 4) {
+                case 1: rc = launch_rel4<1>(sc, P, indptr, idx, val, data, sel, V, dim, out, carry, carry_row, st); break;
+                case 2: rc = launch_rel4<2>(sc, P, indptr, idx, val, data, sel, V, dim, out, carry, carry_row, st); break;
+                case 4: rc = launch_rel4<4>(sc, P, indptr, idx, val, data, sel, V, dim, out, carry, carry_row, st); break;
+                default: done = false;
+                }
+                if (rc == -1) done = false;  // LDS too large for this (k, R): generic kernel
+            }
+            if (!done) {
+                const size_t lds = (size_t)kWavesPerBlock * R * kMultiRow * sizeof(float);
+                hipLaunchKernelGGL(fwd_multi_panel_kernel<K>, dim3((unsigned)blocks), dim3(kBlock),
+                                   lds, st, sc, P, indptr, idx, val, R, data, sel, V, dim, out,
+                                   carry, carry_row);
+                rc = launch_status();
+            }
             if (rc) return rc;
             hipLaunchKernelGGL(carry_fixup_kernel, dim3((unsigned)blocks), dim3(kBlock), 0, st, P,
                                carry, carry_row, out, dim, (dim + 3) & ~3, R, (size_t)V * dim);

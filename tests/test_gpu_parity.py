@@ -358,8 +358,8 @@ def test_direct_kernel_interface(dev, oracle, tmp_path):
     assert test_direct_kernels(str(tmp_path))
 
 
-@pytest.mark.parametrize("k", [8, 16, 32, 64])
-@pytest.mark.parametrize("R", [1, 3, 8, 16])
+@pytest.mark.parametrize("k", [4, 8, 16, 32, 64, 256])
+@pytest.mark.parametrize("R", [1, 3, 4, 8, 12, 16])
 def test_forward_multi_relation(dev, oracle, k, R):
     """Fused R-relation forward (config 5) == R independent single-relation
     forwards (SURVEY.md §8 a10 parity definition) == the fp64 oracle."""
