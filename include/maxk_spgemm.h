@@ -85,6 +85,22 @@ int maxk_spgemm_forward(const int32_t *sched, int64_t num_panels, const int32_t 
                         size_t workspace_bytes, void *stream);
 
 /* ---------------------------------------------------------------------------
+ * Packed CBSR forward (k = 4, 8, 16).  maxk_cbsr_pack writes one record per
+ * node: k fp32 values, then k selector bytes, zero-padded to
+ * maxk_cbsr_packed_row_bytes(k) = 32 / 64 / 128 bytes (packed: num_cols x
+ * that many bytes, 16-B aligned).  maxk_spgemm_forward_packed is
+ * maxk_spgemm_forward reading the records (one cache line per gathered
+ * neighbour instead of two); same schedule and workspace.
+ * ------------------------------------------------------------------------- */
+size_t maxk_cbsr_packed_row_bytes(int dim_k);
+int maxk_cbsr_pack(const float *cbsr_data, const uint8_t *cbsr_sel, int num_cols, int dim_k,
+                   void *packed, void *stream);
+int maxk_spgemm_forward_packed(const int32_t *sched, int64_t num_panels, const int32_t *indptr,
+                               const int32_t *indices, const float *values, const void *packed,
+                               int num_rows, int dim_origin, int dim_k, float *out,
+                               void *workspace, size_t workspace_bytes, void *stream);
+
+/* ---------------------------------------------------------------------------
  * Fused multi-relation forward (ogbn-proteins, BASELINE config 5; no
  * reference function -- the reference sums proteins' 8 edge features into
  * node features, utils/proteins_loader.py:41-44).  Y[q] = A_q . scatter(CBSR)

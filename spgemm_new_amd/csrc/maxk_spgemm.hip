@@ -203,7 +203,15 @@ __device__ __forceinline__ void rmw_acc(float *acc, typename VecT<VEC>::S sb, fl
     }
 }
 
+// Packed CBSR (k <= 16): one record per node = k fp32 values, then k selector
+// bytes, padded to RS = 32 / 64 / 128 bytes (k = 4 / 8 / 16), so a gathered
+// neighbour costs one cache line instead of two (data line + selector line).
 template <int K>
+struct Packed {
+    static constexpr int RS = K == 4 ? 32 : (K == 8 ? 64 : (K == 16 ? 128 : 0));
+};
+
+template <int K, int RS = 0>
 __device__ __forceinline__ void fwd_edges_vec(int e0, int e1, const int32_t *__restrict__ idx,
                                               const float *__restrict__ val,
                                               const float *__restrict__ data,
@@ -239,11 +247,17 @@ __device__ __forceinline__ void fwd_edges_vec(int e0, int e1, const int32_t *__r
                 const int c = __shfl(my_c, t < kWave ? t : 0);
                 v[u] = __shfl(my_v, t < kWave ? t : 0);
                 if (t < n) {
-                    const size_t off = (size_t)c * K + sub * VEC;
-                    // data rows non-temporal (measured 3.45 -> 3.18 ms on Reddit k=32);
-                    // selector words plain (nt 4-B loads measured slower)
-                    d[u] = __builtin_nontemporal_load(reinterpret_cast<const D *>(data + off));
-                    sb[u] = *reinterpret_cast<const SB *>(sel + off);
+                    if constexpr (RS == 0) {
+                        const size_t off = (size_t)c * K + sub * VEC;
+                        // data rows non-temporal (measured 3.45 -> 3.18 ms on Reddit k=32);
+                        // selector words plain (nt 4-B loads measured slower)
+                        d[u] = __builtin_nontemporal_load(reinterpret_cast<const D *>(data + off));
+                        sb[u] = *reinterpret_cast<const SB *>(sel + off);
+                    } else {  // data = record base, sel = record base + 4K bytes
+                        const size_t rec = (size_t)c * RS;
+                        d[u] = *reinterpret_cast<const D *>(reinterpret_cast<const uint8_t *>(data) + rec + 4 * sub * VEC);
+                        sb[u] = *reinterpret_cast<const SB *>(sel + rec + sub * VEC);
+                    }
                 }
             }
 #pragma unroll
@@ -288,14 +302,14 @@ __device__ __forceinline__ void fwd_edges_scalar(int e0, int e1, int k,
     }
 }
 
-template <int K>
+template <int K, int RS = 0>
 __device__ __forceinline__ void fwd_edges(int e0, int e1, int k, const int32_t *__restrict__ idx,
                                           const float *__restrict__ val,
                                           const float *__restrict__ data,
                                           const uint8_t *__restrict__ sel, float *acc)
 {
     if constexpr (K > 0)
-        fwd_edges_vec<K>(e0, e1, idx, val, data, sel, acc);
+        fwd_edges_vec<K, RS>(e0, e1, idx, val, data, sel, acc);
     else
         fwd_edges_scalar(e0, e1, k, idx, val, data, sel, acc);
 }
@@ -343,7 +357,7 @@ __device__ __forceinline__ void zero_lds(float *acc, int n)
 
 // Panel-scheduled forward.  Rows [i0, i1) are finished and owned by this
 // wave (plain store); row i1 is in progress at the panel end -> carry.
-template <int K>
+template <int K, int RS = 0>
 __global__ __launch_bounds__(kBlock) void fwd_panel_kernel(
     const int2 *__restrict__ sched, int64_t num_panels, const int32_t *__restrict__ indptr,
     const int32_t *__restrict__ idx, const float *__restrict__ val,
@@ -363,7 +377,7 @@ __global__ __launch_bounds__(kBlock) void fwd_panel_kernel(
     int e = j0;
     for (int r = i0; r < i1; ++r) {
         const int re = indptr[r + 1];
-        if (e < re) fwd_edges<K>(e, re, k, idx, val, data, sel, acc);
+        if (e < re) fwd_edges<K, RS>(e, re, k, idx, val, data, sel, acc);
         flush_row<kStore>(acc, copies, out + (size_t)r * dim, dim);
         e = re;
     }
@@ -371,7 +385,7 @@ __global__ __launch_bounds__(kBlock) void fwd_panel_kernel(
     if (i1 < num_rows) {
         const int eb = e > indptr[i1] ? e : indptr[i1];
         if (eb < j1) {
-            fwd_edges<K>(eb, j1, k, idx, val, data, sel, acc);
+            fwd_edges<K, RS>(eb, j1, k, idx, val, data, sel, acc);
             has_carry = 1;
         }
     }
@@ -1297,6 +1311,26 @@ __global__ __launch_bounds__(kBlock) void bwd_local_kernel(
     for (int i = lane; i < nent; i += kWave) dst[i] = srow[i] < dim ? acc[i] : 0.f;
 }
 
+template <int K>
+__global__ __launch_bounds__(kBlock) void cbsr_pack_kernel(const float *__restrict__ data,
+                                                           const uint8_t *__restrict__ sel,
+                                                           int num_cols, uint8_t *__restrict__ rec)
+{
+    constexpr int RS = Packed<K>::RS;
+    constexpr int W = RS / 4;  // dwords per record
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;  // dword of the output
+    if (i >= (int64_t)num_cols * W) return;
+    const int64_t c = i / W;
+    const int w = (int)(i - c * W);
+    uint32_t v = 0;
+    if (w < K) {
+        v = __builtin_bit_cast(uint32_t, data[c * K + w]);
+    } else if (w < K + K / 4) {
+        v = *reinterpret_cast<const uint32_t *>(sel + c * K + 4 * (w - K));
+    }
+    reinterpret_cast<uint32_t *>(rec)[i] = v;
+}
+
 // ---------------------------------------------------------------------------
 // Host-side dispatch
 // ---------------------------------------------------------------------------
@@ -1349,6 +1383,45 @@ struct FwdPanel {
         hipLaunchKernelGGL(carry_fixup_kernel, dim3((unsigned)blocks), dim3(kBlock), 0, st, P,
                            carry, carry_row, out, dim, (dim + 3) & ~3);
         return launch_status();
+    }
+};
+
+template <int K>
+struct FwdPanelPacked {
+    static int run(const int32_t *sched, int64_t P, const int32_t *indptr, const int32_t *idx,
+                   const float *val, const uint8_t *rec, int V, int dim, int k, float *out,
+                   float *carry, int32_t *carry_row, hipStream_t st)
+    {
+        if constexpr (Packed<K>::RS == 0) {
+            return MAXK_E_DIM;
+        } else {
+            constexpr int RS = Packed<K>::RS;
+            const int64_t blocks = ceil_div(P, kWavesPerBlock);
+            hipLaunchKernelGGL((fwd_panel_kernel<K, RS>), dim3((unsigned)blocks), dim3(kBlock),
+                               fwd_lds_bytes<K>(k), st, reinterpret_cast<const int2 *>(sched), P,
+                               indptr, idx, val, reinterpret_cast<const float *>(rec),
+                               rec + 4 * K, V, dim, k, out, carry, carry_row);
+            int rc = launch_status();
+            if (rc) return rc;
+            hipLaunchKernelGGL(carry_fixup_kernel, dim3((unsigned)blocks), dim3(kBlock), 0, st, P,
+                               carry, carry_row, out, dim, (dim + 3) & ~3, 1, (size_t)0);
+            return launch_status();
+        }
+    }
+};
+
+template <int K>
+struct CbsrPack {
+    static int run(const float *data, const uint8_t *sel, int num_cols, uint8_t *rec, hipStream_t st)
+    {
+        if constexpr (Packed<K>::RS == 0) {
+            return MAXK_E_DIM;
+        } else {
+            const int64_t n = (int64_t)num_cols * (Packed<K>::RS / 4);
+            hipLaunchKernelGGL(cbsr_pack_kernel<K>, dim3((unsigned)ceil_div(n, kBlock)), dim3(kBlock),
+                               0, st, data, sel, num_cols, rec);
+            return launch_status();
+        }
     }
 };
 
@@ -1565,6 +1638,50 @@ int maxk_spgemm_forward(const int32_t *sched, int64_t num_panels, const int32_t 
     return dispatch_k<FwdPanel>(dim_k, sched, num_panels, indptr, indices, values, cbsr_data,
                                 cbsr_sel, num_rows, dim_origin, dim_k, out, carry, carry_row,
                                 as_stream(stream));
+}
+
+size_t maxk_cbsr_packed_row_bytes(int dim_k)
+{
+    return dim_k == 4 ? 32 : (dim_k == 8 ? 64 : (dim_k == 16 ? 128 : 0));
+}
+
+int maxk_cbsr_pack(const float *cbsr_data, const uint8_t *cbsr_sel, int num_cols, int dim_k,
+                   void *packed, void *stream)
+{
+    if (maxk_cbsr_packed_row_bytes(dim_k) == 0) return MAXK_E_DIM;
+    if (num_cols < 0 || (num_cols > 0 && (!cbsr_data || !cbsr_sel || !packed))) return MAXK_E_ARG;
+    if (num_cols == 0) return MAXK_OK;
+    uint8_t *rec = static_cast<uint8_t *>(packed);
+    hipStream_t st = as_stream(stream);
+    switch (dim_k) {
+    case 4: return CbsrPack<4>::run(cbsr_data, cbsr_sel, num_cols, rec, st);
+    case 8: return CbsrPack<8>::run(cbsr_data, cbsr_sel, num_cols, rec, st);
+    default: return CbsrPack<16>::run(cbsr_data, cbsr_sel, num_cols, rec, st);
+    }
+}
+
+int maxk_spgemm_forward_packed(const int32_t *sched, int64_t num_panels, const int32_t *indptr,
+                               const int32_t *indices, const float *values, const void *packed,
+                               int num_rows, int dim_origin, int dim_k, float *out,
+                               void *workspace, size_t workspace_bytes, void *stream)
+{
+    if (!sched || !indptr || !out || num_panels < 1 || num_rows < 0) return MAXK_E_ARG;
+    if (!dims_ok(dim_origin, dim_k) || maxk_cbsr_packed_row_bytes(dim_k) == 0) return MAXK_E_DIM;
+    if (num_rows == 0) return MAXK_OK;
+    if (!indices || !values || !packed) return MAXK_E_ARG;
+    if (!workspace || workspace_bytes < maxk_forward_workspace_bytes(num_panels, dim_origin))
+        return MAXK_E_WORKSPACE;
+    const size_t dimp = (size_t)((dim_origin + 3) & ~3);
+    float *carry = static_cast<float *>(workspace);
+    int32_t *carry_row = reinterpret_cast<int32_t *>(
+        static_cast<char *>(workspace) + align_up((size_t)num_panels * dimp * sizeof(float), 256));
+    const uint8_t *rec = static_cast<const uint8_t *>(packed);
+    hipStream_t st = as_stream(stream);
+    switch (dim_k) {
+    case 4: return FwdPanelPacked<4>::run(sched, num_panels, indptr, indices, values, rec, num_rows, dim_origin, dim_k, out, carry, carry_row, st);
+    case 8: return FwdPanelPacked<8>::run(sched, num_panels, indptr, indices, values, rec, num_rows, dim_origin, dim_k, out, carry, carry_row, st);
+    default: return FwdPanelPacked<16>::run(sched, num_panels, indptr, indices, values, rec, num_rows, dim_origin, dim_k, out, carry, carry_row, st);
+    }
 }
 
 size_t maxk_forward_multi_workspace_bytes(int64_t num_panels, int dim_origin, int num_rel)

@@ -55,6 +55,8 @@ LOCAL_WAVES_PER_CU = int(os.environ.get("MAXK_LOCAL_WAVES_PER_CU", 16))
 # LOCAL backward: gradient-row bytes per source band (one launch each); about 32 MB keeps a
 # band's G rows resident in the Infinity Cache (tools/exp_local_window.py)
 LOCAL_BAND_BYTES = int(os.environ.get("MAXK_LOCAL_BAND_BYTES", 32 << 20))
+# forward at k in {4, 8, 16}: pack CBSR into one record per node (MAXK_FWD_PACKED=0 disables)
+FWD_PACKED = os.environ.get("MAXK_FWD_PACKED", "1") != "0"
 
 
 def _build_schedule(indptr: torch.Tensor, num_rows: int, num_edges: int, panel_cost: int,
@@ -314,6 +316,16 @@ def spgemm_forward(g: MaxKGraph, data, sel, dim_origin: int = 256, out=None, val
     L = _lib.load()
     nbytes = L.maxk_forward_workspace_bytes(g.num_panels, dim_origin)
     ws = g._workspace(("fwd", dim_origin), nbytes)
+    rs = L.maxk_cbsr_packed_row_bytes(k) if FWD_PACKED else 0
+    if rs:  # k in {4, 8, 16}: one cache line per gathered neighbour (packed records)
+        rec = g._workspace(("packed", k), g.num_cols * rs)
+        _lib.check(L.maxk_cbsr_pack(data.data_ptr(), sel.data_ptr(), g.num_cols, k, rec.data_ptr(),
+                                    _stream(out)), "maxk_cbsr_pack")
+        _lib.check(L.maxk_spgemm_forward_packed(
+            g.sched.data_ptr(), g.num_panels, g.indptr.data_ptr(), g.indices.data_ptr(),
+            values.data_ptr(), rec.data_ptr(), g.num_rows, dim_origin, k, out.data_ptr(),
+            ws.data_ptr(), ws.numel(), _stream(out)), "maxk_spgemm_forward_packed")
+        return out
     _lib.check(L.maxk_spgemm_forward(g.sched.data_ptr(), g.num_panels, g.indptr.data_ptr(),
                                      g.indices.data_ptr(), values.data_ptr(), data.data_ptr(),
                                      sel.data_ptr(), g.num_rows, dim_origin, k, out.data_ptr(),

@@ -403,3 +403,31 @@ def test_forward_multi_edge_cases(dev, oracle, kind):
     for q in range(R):
         ref = oracle.np_forward(indptr, indices, vals[:, q], data, sel, 256)
         assert oracle.parity_error(out[q].cpu().numpy(), ref) <= TOL
+
+
+@pytest.mark.parametrize("k", [4, 8, 16])
+def test_forward_packed_cbsr(dev, oracle, g_small, monkeypatch, k):
+    """Packed CBSR records (k <= 16): record layout, and the packed forward ==
+    the two-array forward == the oracle (including a row split across panels)."""
+    from spgemm_new_amd import ops
+    indptr, indices, values = g_small
+    v = len(indptr) - 1
+    data, sel = random_cbsr(v, k, 256, seed=40 + k)
+    L = _lib.load()
+    rs = L.maxk_cbsr_packed_row_bytes(k)
+    rec = torch.empty(v * rs, dtype=torch.uint8, device=dev)
+    assert L.maxk_cbsr_pack(T(data, dev).data_ptr(), T(sel, dev).data_ptr(), v, k, rec.data_ptr(),
+                            None) == 0
+    torch.cuda.synchronize()
+    r = rec.cpu().numpy().reshape(v, rs)
+    np.testing.assert_array_equal(r[:, :4 * k].copy().view(np.float32), data)
+    np.testing.assert_array_equal(r[:, 4 * k:5 * k], sel)
+    assert not r[:, 5 * k:].any()
+    g = S.MaxKGraph(T(indptr, dev), T(indices, dev), T(values, dev), panel_cost=200)
+    y_packed = g.forward(T(data, dev), T(sel, dev), 256)
+    monkeypatch.setattr(ops, "FWD_PACKED", False)
+    y_plain = g.forward(T(data, dev), T(sel, dev), 256)
+    assert torch.allclose(y_packed, y_plain, rtol=1e-6, atol=1e-6)
+    ref = oracle.np_forward(indptr, indices, values, data, sel, 256)
+    assert oracle.parity_error(y_packed.cpu().numpy(), ref) <= TOL
+    assert L.maxk_cbsr_packed_row_bytes(32) == 0
