@@ -45,6 +45,8 @@ def parse():
     p.add_argument("--partitioned", action="store_true",
                    help="use the multi-GPU (row partition + halo exchange) path even at N=1")
     p.add_argument("--verbose", action="store_true")
+    p.add_argument("--cbsr-order", default="column", choices=["column", "lane", "value"],
+                   help="entry order the HIP top-k producer emits (any order is valid CBSR)")
     p.add_argument("--relations", type=int, default=1,
                    help="R > 1: BASELINE config 5, the fused R-relation forward "
                         "(use with --graph proteins) vs R single-relation forwards")
@@ -229,7 +231,7 @@ def main():
     values = torch.rand(E, generator=gen, device=dev)          # main.cu:83-84 U(0,1)
     X = torch.rand((V, h), generator=gen, device=dev)
     G = torch.rand((V, h), generator=gen, device=dev)
-    data, sel = topk_cbsr(X, k, order="column")  # HIP CBSR producer
+    data, sel = topk_cbsr(X, k, order=args.cbsr_order)  # HIP CBSR producer
     log(f"[bench] graph {args.graph} V={V} E={E} built in {time.time() - t0:.1f}s")
 
     algo = {"auto": _lib.MAXK_BWD_AUTO, "atomic": _lib.MAXK_BWD_ATOMIC,
@@ -353,7 +355,7 @@ def main():
             b.synchronize()
             return a.elapsed_time(b) / reps
         dx_tmp = torch.empty((V, k), device=dev)
-        result["topk_ms"] = round(ev_ms(lambda: topk_cbsr(X, k, order="column")), 4)
+        result["topk_ms"] = round(ev_ms(lambda: topk_cbsr(X, k, order=args.cbsr_order)), 4)
         result["scatter_ms"] = round(ev_ms(lambda: cbsr_scatter(dx_tmp, sel, h)), 4)
         if not args.no_cpu_baseline and rank == 0:
             mask = torch.zeros((V, h), device=dev)

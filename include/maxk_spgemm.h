@@ -169,7 +169,8 @@ int maxk_sspmm_backward_local(const int32_t *seg_edge_off, int num_segments,
  *   dim <= 256) the k largest entries -> cbsr_data[r, j] = x[r, cbsr_sel[r, j]]
  *   (num_rows x k, fp32 / uint8).  NaN counts as the largest value, -0 == +0,
  *   ties at the k-th value go to the lower column.  order: COLUMN = ascending
- *   column, VALUE = descending value (torch.topk's sorted order).  dense_out
+ *   column, VALUE = descending value (torch.topk's sorted order), LANE = column
+ *   ranks interleaved for the forward kernel's lane layout.  dense_out
  *   (nullable, num_rows x dim): the MaxK forward (selected kept, rest 0).
  *   maxk_cbsr_scatter: out[r, :] = 0 except out[r, cbsr_sel[r, j]] = vals[r, j].
  *   maxk_cbsr_mask: out[r, :] = 0 except out[r, c] = src[r, c] for c in
@@ -177,6 +178,7 @@ int maxk_sspmm_backward_local(const int32_t *seg_edge_off, int num_segments,
  * ------------------------------------------------------------------------- */
 #define MAXK_TOPK_ORDER_COLUMN 0
 #define MAXK_TOPK_ORDER_VALUE 1
+#define MAXK_TOPK_ORDER_LANE 2  /* column rank q at VEC*(q % LPE) + q/LPE: the forward's lane layout */
 int maxk_topk_cbsr(const float *x, int num_rows, int dim, int64_t ld, int k, int order,
                    float *cbsr_data, uint8_t *cbsr_sel, float *dense_out, void *stream);
 int maxk_cbsr_scatter(const float *vals, const uint8_t *cbsr_sel, int num_rows, int k, int dim,

@@ -29,6 +29,7 @@ MAXK_BWD_STAGED = 2
 MAXK_BWD_LOCAL = 3
 MAXK_TOPK_ORDER_COLUMN = 0
 MAXK_TOPK_ORDER_VALUE = 1
+MAXK_TOPK_ORDER_LANE = 2
 DEFAULT_PANEL_COST = 2048
 DEFAULT_ROW_COST = 16
 

@@ -1267,8 +1267,9 @@ __device__ __forceinline__ void local_edges_scalar(int e_beg, int e_end,
     const int lane = lane_id();
     const int grp = lane / K, l = lane % K;
     const int full_end = e_beg + ((e_end - e_beg) / R) * R;
-    for (int base = e_beg; base < full_end; base += R)
+    for (int base = e_beg; base < full_end; base += R) {
         local_round<K, WIDE>(erc + base, evl + base, grad, (uint32_t)dim, sl, acc, grp, l);
+    }
     if (full_end < e_end) local_edges_shfl<K>(full_end, e_end, erc, evl, grad, dim, sl, acc);
 }
 

@@ -60,7 +60,20 @@ __device__ __forceinline__ int prefix_count(uint64_t m)
                                      __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0));
 }
 
-template <bool VALUE_ORDER>
+// Lane order (ORDER 2): the column-order rank q is stored at position
+// VEC * (q % LPE) + q / LPE, the forward's lane layout (VEC entries per lane,
+// LPE = k / VEC lanes per edge): the LPE lanes of one forward wave-step then
+// hold consecutive ranks, i.e. columns about 256/k apart, which fall in
+// different LDS banks.  Any order is valid CBSR; this one is only faster.
+__device__ __forceinline__ int lane_order_pos(int q, int k)
+{
+    const int vec = k >= 32 ? 4 : (k >= 16 ? 2 : 1);
+    if (k % vec) return q;
+    const int lpe = k / vec;
+    return vec * (q % lpe) + q / lpe;
+}
+
+template <int ORDER>
 __global__ __launch_bounds__(kBlock) void topk_kernel(const float *__restrict__ x, int num_rows,
                                                       int dim, int64_t ld, int k,
                                                       float *__restrict__ data,
@@ -135,12 +148,14 @@ __global__ __launch_bounds__(kBlock) void topk_kernel(const float *__restrict__ 
         for (int j = 0; j < 4; ++j) pos += prefix_count(sm[j]);
         float *drow = data + r * (int64_t)k;
         uint8_t *srow = sel + r * (int64_t)k;
-        if constexpr (!VALUE_ORDER) {
+        if constexpr (ORDER != MAXK_TOPK_ORDER_VALUE) {
 #pragma unroll
             for (int j = 0; j < 4; ++j) {
                 if (take[j]) {
-                    drow[pos + mine] = v[j];
-                    srow[pos + mine] = (uint8_t)(4 * lane + j);
+                    const int q = pos + mine;
+                    const int o = ORDER == MAXK_TOPK_ORDER_LANE ? lane_order_pos(q, k) : q;
+                    drow[o] = v[j];
+                    srow[o] = (uint8_t)(4 * lane + j);
                     ++mine;
                 }
             }
@@ -232,15 +247,21 @@ int maxk_topk_cbsr(const float *x, int num_rows, int dim, int64_t ld, int k, int
 {
     if (num_rows < 0 || (num_rows > 0 && (!x || !cbsr_data || !cbsr_sel))) return MAXK_E_ARG;
     if (dim < 1 || dim > kMaxDim || k < 1 || k > dim || ld < dim) return MAXK_E_DIM;
-    if (order != MAXK_TOPK_ORDER_COLUMN && order != MAXK_TOPK_ORDER_VALUE) return MAXK_E_ARG;
+    if (order != MAXK_TOPK_ORDER_COLUMN && order != MAXK_TOPK_ORDER_VALUE &&
+        order != MAXK_TOPK_ORDER_LANE)
+        return MAXK_E_ARG;
     if (num_rows == 0) return MAXK_OK;
     hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+    const dim3 g(grid_for(num_rows)), b(kBlock);
     if (order == MAXK_TOPK_ORDER_VALUE)
-        hipLaunchKernelGGL(topk_kernel<true>, dim3(grid_for(num_rows)), dim3(kBlock), 0, st, x,
-                           num_rows, dim, ld, k, cbsr_data, cbsr_sel, dense_out);
+        hipLaunchKernelGGL(topk_kernel<MAXK_TOPK_ORDER_VALUE>, g, b, 0, st, x, num_rows, dim, ld,
+                           k, cbsr_data, cbsr_sel, dense_out);
+    else if (order == MAXK_TOPK_ORDER_LANE)
+        hipLaunchKernelGGL(topk_kernel<MAXK_TOPK_ORDER_LANE>, g, b, 0, st, x, num_rows, dim, ld,
+                           k, cbsr_data, cbsr_sel, dense_out);
     else
-        hipLaunchKernelGGL(topk_kernel<false>, dim3(grid_for(num_rows)), dim3(kBlock), 0, st, x,
-                           num_rows, dim, ld, k, cbsr_data, cbsr_sel, dense_out);
+        hipLaunchKernelGGL(topk_kernel<MAXK_TOPK_ORDER_COLUMN>, g, b, 0, st, x, num_rows, dim, ld,
+                           k, cbsr_data, cbsr_sel, dense_out);
     return launch_status();
 }
 

@@ -431,7 +431,8 @@ def warp4_build(indptr: torch.Tensor, warp_max_nz: int = 64) -> torch.Tensor:
 
 
 # ----------------------------------------------------------------- CBSR producer
-_TOPK_ORDERS = {"column": _lib.MAXK_TOPK_ORDER_COLUMN, "value": _lib.MAXK_TOPK_ORDER_VALUE}
+_TOPK_ORDERS = {"column": _lib.MAXK_TOPK_ORDER_COLUMN, "value": _lib.MAXK_TOPK_ORDER_VALUE,
+                "lane": _lib.MAXK_TOPK_ORDER_LANE}
 
 
 def topk_cbsr(x: torch.Tensor, k: int, order: str = "column", dense: bool = False,
@@ -441,7 +442,8 @@ def topk_cbsr(x: torch.Tensor, k: int, order: str = "column", dense: bool = Fals
     MaxK forward (top-k kept, rest 0).  Replaces torch.topk in the reference's
     producers (direct_kernel_interface.py:79-83, spmm_bindings.cpp:163-184,
     utils/models.py:44-50).  order="column": ascending column; "value":
-    descending value as torch.topk(sorted=True), ties to the lower column.
+    descending value as torch.topk(sorted=True), ties to the lower column;
+    "lane": column ranks interleaved for the forward kernel's lane layout.
     NaN ranks as the largest value."""
     check_tensor(x, "input", torch.float32, dim=2)
     V, h = x.shape

@@ -123,3 +123,23 @@ def test_maxk_autograd_matches_reference_semantics(dev):
     gy = torch.randn_like(y)
     y.backward(gy)
     assert torch.equal(x.grad, gy * mask)
+
+
+@pytest.mark.parametrize("k", [8, 16, 32, 64, 24])
+def test_topk_lane_order_is_a_permutation(dev, k):
+    """Lane order = column order with rank q at VEC*(q % LPE) + q // LPE."""
+    g = torch.Generator(device=dev)
+    g.manual_seed(k)
+    x = torch.randn((500, 256), generator=g, device=dev)
+    dc, sc = S.topk_cbsr(x, k, order="column")
+    dl, sl = S.topk_cbsr(x, k, order="lane")
+    vec = 4 if k >= 32 else (2 if k >= 16 else 1)
+    if k % vec:
+        pos = list(range(k))
+    else:
+        lpe = k // vec
+        pos = [vec * (q % lpe) + q // lpe for q in range(k)]
+    assert sorted(pos) == list(range(k))
+    idx = torch.tensor(pos, device=dev)
+    assert torch.equal(sl[:, idx], sc)
+    assert torch.equal(dl[:, idx], dc)
