@@ -177,7 +177,13 @@ def bench_multi(args, S, indptr, indices, data, sel, V, E, h, k, dev, world):
         b.record(st)
         b.synchronize()
         return a.elapsed_time(b) / args.steps
+    G = torch.rand((R, V, h), generator=gen, device=dev)
+    dx = torch.empty((V, k), device=dev)
+
+    def backward():
+        g.backward_multi(G, sel, vals, out=dx)
     t_f, t_u = timed(fused), timed(unfused)
+    t_b = timed(backward)
     b_fused = E * (4 + 4 * R + 5 * k) + R * 4 * h * V
     b_unf = R * (8 * E + 5 * k * E + 4 * h * V)
     val = b_fused / (t_f / 1e3) / 1e9
@@ -194,6 +200,7 @@ def bench_multi(args, S, indptr, indices, data, sel, V, E, h, k, dev, world):
                      "unit": "GB/s", "frac": round(val / HBM_PEAK_GBS, 4), "traffic": None,
                      "kernel": "spgemm_forward_multi", "algorithmic_bytes_per_launch": b_fused},
         "unfused_ms": round(t_u, 4), "fused_speedup": round(t_u / t_f, 3),
+        "bwd_multi_ms": round(t_b, 4), "bwd_algo": g.last_bwd_algo,
         "unfused_bytes": b_unf,
     }
     print(json.dumps(result), flush=True)

@@ -78,3 +78,29 @@ class SpGEMMFunction(Function):
         sel = ctx.sparse_selector
         dxs = g.backward(grad_output.contiguous(), sel)
         return cbsr_scatter(dxs, sel, ctx.features_shape[1]), None, None
+
+
+class SpGEMMMultiFunction(Function):
+    """Multi-relation aggregation (BASELINE config 5, ogbn-proteins' 8 edge
+    features; no reference counterpart -- the reference sums the edge features
+    into node features, utils/proteins_loader.py:41-44): Y[q] = A_q . topk_k(X)
+    for the relations q of values fp32[E, R].  forward -> fp32[R, V, h]
+    (fused kernel); backward -> mask . sum_q A_q^T G_q."""
+
+    @staticmethod
+    def forward(ctx, features, graph_data, values, maxk):
+        indptr, indices = graph_data[0], graph_data[1]
+        x = features.contiguous()
+        data, sel = topk_cbsr(x, maxk, order="column")
+        g = graph_for(indptr.contiguous(), indices.contiguous(), None)
+        vals = values.contiguous()
+        out = g.forward_multi(data, sel, vals, dim_origin=x.size(1))
+        ctx.graph, ctx.sparse_selector, ctx.values = g, sel, vals
+        ctx.features_shape = x.shape
+        return out
+
+    @staticmethod
+    def backward(ctx, grad_output):
+        g, sel = ctx.graph, ctx.sparse_selector
+        dxs = g.backward_multi(grad_output.contiguous(), sel, ctx.values)
+        return cbsr_scatter(dxs, sel, ctx.features_shape[1]), None, None, None

@@ -221,6 +221,19 @@ class MaxKGraph:
         plan["bands"][ns] = hit
         return hit
 
+    def local_values(self, plan, values: torch.Tensor) -> torch.Tensor:
+        """Edge values other than the graph's own, permuted into the LOCAL plan's
+        edge order; cached per values tensor (and version)."""
+        cache = plan.setdefault("val_cache", {})
+        key = _tensor_key(values)
+        ev = cache.get(key)
+        if ev is None:
+            if len(cache) >= 32:
+                cache.clear()
+            ev = values[: self.num_edges][plan["perm"].long()].contiguous()
+            cache[key] = ev
+        return ev
+
     def local_fits(self, dim_k: int) -> bool:
         """True when the LOCAL plan's waves are all co-resident (one sweep of G)."""
         plan = self.local_plan(dim_k)
@@ -245,7 +258,7 @@ class MaxKGraph:
         if self.num_edges == 0 or torch.cuda.is_current_stream_capturing():
             return _lib.MAXK_BWD_STAGED
         cands = [_lib.MAXK_BWD_STAGED, _lib.MAXK_BWD_ATOMIC]
-        if (values is None or values is self.values) and self.local_plan(k) is not None:
+        if self.local_plan(k) is not None:
             cands.append(_lib.MAXK_BWD_LOCAL)
         best, best_ms = None, float("inf")
         for a in cands:
@@ -283,6 +296,36 @@ class MaxKGraph:
         (fp32[E, R], R <= 16).  Returns fp32[R, V, dim_origin]; equals R
         forward() calls with values[:, q].contiguous()."""
         return spgemm_forward_multi(self, cbsr_data, cbsr_sel, values, dim_origin, out)
+
+    def backward_multi(self, grad: torch.Tensor, cbsr_sel: torch.Tensor, values: torch.Tensor,
+                       out: torch.Tensor | None = None, algo: int = _lib.MAXK_BWD_AUTO):
+        """Backward of forward_multi: dXs = sum_q (A_q^T G_q) sampled at sel,
+        with grad fp32[R, V, h] and values fp32[E, R].  Returns fp32[V, k].
+        Composed from R single-relation backward calls (per-relation value
+        columns cached), summed on the device."""
+        check_tensor(grad, "grad_output", torch.float32, dim=3)
+        check_tensor(values, "values", torch.float32, dim=2)
+        R = values.shape[1]
+        if grad.shape[0] != R or values.shape[0] != self.num_edges:
+            raise RuntimeError("grad must be [R, V, h] and values [E, R]")
+        cols = self._multi_cols(values)
+        k = cbsr_sel.shape[1]
+        if out is None:
+            out = torch.empty((self.num_cols, k), dtype=torch.float32, device=self.device)
+        tmp = torch.empty_like(out) if R > 1 else None
+        for q in range(R):
+            sspmm_backward(self, grad[q], cbsr_sel, out if q == 0 else tmp, cols[q], algo)
+            if q > 0:
+                out.add_(tmp)
+        return out
+
+    def _multi_cols(self, values: torch.Tensor):
+        key = _tensor_key(values)
+        hit = getattr(self, "_cols_cache", None)
+        if hit is None or hit[0] != key:
+            cols = [values[:, q].contiguous() for q in range(values.shape[1])]
+            self._cols_cache = (key, cols)
+        return self._cols_cache[1]
 
     def backward(self, grad: torch.Tensor, cbsr_sel: torch.Tensor, out: torch.Tensor | None = None,
                  values: torch.Tensor | None = None, algo: int = _lib.MAXK_BWD_AUTO) -> torch.Tensor:
@@ -382,16 +425,15 @@ def sspmm_backward(g: MaxKGraph, grad, sel, out=None, values=None, algo: int = _
         algo = _lib.MAXK_BWD_ATOMIC  # nothing to stage: the call just zeroes dXs
     L = _lib.load()
     if algo == _lib.MAXK_BWD_LOCAL:
-        if values is not g.values:
-            raise RuntimeError("the LOCAL backward bakes the graph's edge values into its plan")
         plan = g.local_plan(k)
         if plan is None:
             raise RuntimeError("LOCAL backward unsupported for this shape (k must divide 64)")
         g.last_bwd_algo = "local"
         seg, ns = g.local_bands(plan, dim_origin)
+        ev = plan["edge_val"] if values is g.values else g.local_values(plan, values)
         _lib.check(L.maxk_sspmm_backward_local(
             seg.data_ptr(), ns, plan["dstart"].data_ptr(), plan["num_waves"], plan["dmax"],
-            plan["edge_rc"].data_ptr(), plan["edge_val"].data_ptr(), grad.data_ptr(),
+            plan["edge_rc"].data_ptr(), ev.data_ptr(), grad.data_ptr(),
             sel.data_ptr(), g.num_rows, dim_origin, k, out.data_ptr(), _stream(out)),
             "maxk_sspmm_backward_local")
         return out

@@ -431,3 +431,52 @@ def test_forward_packed_cbsr(dev, oracle, g_small, monkeypatch, k):
     ref = oracle.np_forward(indptr, indices, values, data, sel, 256)
     assert oracle.parity_error(y_packed.cpu().numpy(), ref) <= TOL
     assert L.maxk_cbsr_packed_row_bytes(32) == 0
+
+
+@pytest.mark.parametrize("algo", [_lib.MAXK_BWD_AUTO, _lib.MAXK_BWD_LOCAL, _lib.MAXK_BWD_STAGED])
+def test_backward_multi_relation(dev, oracle, algo):
+    """backward_multi = sum_q of the single-relation backward with values[:, q]."""
+    indptr, indices = small_csr(700, seed=8)
+    v, e, R, k = len(indptr) - 1, len(indices), 8, 32
+    vals = np.random.default_rng(9).random((e, R), dtype=np.float32)
+    _, sel = random_cbsr(v, k, 256, seed=6)
+    grad = np.random.default_rng(10).random((R, v, 256), dtype=np.float32)
+    g = S.MaxKGraph(T(indptr, dev), T(indices, dev))
+    dx = g.backward_multi(T(grad, dev), T(sel, dev), T(vals, dev), algo=algo)
+    ref = sum(oracle.np_backward(indptr, indices, vals[:, q], grad[q], sel) for q in range(R))
+    assert oracle.parity_error(dx.cpu().numpy(), ref) <= TOL
+
+
+def test_local_with_explicit_values(dev, oracle, g_small):
+    indptr, indices, values = g_small
+    v = len(indptr) - 1
+    _, sel = random_cbsr(v, 32, 256, seed=2)
+    grad = np.random.default_rng(3).random((v, 256), dtype=np.float32)
+    g = S.MaxKGraph(T(indptr, dev), T(indices, dev), T(values, dev))
+    other = np.random.default_rng(4).random(len(indices), dtype=np.float32)
+    dx = g.backward(T(grad, dev), T(sel, dev), values=T(other, dev), algo=_lib.MAXK_BWD_LOCAL)
+    ref = oracle.np_backward(indptr, indices, other, grad, sel)
+    assert oracle.parity_error(dx.cpu().numpy(), ref) <= TOL
+
+
+def test_spgemm_multi_autograd(dev):
+    """SpGEMMMultiFunction vs the dense fp64 autograd of Y_q = A_q (mask . X)."""
+    from spgemm_new_amd.models import SpGEMMMultiFunction
+    indptr, indices = small_csr(400, seed=12)
+    v, e, R, k, h = len(indptr) - 1, len(indices), 4, 16, 64
+    gen = torch.Generator(device=dev)
+    gen.manual_seed(1)
+    vals = torch.rand((e, R), generator=gen, device=dev)
+    x = torch.randn((v, h), generator=gen, device=dev, requires_grad=True)
+    gd = (T(indptr, dev), T(indices, dev))
+    y = SpGEMMMultiFunction.apply(x, gd, vals, k)
+    gy = torch.randn_like(y)
+    y.backward(gy)
+    xd = x.detach().double().requires_grad_(True)
+    xm = MaxK.apply(xd, k)
+    yd = torch.stack([torch.sparse.mm(torch.sparse_csr_tensor(gd[0].long(), gd[1].long(),
+                                                              vals[:, q].double(), size=(v, v)), xm)
+                      for q in range(R)])
+    yd.backward(gy.double())
+    assert torch.allclose(y.double(), yd, rtol=1e-4, atol=1e-4)
+    assert torch.allclose(x.grad.double(), xd.grad, rtol=1e-4, atol=1e-4)
