@@ -885,6 +885,8 @@ __device__ __forceinline__ void bwd_edges_stage_vec(int e0, int e1,
                     o.y = v * gs[(sb[u] >> 8) & 0xff];
                     o.z = v * gs[(sb[u] >> 16) & 0xff];
                     o.w = v * gs[sb[u] >> 24];
+                    // non-temporal: plain stores measured slower (Reddit 6.60 -> 6.97 ms,
+                    // products 7.85 -> 8.20 ms): the staging lines would evict selector lines
                     __builtin_nontemporal_store(o, reinterpret_cast<f4 *>(P + (size_t)p * K + sub * 4));
                 }
             }

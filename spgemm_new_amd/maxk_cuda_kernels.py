@@ -34,11 +34,65 @@ def _warp4_checks(warp4_metadata, indices, values, input_data, sparse_selector):
     check_tensor(sparse_selector, "sparse_selector", torch.uint8)
 
 
+_W4_GRAPHS: "OrderedDict" = None
+
+
+def _warp4_graph(warp4, indices, values, num_v: int, num_warps: int):
+    """The CSR graph behind a warp4 chunk list, or None.
+
+    generate_meta.py:26-48 cuts each row's edges, in order, into chunks
+    (row, loc, len, 0); so indptr follows from the lengths, and the fast
+    panel-scheduled kernels (no pre-zeroing, LOCAL backward) give the same
+    result as the chunk kernels.  Used only when all chunks are processed
+    (num_warps covers the list) and the list is exactly such a cut of the
+    edges (rows non-decreasing and < V, loc = running edge offset, lengths sum
+    to E); otherwise the caller keeps the warp4 kernels.  Cached per
+    (warp4, indices, values) tensor state."""
+    global _W4_GRAPHS
+    from collections import OrderedDict
+    if _W4_GRAPHS is None:
+        _W4_GRAPHS = OrderedDict()
+    n_chunks = warp4.numel() // 4
+    if num_warps != n_chunks or warp4.numel() % 4:
+        return None
+    key = tuple((t.data_ptr(), t.numel(), t._version) for t in (warp4, indices, values)) + (num_v,)
+    if key in _W4_GRAPHS:
+        _W4_GRAPHS.move_to_end(key)
+        return _W4_GRAPHS[key][0]
+    w = warp4.view(-1, 4).long()
+    rows, loc, ln = w[:, 0], w[:, 1], w[:, 2]
+    E = indices.numel()
+    ok = True
+    if n_chunks:
+        start = torch.cumsum(ln, 0) - ln
+        ok = bool(((rows >= 0) & (rows < num_v) & (ln >= 0)).all()) \
+            and bool((rows[1:] >= rows[:-1]).all()) and torch.equal(loc, start) \
+            and int(ln.sum()) == E
+    else:
+        ok = E == 0
+    g = None
+    if ok:
+        counts = torch.zeros(num_v, dtype=torch.int64, device=warp4.device)
+        if n_chunks:
+            counts.index_add_(0, rows, ln)
+        indptr = torch.zeros(num_v + 1, dtype=torch.int32, device=warp4.device)
+        indptr[1:] = torch.cumsum(counts, 0).to(torch.int32)
+        g = MaxKGraph(indptr, indices, values)
+    # the entry keeps warp4/indices/values alive, so their addresses are not reused
+    _W4_GRAPHS[key] = (g, warp4, indices, values)
+    while len(_W4_GRAPHS) > 8:
+        _W4_GRAPHS.popitem(last=False)
+    return g
+
+
 def spmm_maxk_forward(warp4_metadata, indices, values, input_data, sparse_selector, num_warps,
                       dim_sparse):
     """cuda_kernel_bindings.cpp:42-104 -> fp32[V, 256]."""
     _warp4_checks(warp4_metadata, indices, values, input_data, sparse_selector)
     num_v = input_data.size(0)
+    g = _warp4_graph(warp4_metadata, indices, values, num_v, int(num_warps))
+    if g is not None and sparse_selector.size(1) == int(dim_sparse):
+        return g.forward(input_data, sparse_selector, FULL_DIM)
     output = torch.zeros((num_v, FULL_DIM), dtype=torch.float32, device=input_data.device)
     num_warps = min(int(num_warps), warp4_metadata.numel() // 4)
     L = _lib.load()
@@ -58,6 +112,10 @@ def spmm_maxk_backward(warp4_metadata, indices, values, grad_output, sparse_sele
     check_tensor(grad_output, "grad_output", torch.float32)
     check_tensor(sparse_selector, "sparse_selector", torch.uint8)
     num_v, feat_in = grad_output.size(0), grad_output.size(1)
+    g = _warp4_graph(warp4_metadata, indices, values, num_v, int(num_warps))
+    if g is not None and sparse_selector.size(1) == int(dim_sparse) \
+            and sparse_selector.size(0) == num_v:
+        return g.backward(grad_output, sparse_selector)
     grad_input = torch.zeros((num_v, int(dim_sparse)), dtype=torch.float32,
                              device=grad_output.device)
     num_warps = min(int(num_warps), warp4_metadata.numel() // 4)

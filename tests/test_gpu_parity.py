@@ -480,3 +480,38 @@ def test_spgemm_multi_autograd(dev):
     yd.backward(gy.double())
     assert torch.allclose(y.double(), yd, rtol=1e-4, atol=1e-4)
     assert torch.allclose(x.grad.double(), xd.grad, rtol=1e-4, atol=1e-4)
+
+
+def test_functional_api_fast_path_and_partial_warps(dev, oracle, g_small):
+    """Full chunk lists run on the panel/LOCAL kernels (graph rebuilt from the
+    warp4 lengths); num_warps < #chunks keeps the reference's partial semantics
+    (only those chunks) on the chunk kernels."""
+    indptr, indices, values = g_small
+    v, h, k = len(indptr) - 1, 256, 32
+    data, sel = random_cbsr(v, k, h, seed=77)
+    grad = np.random.default_rng(78).random((v, h), dtype=np.float32)
+    w4 = oracle.c_warp4(indptr)
+    w4_dev = T(w4.reshape(-1), dev)
+    full = len(w4)
+    y = MCK.spmm_maxk_forward(w4_dev, T(indices, dev), T(values, dev), T(data, dev), T(sel, dev),
+                              full, k)
+    assert MCK._warp4_graph(w4_dev, T(indices, dev), T(values, dev), v, full) is not None
+    assert oracle.parity_error(y.cpu().numpy(),
+                               oracle.c_forward(w4, indices, values, data, sel, h)) <= TOL
+    dx = MCK.spmm_maxk_backward(w4_dev, T(indices, dev), T(values, dev), T(grad, dev), T(sel, dev),
+                                full, k)
+    assert oracle.parity_error(dx.cpu().numpy(),
+                               oracle.c_backward(w4, indices, values, grad, sel)) <= TOL
+    half = full // 2
+    y2 = MCK.spmm_maxk_forward(w4_dev, T(indices, dev), T(values, dev), T(data, dev), T(sel, dev),
+                               half, k)
+    assert oracle.parity_error(y2.cpu().numpy(),
+                               oracle.c_forward(w4[:half], indices, values, data, sel, h)) <= TOL
+    dx2 = MCK.spmm_maxk_backward(w4_dev, T(indices, dev), T(values, dev), T(grad, dev),
+                                 T(sel, dev), half, k)
+    assert oracle.parity_error(dx2.cpu().numpy(),
+                               oracle.c_backward(w4[:half], indices, values, grad, sel)) <= TOL
+    # a chunk list that is not a contiguous cut of the edges is not converted
+    bad = w4.copy()
+    bad[0, 1] += 1
+    assert MCK._warp4_graph(T(bad.reshape(-1), dev), T(indices, dev), T(values, dev), v, full) is None
