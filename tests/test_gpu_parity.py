@@ -515,3 +515,30 @@ def test_functional_api_fast_path_and_partial_warps(dev, oracle, g_small):
     bad = w4.copy()
     bad[0, 1] += 1
     assert MCK._warp4_graph(T(bad.reshape(-1), dev), T(indices, dev), T(values, dev), v, full) is None
+
+
+def test_local_wide_offsets(dev):
+    """G >= 4 GiB selects the 64-bit-offset LOCAL variant (WIDE).  V = 4.2 M rows,
+    h = 256 (4.3 GB of G) with a sparse edge set; reference: a plain PyTorch fp32
+    gather + index_add on the device."""
+    V, h, k, E = 4_200_000, 256, 32, 200_000
+    gen = torch.Generator(device=dev)
+    gen.manual_seed(3)
+    rows = torch.sort(torch.randint(0, V, (E,), generator=gen, device=dev)).values
+    cols = torch.randint(0, V, (E,), generator=gen, device=dev)
+    key = torch.unique(rows * V + cols)
+    rows, cols = key // V, key % V
+    indptr = torch.zeros(V + 1, dtype=torch.int32, device=dev)
+    indptr[1:] = torch.cumsum(torch.bincount(rows, minlength=V), 0).to(torch.int32)
+    vals = torch.rand(rows.numel(), generator=gen, device=dev)
+    G = torch.rand((V, h), generator=gen, device=dev)
+    sel = torch.argsort(torch.rand((V, h), generator=gen, device=dev), dim=1)[:, :k].to(torch.uint8)
+    g = S.MaxKGraph(indptr, cols.to(torch.int32), vals)
+    assert V * h * 4 >= 1 << 32
+    dx = g.backward(G, sel, algo=_lib.MAXK_BWD_LOCAL)
+    contrib = vals[:, None] * G[rows][torch.arange(rows.numel(), device=dev)[:, None],
+                                      sel[cols].long()]
+    ref = torch.zeros((V, k), device=dev).index_add_(0, cols, contrib)
+    err = ((dx - ref).abs() / ref.abs().clamp_min(1)).max().item()
+    assert err <= TOL, err
+    del G
