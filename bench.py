@@ -45,6 +45,8 @@ def parse():
     p.add_argument("--partitioned", action="store_true",
                    help="use the multi-GPU (row partition + halo exchange) path even at N=1")
     p.add_argument("--verbose", action="store_true")
+    p.add_argument("--no-vendor", action="store_true",
+                   help="skip the rocSPARSE (torch.sparse.mm) forward baseline")
     p.add_argument("--cbsr-order", default="column", choices=["column", "lane", "value"],
                    help="entry order the HIP top-k producer emits (any order is valid CBSR)")
     p.add_argument("--relations", type=int, default=1,
@@ -134,6 +136,28 @@ def pmc_traffic(key, call, algo=None, bands=1):
     if any(p is None for p in parts):
         return None, None
     return int(sum(parts)), f"profiles/{ent['profile']}_summary.json"
+
+
+def vendor_baseline(indptr, indices, values, X, sel, y, fwd_ms, ev_ms):
+    """The vendor SpMM the reference compares its kernel with (README.md:136,
+    direct_kernel_interface.py:240-269, cuSPARSE -> here rocSPARSE through
+    torch.sparse.mm): Y = A . (X masked to its top-k), dense h-wide operand,
+    on the same GPU and inputs; also checks it against our forward."""
+    V, h = X.shape
+    a = torch.sparse_csr_tensor(indptr.long(), indices.long(), values, size=(V, V))
+    xm = torch.zeros_like(X).scatter_(1, sel.long(), torch.gather(X, 1, sel.long()))
+    out = {}
+    try:
+        ms = ev_ms(lambda: torch.sparse.mm(a, xm), reps=3)
+        ref = torch.sparse.mm(a, xm)
+        err = float(((ref - y).abs() / ref.abs().clamp_min(1)).max())
+        out = {"kind": "rocSPARSE SpMM via torch.sparse.mm (dense masked operand)",
+               "fwd_ms": round(ms, 3), "speedup_vs_vendor": round(ms / fwd_ms, 2),
+               "max_rel_diff": err}
+    except RuntimeError as e:  # a vendor path missing on this build is reported, not fatal
+        out = {"kind": "rocSPARSE SpMM via torch.sparse.mm", "error": str(e)[:200]}
+    del a, xm
+    return out
 
 
 def _cpu_model():
@@ -352,7 +376,7 @@ def main():
         # reported separately: CBSR producer and dense-gradient scatter
         from spgemm_new_amd.ops import cbsr_scatter
 
-        def ev_ms(fn, reps=5):
+        def ev_ms(fn, reps=5):  # noqa: E306
             fn()
             a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
             a.record(st)
@@ -364,6 +388,9 @@ def main():
         dx_tmp = torch.empty((V, k), device=dev)
         result["topk_ms"] = round(ev_ms(lambda: topk_cbsr(X, k, order=args.cbsr_order)), 4)
         result["scatter_ms"] = round(ev_ms(lambda: cbsr_scatter(dx_tmp, sel, h)), 4)
+        if not args.no_vendor and rank == 0:
+            result["vendor_baseline"] = vendor_baseline(indptr, indices, values, X, sel, y, fms,
+                                                        ev_ms)
         if not args.no_cpu_baseline and rank == 0:
             mask = torch.zeros((V, h), device=dev)
             mask.scatter_(1, sel.long(), 1.0)
