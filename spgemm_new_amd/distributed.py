@@ -30,15 +30,27 @@ import torch.distributed as dist
 from .ops import MaxKGraph
 
 
-def a2a(out: torch.Tensor, inp: torch.Tensor, out_split=None, in_split=None):
+class _Done:
+    def wait(self):
+        return None
+
+
+def a2a(out: torch.Tensor, inp: torch.Tensor, out_split=None, in_split=None,
+        async_op: bool = False):
     """all_to_all_single; with the gloo backend, device tensors are staged
-    through host memory (tests on one GPU).  RCCL ("nccl") runs in place."""
+    through host memory (tests on one GPU) and the call completes before it
+    returns.  RCCL ("nccl") runs in place; with async_op the collective is
+    ordered after the work already on the current stream and the returned
+    handle's wait() orders later work after it, so kernels launched in
+    between overlap the transfer."""
     if out.is_cuda and dist.get_backend() == "gloo":
         o = out.cpu()
         dist.all_to_all_single(o, inp.cpu(), out_split, in_split)
         out.copy_(o)
-    else:
-        dist.all_to_all_single(out, inp, out_split, in_split)
+        return _Done() if async_op else out
+    if async_op:
+        return dist.all_to_all_single(out, inp, out_split, in_split, async_op=True)
+    dist.all_to_all_single(out, inp, out_split, in_split)
     return out
 
 
@@ -105,16 +117,39 @@ class PartitionedMaxK:
     """
 
     def __init__(self, indptr, indices, values, rank: int, world: int, device,
-                 engine=None, row_cost: int = 16, **engine_kw):
+                 engine=None, row_cost: int = 16, overlap: bool = True, **engine_kw):
         self.rank, self.world, self.device = rank, world, torch.device(device)
         self.bounds = row_partition(indptr, world, row_cost)
         self.plan = HaloPlan(indptr, indices, self.bounds, rank, world, self.device)
-        e0, e1 = self.plan.edge_range
+        p = self.plan
+        e0, e1 = p.edge_range
         lv = values[e0:e1].to(self.device).contiguous()
         make = engine or _default_engine
-        self.local = make(self.plan.local_indptr, self.plan.local_indices, lv,
-                          self.plan.num_own + self.plan.num_halo, **engine_kw)
+        # overlap (forward): the block is also split by column into own | halo
+        # parts, so the own part computes while the halo CBSR is in flight.  The
+        # backward keeps the single block: split, each part's LOCAL sweep visits
+        # every source band and the pair cost +0.05 ms (N=8) to +0.31 ms (N=2)
+        # more than the block, more than the exchange they would hide
+        # (tools/exp_rank_local.py).
+        self.overlap = overlap and p.num_halo > 0
+        if self.overlap:
+            li = p.local_indices.long()
+            is_own = li < p.num_own
+            rows = torch.repeat_interleave(
+                torch.arange(p.num_own, device=self.device),
+                (p.local_indptr[1:] - p.local_indptr[:-1]).long(), output_size=li.numel())
+
+            def part(mask, col_shift, ncols):
+                ip = torch.zeros(p.num_own + 1, dtype=torch.int32, device=self.device)
+                ip[1:] = torch.cumsum(torch.bincount(rows[mask], minlength=p.num_own), 0)
+                return make(ip, (li[mask] - col_shift).to(torch.int32).contiguous(),
+                            lv[mask].contiguous(), ncols, **engine_kw)
+            self.local_own = part(is_own, 0, p.num_own)
+            self.local_halo = part(~is_own, p.num_own, p.num_halo)
+        self.local = make(p.local_indptr, p.local_indices, lv, p.num_own + p.num_halo,
+                          **engine_kw)
         self._halo_sel = None
+        self._h_sel = None
 
     # --------------------------------------------------------------- helpers
     def local_rows(self, t: torch.Tensor) -> torch.Tensor:
@@ -144,12 +179,32 @@ class PartitionedMaxK:
         return data, sel
 
     def forward(self, data_own: torch.Tensor, sel_own: torch.Tensor, dim_origin: int = 256):
+        if self.overlap:
+            return self._forward_overlap(data_own, sel_own, dim_origin)
         data, sel = self.gather_halo_cbsr(data_own, sel_own)
         self._halo_sel = sel
         return self.local.forward(data, sel, dim_origin)
 
+    def _forward_overlap(self, data_own, sel_own, dim_origin):
+        p = self.plan
+        k = data_own.shape[1]
+        packed = torch.cat([data_own[p.send_local].view(torch.uint8).reshape(-1, 4 * k),
+                            sel_own[p.send_local]], dim=1).contiguous()
+        recv = torch.empty((sum(p.recv_counts), 5 * k), dtype=torch.uint8, device=self.device)
+        work = a2a(recv, packed, p.recv_counts, p.send_counts, async_op=True)
+        y = self.local_own.forward(data_own, sel_own, dim_origin)   # overlaps the exchange
+        work.wait()
+        h_data = recv[:, : 4 * k].contiguous().view(torch.float32).reshape(-1, k)
+        h_sel = recv[:, 4 * k:].contiguous()
+        self._h_sel = h_sel
+        self._halo_sel = None
+        y += self.local_halo.forward(h_data, h_sel, dim_origin)
+        return y
+
     def backward(self, grad_own: torch.Tensor, sel_own: torch.Tensor | None = None):
         p = self.plan
+        if self._halo_sel is None and self._h_sel is not None and sel_own is not None:
+            self._halo_sel = torch.cat([sel_own, self._h_sel]).contiguous()
         sel = self._halo_sel
         if sel is None or (sel_own is not None and sel.shape[0] != p.num_own + p.num_halo):
             if sel_own is None:

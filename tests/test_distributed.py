@@ -45,7 +45,7 @@ def _free_port():
     return p
 
 
-def _worker(rank, world, port, q):
+def _worker(rank, world, port, q, overlap=True):
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
     dist.init_process_group("gloo", rank=rank, world_size=world)
@@ -57,7 +57,9 @@ def _worker(rank, world, port, q):
         data, sel = random_cbsr(v, k, h, seed=2)
         grad = np.random.default_rng(3).random((v, h), dtype=np.float32)
         m = PartitionedMaxK(torch.from_numpy(indptr), torch.from_numpy(indices),
-                            torch.from_numpy(values), rank, world, "cpu", engine=OracleEngine)
+                            torch.from_numpy(values), rank, world, "cpu", engine=OracleEngine,
+                            overlap=overlap)
+        assert m.overlap == (overlap and m.plan.num_halo > 0)
         y = m.forward(m.local_rows(torch.from_numpy(data)), m.local_rows(torch.from_numpy(sel)), h)
         dx = m.backward(m.local_rows(torch.from_numpy(grad)), m.local_rows(torch.from_numpy(sel)))
         # gather to rank 0
@@ -76,12 +78,14 @@ def _worker(rank, world, port, q):
         dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("world", [2, 3])
-def test_partitioned_matches_single(world):
+@pytest.mark.parametrize("world,overlap", [(2, True), (3, True), (2, False), (3, False)])
+def test_partitioned_matches_single(world, overlap):
+    """overlap=True splits each block into own | halo column parts and runs the
+    exchange asynchronously; overlap=False is the single-block path."""
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, world, port, q)) for r in range(world)]
+    procs = [ctx.Process(target=_worker, args=(r, world, port, q, overlap)) for r in range(world)]
     for p in procs:
         p.start()
     for p in procs:
@@ -103,7 +107,7 @@ def test_row_partition_balance():
         assert max(cost) - min(cost) <= int(np.diff(indptr).max()) + 16 + 1
 
 
-def _gpu_worker(rank, world, port, q):
+def _gpu_worker(rank, world, port, q, overlap=True):
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
     dist.init_process_group("gloo", rank=rank, world_size=world)
@@ -116,7 +120,8 @@ def _gpu_worker(rank, world, port, q):
         data, sel = random_cbsr(v, k, h, seed=2)
         grad = np.random.default_rng(3).random((v, h), dtype=np.float32)
         m = PartitionedMaxK(torch.from_numpy(indptr).to(dev), torch.from_numpy(indices).to(dev),
-                            torch.from_numpy(values).to(dev), rank, world, dev, panel_cost=256)
+                            torch.from_numpy(values).to(dev), rank, world, dev, panel_cost=256,
+                            overlap=overlap)
         td = lambda a: m.local_rows(torch.from_numpy(a).to(dev))  # noqa: E731
         y = m.forward(td(data), td(sel), h)
         dx = m.backward(td(grad), td(sel))
@@ -134,13 +139,14 @@ def _gpu_worker(rank, world, port, q):
 
 
 @pytest.mark.gpu
-def test_partitioned_hip_engine_two_ranks_one_gpu():
+@pytest.mark.parametrize("overlap", [True, False])
+def test_partitioned_hip_engine_two_ranks_one_gpu(overlap):
     """2 ranks share cuda:0; HIP kernels on rectangular row blocks with halo columns;
     exchange over gloo (staged through host)."""
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_gpu_worker, args=(r, 2, port, q)) for r in range(2)]
+    procs = [ctx.Process(target=_gpu_worker, args=(r, 2, port, q, overlap)) for r in range(2)]
     for p in procs:
         p.start()
     for p in procs:

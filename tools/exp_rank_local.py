@@ -60,9 +60,34 @@ def main():
             g.backward(g_l, s_l, out=dx)  # autotune
             tf = timed(lambda: g.forward(d_l, s_l, h, out=y))
             tb = timed(lambda: g.backward(g_l, s_l, out=dx))
+            msg = ""
+            if world > 1:  # the overlap split: own-column and halo-column blocks
+                li = local
+                rows = torch.repeat_interleave(torch.arange(r1 - r0, device=dev),
+                                               (lip[1:] - lip[:-1]).long())
+                lv = values[e0:e1]
+                parts = []
+                for m, shift, nc in ((li < (r1 - r0), 0, r1 - r0),
+                                     (li >= (r1 - r0), r1 - r0, halo.numel())):
+                    ip = torch.zeros(r1 - r0 + 1, dtype=torch.int32, device=dev)
+                    ip[1:] = torch.cumsum(torch.bincount(rows[m], minlength=r1 - r0), 0)
+                    parts.append(S.MaxKGraph(ip, (li[m] - shift).to(torch.int32).contiguous(),
+                                             lv[m].contiguous(), num_cols=nc))
+                go, gh = parts
+                d_o, s_o = d_l[: r1 - r0].contiguous(), s_l[: r1 - r0].contiguous()
+                d_h, s_h = d_l[r1 - r0:].contiguous(), s_l[r1 - r0:].contiguous()
+                go.backward(g_l, s_o)
+                gh.backward(g_l, s_h)
+                tfo = timed(lambda: go.forward(d_o, s_o, h))
+                tfh = timed(lambda: gh.forward(d_h, s_h, h))
+                tbo = timed(lambda: go.backward(g_l, s_o))
+                tbh = timed(lambda: gh.backward(g_l, s_h))
+                msg = (f" | split fwd own {tfo:.3f} + halo {tfh:.3f}, bwd own {tbo:.3f} + halo "
+                       f"{tbh:.3f} ms")
+                del go, gh, parts
             print(f"world={world} rank={rank}: rows={r1 - r0} edges={e1 - e0} halo={halo.numel()} "
                   f"fwd {tf:.3f} ms bwd {tb:.3f} ms ({g.last_bwd_algo}) "
-                  f"halo fwd {halo.numel() * 5 * k / 1e6:.1f} MB", flush=True)
+                  f"halo fwd {halo.numel() * 5 * k / 1e6:.1f} MB" + msg, flush=True)
             del g, d_l, s_l, g_l, y, dx
             torch.cuda.empty_cache()
 
