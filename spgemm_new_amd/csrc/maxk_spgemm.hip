@@ -3,26 +3,27 @@
 // Forward  SpGEMM  Y[r,:]   = sum_e val[e] * scatter_h(data[c], sel[c])   (K1, spmm_maxk.cu:17-106)
 // Backward SSpMM   dXs[c,l] = sum_{e:idx[e]=c} val[e] * G[row(e), sel[c,l]] (K2, spmm_maxk_backward.cu:15-115)
 //
-// Design (DESIGN.md has the full rationale and the rooflines):
+// Design (DESIGN.md has the full rationale, the measurements and the rooflines):
 //  * Work decomposition: merge-path panels over "edges of row r, end of row r"
 //    (one wavefront = one panel, equal edge+row cost), built on the device
 //    from indptr.  Rows are never assumed short; a row split across panels is
 //    finished by a carry fixup, so no output is pre-zeroed and no global
 //    atomic touches a row that one wave owns.
-//  * Forward: per wave a fp32 row accumulator in LDS (dim_origin floats).
-//    Each lane gathers 16 B of a neighbour's CBSR values (dwordx4) and the
-//    matching 4 selector bytes (dword), then ds_add_f32's the 4 products into
-//    the accumulator at the selected columns.  A finished row leaves with one
-//    coalesced 16 B/lane store.
-//  * Backward, two algorithms behind one entry point:
+//  * Forward: EPS edges per wave-instruction, each with a private LDS row copy
+//    (plain ds_read/add/ds_write is race-free; LDS float atomics measured ~7x
+//    slower).  CBSR data gathered non-temporally, selector words plain; for
+//    k <= 16 a packed record (data + selectors in one line).  Fused
+//    multi-relation variants share one CBSR gather across R relations.
+//  * Backward, three algorithms behind one entry point:
 //      ATOMIC  push: G[r,:] staged in LDS once per (row, panel); per edge the
-//              k sampled gradients are gathered from LDS and added into
-//              dXs[c,:] with no-return global float atomics, 256 contiguous
-//              bytes per wave-instruction.
-//      STAGED  push to staging rows: the same gather writes each edge's
-//              k-vector to P[csc_pos[e]] (full 16 B/lane rows, non-temporal),
-//              then a merge-path segmented sum over the CSC ranges writes
-//              dXs with plain stores (no atomics at all).
+//              k sampled gradients are added into dXs[c,:] with no-return
+//              global float atomics (the reference's scheme, fixed).
+//      STAGED  push to staging rows P[csc_pos[e]] (non-temporal 16 B stores),
+//              then a merge-path segmented sum over the CSC ranges.
+//      LOCAL   destination-owned: dXs and selectors of <= dmax destinations in
+//              a wave's LDS, in-edges sorted by source row, one launch per
+//              source band so the G window stays cache-resident; edge records
+//              read into SGPRs (k = 32, 64).
 //  * wave64 everywhere; no CUDA-isms, no warp32 tiling.
 #include <hip/hip_runtime.h>
 #include <stdint.h>
