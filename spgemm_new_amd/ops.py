@@ -7,7 +7,12 @@ need that the reference kept in files or rebuilt per call:
   kernels/generate_meta.py:26-48, read per call at spmm_maxk.cu:117);
 * the CSC transpose (edge -> CSC slot, CSC row pointer and its own panel
   schedule) used by the STAGED backward;
-* cached workspaces (carry rows, staging rows).
+* the LOCAL backward plan (destination ranges, in-edges sorted by source row,
+  source bands) and the measured AUTO backward choice;
+* cached workspaces (carry rows, staging rows, packed CBSR records).
+
+Also here: the CBSR producer (top-k), the dense gradient scatter / MaxK mask,
+and the fused multi-relation forward.
 
 All compute goes through the C ABI (``_lib``); there is no CPU or PyTorch
 fallback for the kernels.  Building the transpose uses torch GPU sort/scan
@@ -49,7 +54,7 @@ def _tensor_key(t):
     return (t.data_ptr(), t.numel(), t._version)
 
 
-# LOCAL backward: target LDS bytes per wave (8 waves per CU share 160 KiB)
+# LOCAL backward: target LDS bytes per wave (16 waves per CU share 160 KiB)
 LOCAL_WAVE_LDS_BYTES = int(os.environ.get("MAXK_LOCAL_WAVE_LDS", 10 * 1024))
 LOCAL_WAVES_PER_CU = int(os.environ.get("MAXK_LOCAL_WAVES_PER_CU", 16))
 # LOCAL backward: gradient-row bytes per source band (one launch each); about 32 MB keeps a
@@ -226,13 +231,15 @@ class MaxKGraph:
         edge order; cached per values tensor (and version)."""
         cache = plan.setdefault("val_cache", {})
         key = _tensor_key(values)
-        ev = cache.get(key)
-        if ev is None:
+        hit = cache.get(key)
+        if hit is None:
             if len(cache) >= 32:
                 cache.clear()
             ev = values[: self.num_edges][plan["perm"].long()].contiguous()
-            cache[key] = ev
-        return ev
+            # the entry holds `values` too: while cached its address cannot be
+            # reused by another tensor that would then match the key
+            hit = cache[key] = (ev, values)
+        return hit[0]
 
     def local_fits(self, dim_k: int) -> bool:
         """True when the LOCAL plan's waves are all co-resident (one sweep of G)."""
@@ -324,7 +331,7 @@ class MaxKGraph:
         hit = getattr(self, "_cols_cache", None)
         if hit is None or hit[0] != key:
             cols = [values[:, q].contiguous() for q in range(values.shape[1])]
-            self._cols_cache = (key, cols)
+            self._cols_cache = (key, cols, values)  # holds values: its address stays unique
         return self._cols_cache[1]
 
     def backward(self, grad: torch.Tensor, cbsr_sel: torch.Tensor, out: torch.Tensor | None = None,
