@@ -10,8 +10,9 @@
 // topk_kernel: one wave64 per row (dim <= 256: each lane holds 4 entries,
 // loaded as one float4 when the row allows).  Entries map to order-preserving
 // u32 keys (NaN = the largest key, as torch.topk treats NaN; -0 == +0).  The
-// k-th largest key T comes from a 32-step bitwise search: per step, four
-// v_cmp produce lane masks and s_bcnt1 counts them (no LDS, no sort).
+// k-th largest key T comes from a counting search: per step, four v_cmp
+// produce lane masks and s_bcnt1 counts them (no LDS, no sort); the search
+// gallops from the previous row's threshold and bisects with an early stop.
 // Selected = key > T, plus the lowest-column entries with key == T until k
 // are taken (ties go to the lower column).  Output order:
 //   column order: ascending column (prefix counts with v_mbcnt);
@@ -96,6 +97,7 @@ __global__ __launch_bounds__(kBlock) void topk_kernel(const float *__restrict__ 
         }
     };
     int64_t r = (int64_t)blockIdx.x * kWavesPerBlock + wl;
+    uint32_t prevT = 0xbf800000u;  // key of 1.0f: a start for the first row
     float nx[4] = {0.f, 0.f, 0.f, 0.f};
     if (r < num_rows) load_row(r, nx);
     for (; r < num_rows; r += nwaves) {
@@ -106,18 +108,58 @@ __global__ __launch_bounds__(kBlock) void topk_kernel(const float *__restrict__ 
         if (r + nwaves < num_rows) load_row(r + nwaves, nx);  // next row in flight
 #pragma unroll
         for (int j = 0; j < 4; ++j) key[j] = (4 * lane + j < dim) ? float_key(v[j]) : 0u;
-        // largest T with #{key >= T} >= k (every valid key is >= 0x007fffff > 0);
-        // stops early once exactly k keys are >= T: then they are the selection
-        uint32_t T = 0;
-        for (int b = 31; b >= 0; --b) {
-            const uint32_t cand = T | (1u << b);
+        // T = the largest key value with #{key >= T} >= k (the k-th largest key),
+        // or any T with exactly k keys >= T (then those k are the selection).
+        // Search: bracket [lo, hi) with count(lo) >= k > count(hi), found by
+        // galloping from the previous row's T (rows of one feature matrix have
+        // similar distributions), then bisection with an early stop.
+        auto count_ge = [&](uint64_t t) -> int {
+            if (t > 0xffffffffull) return 0;
+            const uint32_t c32 = (uint32_t)t;
             int cnt = 0;
 #pragma unroll
-            for (int j = 0; j < 4; ++j) cnt += popc64(__ballot(key[j] >= cand));
-            if (cnt >= k) {
-                T = cand;
-                if (cnt == k) break;
+            for (int j = 0; j < 4; ++j) cnt += popc64(__ballot(key[j] >= c32));
+            return cnt;
+        };
+        uint64_t lo, hi;
+        uint32_t T;
+        bool exact = false;
+        {
+            const int c0 = count_ge(prevT);
+            if (c0 == k) {
+                T = prevT;
+                exact = true;
+            } else if (c0 > k) {  // gallop up
+                lo = prevT;
+                uint64_t step = 1u << 12;
+                for (;;) {
+                    const uint64_t t = lo + step;
+                    const int c = count_ge(t);
+                    if (c == k) { T = (uint32_t)t; exact = true; break; }
+                    if (c < k) { hi = t; break; }
+                    lo = t;
+                    step <<= 2;
+                }
+            } else {  // gallop down (count(0) = #valid >= k, so this ends)
+                hi = prevT;
+                uint64_t step = 1u << 12;
+                for (;;) {
+                    const uint64_t t = hi > step ? hi - step : 0;
+                    const int c = count_ge(t);
+                    if (c == k) { T = (uint32_t)t; exact = true; break; }
+                    if (c > k) { lo = t; break; }
+                    hi = t;
+                    step <<= 2;
+                }
             }
+            while (!exact && hi - lo > 1) {
+                const uint64_t mid = lo + ((hi - lo) >> 1);
+                const int c = count_ge(mid);
+                if (c == k) { T = (uint32_t)mid; exact = true; break; }
+                if (c > k) lo = mid; else hi = mid;
+            }
+            if (!exact) T = (uint32_t)lo;
+            prevT = T;
         }
         uint64_t gt[4], eq[4];
         int n_gt = 0;
