@@ -340,6 +340,35 @@ def main():
         p = model.plan
         result["config"]["halo_nodes_rank0"] = p.num_halo
         result["config"]["own_nodes_rank0"] = p.num_own
+        result["config"]["overlap"] = model.overlap
+        # per-call timing on each rank (HIP events on the launch stream; the
+        # calls include their halo all-to-all-v), max over ranks
+        st = torch.cuda.current_stream()
+        fw, bw = [], []
+        for _ in range(args.steps):
+            e0, e1, e2 = (torch.cuda.Event(enable_timing=True) for _ in range(3))
+            e0.record(st)
+            model.forward(data_l, sel_l, h)
+            e1.record(st)
+            model.backward(G_l, sel_l)
+            e2.record(st)
+            e2.synchronize()
+            fw.append(e0.elapsed_time(e1))
+            bw.append(e1.elapsed_time(e2))
+        b_rank = model.algorithmic_bytes(k, h)
+        t = torch.tensor([sum(fw) / len(fw), sum(bw) / len(bw), float(b_rank)], device=dev,
+                         dtype=torch.float64)
+        if dist:
+            dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        fms, bms, b_max = float(t[0]), float(t[1]), float(t[2])
+        dom = ("sspmm_backward", bms) if bms >= fms else ("spgemm_forward", fms)
+        ach = b_max / (dom[1] / 1e3) / 1e9
+        result["roofline"] = {"bound": "hbm", "achieved": round(ach, 1), "peak": HBM_PEAK_GBS,
+                              "unit": "GB/s", "frac": round(ach / HBM_PEAK_GBS, 4),
+                              "traffic": None, "kernel": dom[0] + " (per rank, incl. halo exchange)",
+                              "algorithmic_bytes_per_launch": int(b_max)}
+        result["fwd_ms"] = round(fms, 4)
+        result["bwd_ms"] = round(bms, 4)
     if not partitioned:
         # per-call timing with HIP events on the launch stream (the current stream)
         st = torch.cuda.current_stream()

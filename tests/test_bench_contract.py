@@ -1,0 +1,37 @@
+"""bench.py's output contract (the driver parses its last stdout line): one JSON
+object with the metric, whole-job value, timing fields, roofline and
+cpu_baseline objects.  Runs a small configuration as a subprocess (GPU)."""
+import json
+import os
+import subprocess
+import sys
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("extra", [[], ["--partitioned"], ["--graph", "proteins", "--relations", "4"]])
+def test_bench_json_line(extra):
+    cmd = [sys.executable, os.path.join(ROOT, "bench.py"), "--graph", "flickr", "--h", "64",
+           "--k", "16", "--steps", "2", "--warmup", "1", "--cpu-seconds", "1", "--no-vendor"] + extra
+    if "--relations" in extra:
+        cmd = [sys.executable, os.path.join(ROOT, "bench.py"), "--steps", "2", "--warmup", "1",
+               "--k", "32"] + extra
+    out = subprocess.run(cmd, cwd=ROOT, capture_output=True, text=True, timeout=600)
+    assert out.returncode == 0, out.stderr[-2000:]
+    line = out.stdout.strip().splitlines()[-1]
+    d = json.loads(line)
+    for key in ("metric", "value", "unit", "n_gpus", "steps", "warmup", "ms_per_step",
+                "higher_is_better", "scaling", "vs_baseline", "dtype", "data", "config",
+                "roofline"):
+        assert key in d, key
+    assert d["n_gpus"] == 1 and d["steps"] == 2 and d["value"] > 0
+    r = d["roofline"]
+    assert r["bound"] == "hbm" and r["peak"] == 8000.0 and 0 < r["frac"] < 1.5
+    assert abs(r["frac"] - r["achieved"] / r["peak"]) < 1e-3
+    if not extra:
+        cb = d["cpu_baseline"]
+        assert cb["kind"] == "reference" and cb["value"] > 0 and cb["cores"] >= 1
+        assert "sample" in cb
