@@ -415,6 +415,13 @@ def main():
             b.synchronize()
             return a.elapsed_time(b) / reps
         dx_tmp = torch.empty((V, k), device=dev)
+        # compulsory bytes (each operand once) and the achievable
+        # ceiling of a plain device copy (read + write of 1 GiB)
+        result["compulsory_bytes_fwd"] = 8 * E + 5 * k * V + 4 * h * V
+        src = torch.empty(1 << 28, dtype=torch.float32, device=dev)
+        dst = torch.empty_like(src)
+        result["copy_GBs"] = round(2 * src.numel() * 4 / ev_ms(lambda: dst.copy_(src)) / 1e6, 1)
+        del src, dst
         result["topk_ms"] = round(ev_ms(lambda: topk_cbsr(X, k, order=args.cbsr_order)), 4)
         result["scatter_ms"] = round(ev_ms(lambda: cbsr_scatter(dx_tmp, sel, h)), 4)
         if not args.no_vendor and rank == 0:
