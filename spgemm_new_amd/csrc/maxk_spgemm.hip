@@ -221,7 +221,10 @@ __device__ __forceinline__ void fwd_edges_vec(int e0, int e1, const int32_t *__r
     using Lay = FwdLayout<K>;
     constexpr int VEC = Lay::VEC, LPE = Lay::LPE, EPS = Lay::EPS;
     constexpr int STEPS = kWave / EPS;  // steps per 64-edge batch
-    constexpr int U = STEPS < 8 ? STEPS : 8;
+#ifndef FWD_U
+#define FWD_U 8
+#endif
+    constexpr int U = STEPS < FWD_U ? STEPS : FWD_U;  // gathers in flight per lane
     using D = typename VecT<VEC>::D;
     using SB = typename VecT<VEC>::S;
     const int lane = lane_id();
