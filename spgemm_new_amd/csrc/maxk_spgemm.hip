@@ -173,7 +173,12 @@ struct FwdLayout {
     static constexpr int EPS = kWave / LPE;
 };
 
-__host__ __device__ constexpr int fwd_copies_generic(int k) { return k >= kWave ? 1 : kWave / k; }
+// Generic k: 64/k edges per step, capped at 8 (each slot owns a 1 KB row copy;
+// uncapped, k = 1 would need 64 KB per wave and the launch would fail).
+__host__ __device__ constexpr int fwd_copies_generic(int k)
+{
+    return k >= kWave ? 1 : (kWave / k < 8 ? kWave / k : 8);
+}
 
 template <int K>
 __host__ __device__ constexpr int fwd_copies(int k)
@@ -282,7 +287,7 @@ __device__ __forceinline__ void fwd_edges_scalar(int e0, int e1, int k,
 {
     const int lane = lane_id();
     if (k <= kWave) {
-        const int eps = kWave / k;
+        const int eps = fwd_copies_generic(k);
         const int slot = lane / k, l = lane % k;
         float *my_acc = acc + slot * kMaxDim;
         for (int e = e0; e < e1; e += eps) {

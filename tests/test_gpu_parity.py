@@ -542,3 +542,22 @@ def test_local_wide_offsets(dev):
     err = ((dx - ref).abs() / ref.abs().clamp_min(1)).max().item()
     assert err <= TOL, err
     del G
+
+
+@pytest.mark.parametrize("k,h", [(1, 256), (2, 256), (1, 1), (2, 3), (1, 64), (2, 2)])
+@pytest.mark.parametrize("algo", [_lib.MAXK_BWD_ATOMIC, _lib.MAXK_BWD_STAGED, _lib.MAXK_BWD_LOCAL])
+def test_tiny_k_and_h(dev, oracle, g_small, k, h, algo):
+    """k = 1, 2 (LOCAL with 64 / 32 edges per wave-instruction, generic forward)
+    and h down to 1."""
+    indptr, indices, values = g_small
+    v = len(indptr) - 1
+    data, sel = random_cbsr(v, k, h, seed=k * 10 + h)
+    g = S.MaxKGraph(T(indptr, dev), T(indices, dev), T(values, dev), panel_cost=300)
+    y = g.forward(T(data, dev), T(sel, dev), h)
+    assert oracle.parity_error(y.cpu().numpy(),
+                               oracle.np_forward(indptr, indices, values, data, sel, h)) <= TOL
+    grad = np.random.default_rng(h).random((v, h), dtype=np.float32)
+    dx = torch.full((v, k), float("nan"), device=dev)
+    g.backward(T(grad, dev), T(sel, dev), out=dx, algo=algo)
+    assert oracle.parity_error(dx.cpu().numpy(),
+                               oracle.np_backward(indptr, indices, values, grad, sel)) <= TOL
