@@ -804,6 +804,9 @@ __device__ __forceinline__ void stage_row(float *gs, const float *__restrict__ g
     } else {
         for (int c = lane; c < dim; c += kWave) gs[c] = g[c];
     }
+    // selector bytes >= dim (invalid input) read 0: every algorithm then gives
+    // such an entry no contribution, as LOCAL and the forward do
+    for (int c = dim + lane; c < kMaxDim; c += kWave) gs[c] = 0.f;
     wave_sync_lds();
 }
 

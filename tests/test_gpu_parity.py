@@ -561,3 +561,25 @@ def test_tiny_k_and_h(dev, oracle, g_small, k, h, algo):
     g.backward(T(grad, dev), T(sel, dev), out=dx, algo=algo)
     assert oracle.parity_error(dx.cpu().numpy(),
                                oracle.np_backward(indptr, indices, values, grad, sel)) <= TOL
+
+
+@pytest.mark.parametrize("algo", [_lib.MAXK_BWD_ATOMIC, _lib.MAXK_BWD_STAGED, _lib.MAXK_BWD_LOCAL])
+def test_out_of_range_selectors(dev, oracle, g_small, algo):
+    """Selector bytes >= h (invalid input; undefined in the reference) contribute
+    nothing, consistently: the forward drops them, every backward writes 0."""
+    indptr, indices, values = g_small
+    v, h, k = len(indptr) - 1, 100, 32
+    data, sel = random_cbsr(v, k, 256, seed=5)          # columns up to 255 > h
+    bad = sel >= h
+    g = S.MaxKGraph(T(indptr, dev), T(indices, dev), T(values, dev), panel_cost=300)
+    y = g.forward(T(data, dev), T(sel, dev), h)
+    # expected: the 256-wide result restricted to the first h columns
+    ref_y = oracle.np_forward(indptr, indices, values, data, sel, 256)[:, :h]
+    assert oracle.parity_error(y.cpu().numpy(), ref_y) <= TOL
+    grad = np.random.default_rng(6).random((v, h), dtype=np.float32)
+    dx = g.backward(T(grad, dev), T(sel, dev), algo=algo).cpu().numpy()
+    g256 = np.zeros((v, 256), np.float32)
+    g256[:, :h] = grad                                    # columns >= h read as 0
+    ref = oracle.np_backward(indptr, indices, values, g256, sel)
+    assert bad.any() and not ref[bad].any()
+    assert oracle.parity_error(dx, ref) <= TOL
