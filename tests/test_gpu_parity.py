@@ -583,3 +583,58 @@ def test_out_of_range_selectors(dev, oracle, g_small, algo):
     ref = oracle.np_backward(indptr, indices, values, g256, sel)
     assert bad.any() and not ref[bad].any()
     assert oracle.parity_error(dx, ref) <= TOL
+
+
+@pytest.mark.parametrize("k,algo", [(32, _lib.MAXK_BWD_LOCAL), (8, _lib.MAXK_BWD_LOCAL),
+                                    (8, _lib.MAXK_BWD_ATOMIC)])
+def test_hipgraph_full_step(dev, oracle, g_small, monkeypatch, k, algo):
+    """A whole step captured once and replayed on new inputs: HIP top-k,
+    forward (packed records at k=8), LOCAL / ATOMIC backward over several
+    source bands, dense gradient scatter.  Plans are built by a warm-up call
+    before capture; the calls themselves allocate nothing and never sync."""
+    from spgemm_new_amd import ops
+    monkeypatch.setattr(ops, "LOCAL_BAND_BYTES", 200 * 1024)   # several bands
+    indptr, indices, values = g_small
+    v, h = len(indptr) - 1, 256
+    g = S.MaxKGraph(T(indptr, dev), T(indices, dev), T(values, dev))
+    x = torch.empty((v, h), device=dev)
+    gr = torch.empty((v, h), device=dev)
+    d = torch.empty((v, k), device=dev)
+    s = torch.empty((v, k), dtype=torch.uint8, device=dev)
+    y = torch.empty((v, h), device=dev)
+    dx = torch.empty((v, k), device=dev)
+    gx = torch.empty((v, h), device=dev)
+
+    def step():
+        S.topk_cbsr(x, k, data=d, sel=s)
+        g.forward(d, s, h, out=y)
+        g.backward(gr, s, out=dx, algo=algo)
+        S.cbsr_scatter(dx, s, h, out=gx)
+    x.copy_(torch.rand((v, h), device=dev))
+    gr.copy_(torch.rand((v, h), device=dev))
+    step()                                          # builds plans and workspaces
+    torch.cuda.synchronize()
+    graph = torch.cuda.CUDAGraph()
+    stream = torch.cuda.Stream()
+    stream.wait_stream(torch.cuda.current_stream())
+    with torch.cuda.stream(stream):
+        with torch.cuda.graph(graph, stream=stream):
+            step()
+    torch.cuda.current_stream().wait_stream(stream)
+    gen = np.random.default_rng(k)
+    xn = gen.random((v, h), dtype=np.float32)
+    gn = gen.random((v, h), dtype=np.float32)
+    x.copy_(T(xn, dev))
+    gr.copy_(T(gn, dev))
+    graph.replay()
+    torch.cuda.synchronize()
+    data, sel = d.cpu().numpy(), s.cpu().numpy()
+    ti = torch.topk(torch.from_numpy(xn), k, dim=1).indices.numpy()
+    assert np.array_equal(np.sort(sel.astype(np.int64), 1), np.sort(ti, 1))
+    assert oracle.parity_error(y.cpu().numpy(),
+                               oracle.np_forward(indptr, indices, values, data, sel, h)) <= TOL
+    ref = oracle.np_backward(indptr, indices, values, gn, sel)
+    assert oracle.parity_error(dx.cpu().numpy(), ref) <= TOL
+    dense = np.zeros((v, h))
+    np.put_along_axis(dense, sel.astype(np.int64), ref, axis=1)
+    assert oracle.parity_error(gx.cpu().numpy(), dense) <= TOL
