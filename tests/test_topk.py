@@ -143,3 +143,21 @@ def test_topk_lane_order_is_a_permutation(dev, k):
     idx = torch.tensor(pos, device=dev)
     assert torch.equal(sl[:, idx], sc)
     assert torch.equal(dl[:, idx], dc)
+
+
+def test_topk_abi_row_stride(dev):
+    """C ABI: rows ld floats apart (a column slice of a wider matrix)."""
+    g = torch.Generator(device=dev)
+    g.manual_seed(21)
+    big = torch.randn((300, 132), generator=g, device=dev)
+    for dim, k in ((100, 16), (128, 32), (7, 3)):
+        data = torch.empty((300, k), device=dev)
+        sel = torch.empty((300, k), dtype=torch.uint8, device=dev)
+        L = _lib.load()
+        assert L.maxk_topk_cbsr(big.data_ptr(), 300, dim, 132, k, _lib.MAXK_TOPK_ORDER_VALUE,
+                                data.data_ptr(), sel.data_ptr(), None, None) == 0
+        torch.cuda.synchronize()
+        ref_v, ref_i = torch.topk(big[:, :dim], k, dim=1)
+        assert torch.equal(sel.long(), ref_i) and torch.equal(data, ref_v)
+    assert L.maxk_topk_cbsr(big.data_ptr(), 300, 100, 99, 8, 0, data.data_ptr(), sel.data_ptr(),
+                            None, None) == _lib.MAXK_E_DIM
