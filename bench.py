@@ -423,6 +423,15 @@ def main():
         result["copy_GBs"] = round(2 * src.numel() * 4 / ev_ms(lambda: dst.copy_(src)) / 1e6, 1)
         del src, dst
         result["topk_ms"] = round(ev_ms(lambda: topk_cbsr(X, k, order=args.cbsr_order)), 4)
+        # end-to-end autograd step: SpGEMMFunction forward + backward =
+        # top-k, SpGEMM, SSpMM and the dense gradient scatter
+        from spgemm_new_amd.models import SpGEMMFunction
+        xg = X.clone().requires_grad_(True)
+
+        def autograd_step():
+            SpGEMMFunction.apply(xg, (indptr, indices, values), k).backward(G)
+        result["autograd_step_ms"] = round(ev_ms(autograd_step), 4)
+        del xg
         result["scatter_ms"] = round(ev_ms(lambda: cbsr_scatter(dx_tmp, sel, h)), 4)
         if not args.no_vendor and rank == 0:
             result["vendor_baseline"] = vendor_baseline(indptr, indices, values, X, sel, y, fms,
