@@ -397,6 +397,9 @@ def main():
                               "traffic": traffic, "traffic_source": tsrc, "kernel": dom[0],
                               "algorithmic_bytes_per_launch": b_call,
                               "launches_per_call": bands if dom[0] == "sspmm_backward" else 1}
+        # per-launch average, directly comparable with the rocprofv3 kernel stats
+        result["roofline"]["launch_avg_ms"] = round(
+            dom[1] / result["roofline"]["launches_per_call"], 4)
         result["config"]["bwd_algo"] = g.last_bwd_algo
         result["fwd_ms"] = round(fms, 4)
         result["bwd_ms"] = round(bms, 4)
