@@ -397,9 +397,14 @@ def main():
                               "traffic": traffic, "traffic_source": tsrc, "kernel": dom[0],
                               "algorithmic_bytes_per_launch": b_call,
                               "launches_per_call": bands if dom[0] == "sspmm_backward" else 1}
-        # per-launch average, directly comparable with the rocprofv3 kernel stats
-        result["roofline"]["launch_avg_ms"] = round(
-            dom[1] / result["roofline"]["launches_per_call"], 4)
+        # per-launch figures, directly comparable with the rocprofv3 kernel stats
+        # (achieved = bytes per launch / launch average = bytes per call / call time)
+        rf = result["roofline"]
+        rf["algorithmic_bytes_per_call"] = b_call
+        rf["algorithmic_bytes_per_launch"] = b_call // rf["launches_per_call"]
+        rf["launch_avg_ms"] = round(dom[1] / rf["launches_per_call"], 4)
+        if traffic is not None:
+            rf["traffic_per_launch"] = traffic // rf["launches_per_call"]
         result["config"]["bwd_algo"] = g.last_bwd_algo
         result["fwd_ms"] = round(fms, 4)
         result["bwd_ms"] = round(bms, 4)
