@@ -1346,6 +1346,16 @@ __global__ __launch_bounds__(kBlock) void cbsr_pack_kernel(const float *__restri
     reinterpret_cast<uint32_t *>(rec)[i] = v;
 }
 
+// dXs zeroing for the ATOMIC backward / empty graphs.  A kernel rather than
+// hipMemsetAsync: captured into a hipGraph, the memset node was not reliably
+// ordered before the following atomics (wrong results in about half of the
+// replays; eager runs always right -- tools/exp_graph_flaky.py).
+__global__ __launch_bounds__(kBlock) void zero_kernel(float *__restrict__ p, size_t n)
+{
+    const size_t stride = (size_t)gridDim.x * blockDim.x;
+    for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) p[i] = 0.f;
+}
+
 // ---------------------------------------------------------------------------
 // Host-side dispatch
 // ---------------------------------------------------------------------------
@@ -1358,6 +1368,15 @@ inline int launch_status()
 }
 
 inline int64_t ceil_div(int64_t a, int64_t b) { return (a + b - 1) / b; }
+
+inline int zero_floats(float *p, size_t n, hipStream_t st)
+{
+    if (n == 0) return MAXK_OK;
+    const int64_t blocks = ceil_div((int64_t)n, kBlock);
+    hipLaunchKernelGGL(zero_kernel, dim3((unsigned)(blocks < 4096 ? blocks : 4096)), dim3(kBlock),
+                       0, st, p, n);
+    return launch_status();
+}
 
 inline size_t align_up(size_t x, size_t a) { return (x + a - 1) / a * a; }
 
@@ -1753,17 +1772,15 @@ int maxk_sspmm_backward(int algo, const int32_t *sched, int64_t num_panels,
     if (!dims_ok(dim_origin, dim_k)) return MAXK_E_DIM;
     hipStream_t st = as_stream(stream);
     if (num_cols == 0) return MAXK_OK;
-    if (num_rows == 0 || num_edges == 0) {  // no edge: dXs = 0
-        hipError_t e = hipMemsetAsync(dxs, 0, (size_t)num_cols * dim_k * sizeof(float), st);
-        return e == hipSuccess ? MAXK_OK : (int)e;
-    }
+    if (num_rows == 0 || num_edges == 0)  // no edge: dXs = 0
+        return zero_floats(dxs, (size_t)num_cols * dim_k, st);
     if (!indices || !values || !grad || !cbsr_sel) return MAXK_E_ARG;
     const bool staged_ready = csc_pos && csc_sched && csc_indptr && csc_num_panels >= 1 &&
                               workspace;
     if (algo == MAXK_BWD_AUTO) algo = staged_ready ? MAXK_BWD_STAGED : MAXK_BWD_ATOMIC;
     if (algo == MAXK_BWD_ATOMIC) {
-        hipError_t e = hipMemsetAsync(dxs, 0, (size_t)num_cols * dim_k * sizeof(float), st);
-        if (e != hipSuccess) return (int)e;
+        const int e = zero_floats(dxs, (size_t)num_cols * dim_k, st);
+        if (e) return e;
         return dispatch_k<BwdPanel>(dim_k, false, sched, num_panels, indptr, indices, values, grad,
                                     cbsr_sel, (const int32_t *)nullptr, num_rows, dim_origin, dim_k,
                                     dxs, (float *)nullptr, st);

@@ -78,6 +78,32 @@ def _build_schedule(indptr: torch.Tensor, num_rows: int, num_edges: int, panel_c
     return sched, P
 
 
+def _validate_csr(indptr: torch.Tensor, indices: torch.Tensor, num_cols: int) -> None:
+    """One-time device check that the kernels will stay in bounds: indptr
+    non-decreasing within [0, E], and the referenced columns in [0, num_cols).
+    (The reference kernels do not check; an out-of-range index there reads
+    out of bounds.)  One O(E) reduction and one host sync per graph."""
+    E = indices.numel()
+    if indptr.numel() == 0:
+        raise RuntimeError("indptr must have at least one element")
+    lo, hi = indptr[0], indptr[-1]
+    checks = [lo < 0, hi > E, (indptr[1:] < indptr[:-1]).any() if indptr.numel() > 1
+              else torch.zeros((), dtype=torch.bool, device=indptr.device)]
+    bad_cols = torch.zeros((), dtype=torch.bool, device=indptr.device)
+    if E > 0:
+        e0, e1 = int(lo.clamp(0, E)), int(hi.clamp(0, E))
+        if e1 > e0:
+            mn, mx = torch.aminmax(indices[e0:e1])
+            bad_cols = (mn < 0) | (mx >= num_cols)
+    flags = torch.stack([c.reshape(()).bool() for c in checks] + [bad_cols]).tolist()
+    if flags[0] or flags[1]:
+        raise RuntimeError(f"indptr out of range: must satisfy 0 <= indptr[0] <= indptr[-1] <= {E}")
+    if flags[2]:
+        raise RuntimeError("indptr must be non-decreasing")
+    if flags[3]:
+        raise RuntimeError(f"indices out of range: every column must be in [0, {num_cols})")
+
+
 class MaxKGraph:
     """A CSR graph on one GPU, ready for the MaxK SpGEMM / SSpMM kernels.
 
@@ -89,7 +115,8 @@ class MaxKGraph:
     def __init__(self, indptr: torch.Tensor, indices: torch.Tensor,
                  values: torch.Tensor | None = None, *, panel_cost: int = _lib.DEFAULT_PANEL_COST,
                  row_cost: int = _lib.DEFAULT_ROW_COST, bwd_panel_cost: int | None = None,
-                 csc_panel_cost: int | None = None, num_cols: int | None = None):
+                 csc_panel_cost: int | None = None, num_cols: int | None = None,
+                 validate: bool = True):
         check_tensor(indptr, "indptr", torch.int32, dim=1)
         check_tensor(indices, "indices", torch.int32, dim=1)
         if values is None:
@@ -103,6 +130,8 @@ class MaxKGraph:
         # A may be rectangular (a multi-GPU rank's row block with halo columns)
         self.num_cols = self.num_rows if num_cols is None else int(num_cols)
         self.num_edges = indices.numel()
+        if validate:
+            _validate_csr(indptr, indices, self.num_cols)
         if self.num_edges == 0:  # the C ABI wants valid pointers even for an empty edge list
             indices = torch.zeros(1, dtype=torch.int32, device=indices.device)
             values = torch.zeros(1, dtype=torch.float32, device=indices.device)

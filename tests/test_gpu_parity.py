@@ -233,7 +233,8 @@ def test_offset_csr_view(dev, oracle, g_small):
     lo, hi = 500, 1700
     sub_ptr = indptr[lo:hi + 1]
     data, sel = random_cbsr(len(indptr) - 1, 16, 256, seed=8)
-    g = S.MaxKGraph(T(sub_ptr, dev), T(indices, dev), T(values, dev), panel_cost=200)
+    g = S.MaxKGraph(T(sub_ptr, dev), T(indices, dev), T(values, dev), panel_cost=200,
+                    num_cols=len(indptr) - 1)
     # rows of the view gather columns of the full graph: CBSR must cover all V nodes,
     # so compare the view's rows against the full-graph result.
     full = oracle.np_forward(indptr, indices, values, data, sel, 256)[lo:hi]
@@ -638,3 +639,19 @@ def test_hipgraph_full_step(dev, oracle, g_small, monkeypatch, k, algo):
     dense = np.zeros((v, h))
     np.put_along_axis(dense, sel.astype(np.int64), ref, axis=1)
     assert oracle.parity_error(gx.cpu().numpy(), dense) <= TOL
+
+
+def test_graph_validation(dev):
+    """Malformed CSR is rejected before any kernel runs (the kernels would read
+    out of bounds)."""
+    ip = T(np.array([0, 2, 3], np.int32), dev)
+    with pytest.raises(RuntimeError, match="indices out of range"):
+        S.MaxKGraph(ip, T(np.array([0, 5, 1], np.int32), dev))
+    with pytest.raises(RuntimeError, match="indices out of range"):
+        S.MaxKGraph(ip, T(np.array([0, -1, 1], np.int32), dev))
+    with pytest.raises(RuntimeError, match="non-decreasing"):
+        S.MaxKGraph(T(np.array([0, 3, 2, 3], np.int32), dev), T(np.array([0, 1, 2], np.int32), dev))
+    with pytest.raises(RuntimeError, match="indptr out of range"):
+        S.MaxKGraph(T(np.array([0, 2, 4], np.int32), dev), T(np.array([0, 1, 1], np.int32), dev))
+    g = S.MaxKGraph(ip, T(np.array([0, 1, 2], np.int32), dev), num_cols=3)
+    assert g.num_cols == 3
