@@ -623,6 +623,18 @@ def test_hipgraph_full_step(dev, oracle, g_small, monkeypatch, k, algo):
             step()
     torch.cuda.current_stream().wait_stream(stream)
     gen = np.random.default_rng(k)
+    # several replays on fresh inputs, each checked against the eager step (a
+    # captured memset node once made about half of the ATOMIC replays wrong)
+    for _ in range(6):
+        x.copy_(torch.rand((v, h), device=dev))
+        gr.copy_(torch.rand((v, h), device=dev))
+        graph.replay()
+        torch.cuda.synchronize()
+        got = [t.clone() for t in (d, s, y, dx, gx)]
+        step()
+        torch.cuda.synchronize()
+        for a, b in zip(got, (d, s, y, dx, gx)):
+            assert torch.allclose(a.float(), b.float(), rtol=1e-4, atol=1e-4)
     xn = gen.random((v, h), dtype=np.float32)
     gn = gen.random((v, h), dtype=np.float32)
     x.copy_(T(xn, dev))
