@@ -49,7 +49,7 @@ def test_full_size_properties(dev, graph, k):
     del a, ref
     # backward: adjoint identity, algorithms agree
     algos = [_lib.MAXK_BWD_STAGED, _lib.MAXK_BWD_ATOMIC]
-    if g.local_plan(k) is not None and graph == "reddit":
+    if g.local_plan(k) is not None:   # slow on products (78 source bands) but must be right
         algos.append(_lib.MAXK_BWD_LOCAL)
     outs = {a_: g.backward(Gr, sel, algo=a_) for a_ in algos}
     lhs = float((y.double() * Gr.double()).sum())
