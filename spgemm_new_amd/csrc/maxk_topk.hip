@@ -211,17 +211,41 @@ __global__ __launch_bounds__(kBlock) void topk_kernel(const float *__restrict__ 
                 }
             }
             wave_sync_lds();
-            // rank = #selected entries ordered before this one (key desc, column asc)
-            mine = 0;
+            if (k > 16 && k <= kWave) {  // (k <= 16: the rank loop below measured faster)
+                // bitonic sort of the k composites (key desc, column asc) across
+                // the first n lanes (padding = 0 sorts last); lane i then holds rank i
+                uint64_t a = lane < k ? st[lane] : 0ull;
+                int n = 1;  // network size: the next power of two >= k (lanes < n)
+                while (n < k) n <<= 1;
+                for (int size = 2; size <= n; size <<= 1) {
+                    for (int stride = size >> 1; stride > 0; stride >>= 1) {
+                        const uint64_t b = __shfl_xor(a, stride);
+                        // block direction: descending where bit `size` is clear (every
+                        // lane below n in the final merge, size = n)
+                        const bool desc = (lane & size) == 0;
+                        const bool lower = (lane & stride) == 0;
+                        a = (desc == lower) ? (a > b ? a : b) : (a < b ? a : b);
+                    }
+                }
+                if (lane < k) {
+                    const int col = (int)(~(uint32_t)a);
+                    drow[lane] = x[r * ld + col];  // the original value (keeps -0.0)
+                    srow[lane] = (uint8_t)col;
+                }
+            } else {
+                // k <= 16 or k > 64: rank = #selected entries ordered before this one
+                // (key desc, column asc)
+                mine = 0;
 #pragma unroll
-            for (int j = 0; j < 4; ++j) {
-                if (take[j]) {
-                    const uint64_t me = st[pos + mine];
-                    int rank = 0;
-                    for (int t = 0; t < k; ++t) rank += st[t] > me;
-                    drow[rank] = v[j];
-                    srow[rank] = (uint8_t)(4 * lane + j);
-                    ++mine;
+                for (int j = 0; j < 4; ++j) {
+                    if (take[j]) {
+                        const uint64_t me = st[pos + mine];
+                        int rank = 0;
+                        for (int t = 0; t < k; ++t) rank += st[t] > me;
+                        drow[rank] = v[j];
+                        srow[rank] = (uint8_t)(4 * lane + j);
+                        ++mine;
+                    }
                 }
             }
             wave_sync_lds();
