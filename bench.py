@@ -242,15 +242,22 @@ def main():
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
     if world != args.gpus and world > 1:
         log(f"warning: WORLD_SIZE={world} but --gpus {args.gpus}")
-    torch.cuda.set_device(local_rank)
-    dev = torch.device("cuda", local_rank)
+    # one GPU per rank; ranks beyond the visible GPUs share them (only for the
+    # BENCH_BACKEND=gloo rehearsal of the N>1 path on a one-GPU box)
+    dev_index = local_rank % max(1, torch.cuda.device_count())
+    torch.cuda.set_device(dev_index)
+    dev = torch.device("cuda", dev_index)
     dist = None
     partitioned = world > 1 or args.partitioned
     if partitioned:
         import torch.distributed as dist
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
         os.environ.setdefault("MASTER_PORT", "29511")
-        dist.init_process_group("nccl", device_id=dev, rank=rank, world_size=world)
+        backend = os.environ.get("BENCH_BACKEND", "nccl")   # nccl = RCCL over xGMI
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=dev, rank=rank, world_size=world)
+        else:  # rehearsal only: exchanges staged through host memory
+            dist.init_process_group(backend, rank=rank, world_size=world)
 
     V, E = CONFIGS[args.graph]
     h, k = args.h, args.k

@@ -35,3 +35,21 @@ def test_bench_json_line(extra):
         cb = d["cpu_baseline"]
         assert cb["kind"] == "reference" and cb["value"] > 0 and cb["cores"] >= 1
         assert "sample" in cb
+
+
+@pytest.mark.gpu
+def test_bench_two_ranks_rehearsal():
+    """The N>1 bench path (torch.distributed.run, row partition, halo exchange,
+    max-over-ranks timing) end to end with 2 ranks on one GPU; gloo stands in
+    for RCCL (BENCH_BACKEND=gloo), so only the logic is exercised here."""
+    env = dict(os.environ, BENCH_BACKEND="gloo")
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
+           "--master-addr", "127.0.0.1", "--master-port", "29613", os.path.join(ROOT, "bench.py"),
+           "--gpus", "2", "--steps", "2", "--warmup", "1", "--graph", "flickr", "--h", "64",
+           "--k", "16"]
+    out = subprocess.run(cmd, cwd=ROOT, capture_output=True, text=True, timeout=600, env=env)
+    assert out.returncode == 0, out.stderr[-3000:]
+    d = json.loads(out.stdout.strip().splitlines()[-1])
+    assert d["n_gpus"] == 2 and d["config"]["parallelism"] == "rowpart2"
+    assert d["value"] > 0 and d["roofline"]["achieved"] > 0
+    assert d["config"]["halo_nodes_rank0"] > 0 and d["config"]["overlap"] is True
