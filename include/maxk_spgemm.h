@@ -101,6 +101,19 @@ int maxk_spgemm_forward_packed(const int32_t *sched, int64_t num_panels, const i
                                void *workspace, size_t workspace_bytes, void *stream);
 
 /* ---------------------------------------------------------------------------
+ * Dense SpMM baseline: out = A . x with x fp32[num_cols, dim] dense, 4 <= dim
+ * <= 256, dim % 4 == 0 (the comparison kernels of the reference's speedup
+ * table: GNNAdvisor SAG kernels/spmm_gnna.cu:60-140 -- unweighted, pass
+ * values = 1 -- and cusparse_spmm, cuda_kernel_bindings.cpp:253-284).  Same
+ * schedule as maxk_spgemm_forward, workspace maxk_forward_workspace_bytes(P,
+ * dim); out need not be zeroed.
+ * ------------------------------------------------------------------------- */
+int maxk_spmm_dense_forward(const int32_t *sched, int64_t num_panels, const int32_t *indptr,
+                            const int32_t *indices, const float *values, const float *x,
+                            int num_rows, int dim, float *out, void *workspace,
+                            size_t workspace_bytes, void *stream);
+
+/* ---------------------------------------------------------------------------
  * Fused multi-relation forward (ogbn-proteins, BASELINE config 5; no
  * reference function -- the reference sums proteins' 8 edge features into
  * node features, utils/proteins_loader.py:41-44).  Y[q] = A_q . scatter(CBSR)

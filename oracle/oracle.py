@@ -198,6 +198,18 @@ def np_backward(indptr, indices, values, grad, sel) -> np.ndarray:
     return np.take_along_axis(agt, sel.astype(np.int64), axis=1)
 
 
+def np_spmm_dense(indptr, indices, values, x) -> np.ndarray:
+    """Dense SpMM Y = A . X in float64: cuSPARSE SpMM (kernels/spmm_cusparse.cu:6-62)
+    and, with values = 1, GNNAdvisor's SAG aggregation (kernels/spmm_gnna.cu:60-140)."""
+    indptr = np.asarray(indptr, dtype=np.int64)
+    v = len(indptr) - 1
+    rows = np.repeat(np.arange(v), np.diff(indptr))
+    out = np.zeros((v, x.shape[1]), dtype=np.float64)
+    np.add.at(out, rows, np.asarray(values, np.float64)[:, None] *
+              np.asarray(x, np.float64)[np.asarray(indices)])
+    return out
+
+
 def np_cbsr(x: np.ndarray, k: int):
     """Top-k CBSR producer (torch.topk semantics: descending values)."""
     idx = np.argsort(-x, axis=1, kind="stable")[:, :k]

@@ -424,6 +424,103 @@ __global__ __launch_bounds__(kBlock) void carry_fixup_kernel(
 }
 
 // ---------------------------------------------------------------------------
+// Dense SpMM baseline Y = A . X, X fp32[V, dim] dense (the
+// kernels the reference compares MaxK against, GNNAdvisor's SAG
+// spmm_gnna.cu:60-140 and cuSPARSE spmm_cusparse.cu:6-62).  Same merge-path
+// panels as the MaxK forward.  A gathered X row is contiguous, so there is no
+// scatter: LPE lanes own 4 consecutive columns each and accumulate in
+// registers; EPS = 64 / LPE edges per step, their partial sums reduced with
+// cross-lane shuffles at each row flush.  No LDS.
+// ---------------------------------------------------------------------------
+template <int LPE>
+__device__ __forceinline__ void dense_edges(int e0, int e1, int dim, const int32_t *__restrict__ idx,
+                                            const float *__restrict__ val,
+                                            const float *__restrict__ x, f4 &acc)
+{
+    constexpr int EPS = kWave / LPE;
+    constexpr int STEPS = LPE;  // steps per 64-edge batch
+    constexpr int U = STEPS < 8 ? STEPS : 8;
+    const int lane = lane_id();
+    const int sub = lane % LPE, slot = lane / LPE;
+    const bool col_ok = sub * 4 < dim;
+    for (int base = e0; base < e1; base += kWave) {
+        const int n = (e1 - base) < kWave ? (e1 - base) : kWave;
+        int my_c = 0;
+        float my_v = 0.f;
+        if (lane < n) {
+            my_c = __builtin_nontemporal_load(idx + base + lane);
+            my_v = __builtin_nontemporal_load(val + base + lane);
+        }
+#pragma unroll
+        for (int s0 = 0; s0 < STEPS; s0 += U) {
+            if (s0 * EPS >= n) break;
+            f4 d[U];
+            float v[U];
+#pragma unroll
+            for (int u = 0; u < U; ++u) {
+                const int t = (s0 + u) * EPS + slot;
+                const int c = __shfl(my_c, t);
+                v[u] = __shfl(my_v, t);
+                d[u] = f4{0.f, 0.f, 0.f, 0.f};
+                if (t < n && col_ok) d[u] = *reinterpret_cast<const f4 *>(x + (size_t)c * dim + sub * 4);
+            }
+#pragma unroll
+            for (int u = 0; u < U; ++u) acc += v[u] * d[u];
+        }
+    }
+}
+
+template <int LPE>
+__device__ __forceinline__ void dense_flush(f4 &acc, float *__restrict__ dst, int dim)
+{
+#pragma unroll
+    for (int m = LPE; m < kWave; m <<= 1) {
+        acc.x += __shfl_xor(acc.x, m);
+        acc.y += __shfl_xor(acc.y, m);
+        acc.z += __shfl_xor(acc.z, m);
+        acc.w += __shfl_xor(acc.w, m);
+    }
+    const int lane = lane_id();
+    if (lane < LPE && lane * 4 < dim) reinterpret_cast<f4 *>(dst)[lane] = acc;
+    acc = f4{0.f, 0.f, 0.f, 0.f};
+}
+
+template <int LPE>
+__global__ __launch_bounds__(kBlock) void dense_panel_kernel(
+    const int2 *__restrict__ sched, int64_t num_panels, const int32_t *__restrict__ indptr,
+    const int32_t *__restrict__ idx, const float *__restrict__ val, const float *__restrict__ x,
+    int num_rows, int dim, float *__restrict__ out, float *__restrict__ carry,
+    int32_t *__restrict__ carry_row)
+{
+    const int64_t w = (int64_t)blockIdx.x * kWavesPerBlock + threadIdx.x / kWave;
+    if (w >= num_panels) return;
+    const int2 a = sched[w], b = sched[w + 1];
+    const int i0 = a.x, j0 = a.y, i1 = b.x, j1 = b.y;
+    f4 acc = f4{0.f, 0.f, 0.f, 0.f};
+    int e = j0;
+    for (int r = i0; r < i1; ++r) {
+        const int re = indptr[r + 1];
+        if (e < re) dense_edges<LPE>(e, re, dim, idx, val, x, acc);
+        dense_flush<LPE>(acc, out + (size_t)r * dim, dim);
+        e = re;
+    }
+    int has_carry = 0;
+    if (i1 < num_rows) {
+        const int eb = e > indptr[i1] ? e : indptr[i1];
+        if (eb < j1) {
+            dense_edges<LPE>(eb, j1, dim, idx, val, x, acc);
+            has_carry = 1;
+        }
+    }
+    if (has_carry) {
+        dense_flush<LPE>(acc, carry + (size_t)w * dim, dim);
+        if (lane_id() == 0) carry_row[w] = i1;
+    } else if (lane_id() == 0) {
+        carry_row[w] = -1;
+    }
+}
+
+// ---------------------------------------------------------------------------
 // Fused multi-relation forward (ogbn-proteins, config 5):
 // Y_q = A_q . X^ for q < R relations sharing one CSR and one CBSR, edge values
 // val[e * R + q].  Parity: R independent calls of the single-relation forward.
@@ -1672,6 +1769,36 @@ int maxk_spgemm_forward(const int32_t *sched, int64_t num_panels, const int32_t 
     return dispatch_k<FwdPanel>(dim_k, sched, num_panels, indptr, indices, values, cbsr_data,
                                 cbsr_sel, num_rows, dim_origin, dim_k, out, carry, carry_row,
                                 as_stream(stream));
+}
+
+int maxk_spmm_dense_forward(const int32_t *sched, int64_t num_panels, const int32_t *indptr,
+                            const int32_t *indices, const float *values, const float *x,
+                            int num_rows, int dim, float *out, void *workspace,
+                            size_t workspace_bytes, void *stream)
+{
+    if (!sched || !indptr || !out || num_panels < 1 || num_rows < 0) return MAXK_E_ARG;
+    if (dim < 4 || dim > kMaxDim || (dim & 3)) return MAXK_E_DIM;
+    if (num_rows == 0) return MAXK_OK;
+    if (!indices || !values || !x) return MAXK_E_ARG;
+    if (!workspace || workspace_bytes < maxk_forward_workspace_bytes(num_panels, dim))
+        return MAXK_E_WORKSPACE;
+    float *carry = static_cast<float *>(workspace);
+    int32_t *carry_row = reinterpret_cast<int32_t *>(
+        static_cast<char *>(workspace) + align_up((size_t)num_panels * dim * sizeof(float), 256));
+    hipStream_t st = as_stream(stream);
+    const int64_t blocks = ceil_div(num_panels, kWavesPerBlock);
+    const int2 *sc = reinterpret_cast<const int2 *>(sched);
+    const int q = dim / 4;  // lanes per edge: the smallest power of two >= dim / 4
+    auto k = q > 32 ? dense_panel_kernel<64> : q > 16 ? dense_panel_kernel<32>
+           : q > 8 ? dense_panel_kernel<16> : q > 4 ? dense_panel_kernel<8>
+           : q > 2 ? dense_panel_kernel<4> : q > 1 ? dense_panel_kernel<2> : dense_panel_kernel<1>;
+    hipLaunchKernelGGL(k, dim3((unsigned)blocks), dim3(kBlock), 0, st, sc, num_panels, indptr,
+                       indices, values, x, num_rows, dim, out, carry, carry_row);
+    int rc = launch_status();
+    if (rc) return rc;
+    hipLaunchKernelGGL(carry_fixup_kernel, dim3((unsigned)blocks), dim3(kBlock), 0, st, num_panels,
+                       carry, carry_row, out, dim, dim, 1, (size_t)0);
+    return launch_status();
 }
 
 size_t maxk_cbsr_packed_row_bytes(int dim_k)

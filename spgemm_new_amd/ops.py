@@ -27,7 +27,7 @@ import torch
 from . import _lib
 
 __all__ = ["MaxKGraph", "check_tensor", "spgemm_forward", "spgemm_forward_multi",
-           "sspmm_backward", "warp4_build",
+           "sspmm_backward", "spmm_dense", "warp4_build",
            "topk_cbsr", "cbsr_scatter", "cbsr_mask"]
 
 
@@ -363,10 +363,34 @@ class MaxKGraph:
             self._cols_cache = (key, cols, values)  # holds values: its address stays unique
         return self._cols_cache[1]
 
+    def spmm_dense(self, x: torch.Tensor, out: torch.Tensor | None = None,
+                   values: torch.Tensor | None = None) -> torch.Tensor:
+        """Dense SpMM baseline Y = A . x (x fp32[num_cols, h], h % 4 == 0, h <= 256):
+        the comparison the reference's speedup table makes (GNNAdvisor SAG,
+        kernels/spmm_gnna.cu:60-140; cuSPARSE, cuda_kernel_bindings.cpp:253-284)."""
+        return spmm_dense(self, x, out, values)
+
     def backward(self, grad: torch.Tensor, cbsr_sel: torch.Tensor, out: torch.Tensor | None = None,
                  values: torch.Tensor | None = None, algo: int = _lib.MAXK_BWD_AUTO) -> torch.Tensor:
         """dXs = (A^T G) sampled at sel  (spmm_maxk_backward.cu:15-115).  Returns fp32[V, k]."""
         return sspmm_backward(self, grad, cbsr_sel, out, values, algo)
+
+
+def _on_device(g: MaxKGraph, **tensors):
+    for name, t in tensors.items():
+        if t is not None and t.device != g.device:
+            raise RuntimeError(f"{name} must be on the graph's device ({g.device}), got {t.device}")
+
+
+def _check_values(g: MaxKGraph, values):
+    """Edge values other than the graph's own: fp32[E] on the graph's device."""
+    if values is None:
+        return g.values
+    check_tensor(values, "values", torch.float32, dim=1)
+    if values.numel() != g.num_edges:
+        raise RuntimeError(f"values must have num_edges = {g.num_edges} elements, got {values.numel()}")
+    _on_device(g, values=values)
+    return values if g.num_edges > 0 else g.values
 
 
 def _check_cbsr(g: MaxKGraph, data, sel):
@@ -383,15 +407,14 @@ def _check_cbsr(g: MaxKGraph, data, sel):
 def spgemm_forward(g: MaxKGraph, data, sel, dim_origin: int = 256, out=None, values=None):
     _check_cbsr(g, data, sel)
     k = data.shape[1]
-    if values is None:
-        values = g.values
-    check_tensor(values, "values", torch.float32, dim=1)
+    values = _check_values(g, values)
     if out is None:
         out = torch.empty((g.num_rows, dim_origin), dtype=torch.float32, device=g.device)
     else:
         check_tensor(out, "output", torch.float32, dim=2)
         if tuple(out.shape) != (g.num_rows, dim_origin):
             raise RuntimeError("output has the wrong shape")
+        _on_device(g, output=out)
     L = _lib.load()
     nbytes = L.maxk_forward_workspace_bytes(g.num_panels, dim_origin)
     ws = g._workspace(("fwd", dim_origin), nbytes)
@@ -418,6 +441,7 @@ def spgemm_forward_multi(g: MaxKGraph, data, sel, values, dim_origin: int = 256,
     check_tensor(values, "values", torch.float32, dim=2)
     if values.shape[0] != g.num_edges:
         raise RuntimeError("values must be [num_edges, num_relations]")
+    _on_device(g, values=values)
     R = values.shape[1]
     if not 1 <= R <= 16:
         raise RuntimeError("1 <= num_relations <= 16")
@@ -429,6 +453,7 @@ def spgemm_forward_multi(g: MaxKGraph, data, sel, values, dim_origin: int = 256,
         check_tensor(out, "output", torch.float32, dim=3)
         if tuple(out.shape) != (R, g.num_rows, dim_origin):
             raise RuntimeError("output must be [R, V, dim_origin]")
+        _on_device(g, output=out)
     vals = values if g.num_edges > 0 else torch.zeros((1, R), device=g.device)
     L = _lib.load()
     nbytes = L.maxk_forward_multi_workspace_bytes(g.num_panels, dim_origin, R)
@@ -447,14 +472,15 @@ def sspmm_backward(g: MaxKGraph, grad, sel, out=None, values=None, algo: int = _
         raise RuntimeError("grad_output rows must equal the graph's rows and sparse_selector "
                            "rows its columns")
     dim_origin, k = grad.shape[1], sel.shape[1]
-    if values is None:
-        values = g.values
+    _on_device(g, grad_output=grad, sparse_selector=sel)
+    values = _check_values(g, values)
     if out is None:
         out = torch.empty((g.num_cols, k), dtype=torch.float32, device=g.device)
     else:
         check_tensor(out, "grad_input", torch.float32, dim=2)
         if tuple(out.shape) != (g.num_cols, k):
             raise RuntimeError("grad_input has the wrong shape")
+        _on_device(g, grad_input=out)
     if algo == _lib.MAXK_BWD_AUTO:
         algo = g.autotune_backward(grad, sel, out, values)
     if g.num_edges == 0:
@@ -487,6 +513,31 @@ def sspmm_backward(g: MaxKGraph, grad, sel, out=None, values=None, algo: int = _
         dim_origin, k,
         out.data_ptr(), _lib.ptr(csc_pos), _lib.ptr(csc_sched), CP, _lib.ptr(csc_indptr),
         _lib.ptr(ws), 0 if ws is None else ws.numel(), _stream(out)), "maxk_sspmm_backward")
+    return out
+
+
+def spmm_dense(g: MaxKGraph, x, out=None, values=None):
+    check_tensor(x, "input_features", torch.float32, dim=2)
+    _on_device(g, input_features=x)
+    if x.shape[0] != g.num_cols:
+        raise RuntimeError(f"input_features has {x.shape[0]} rows, graph has {g.num_cols} columns")
+    dim = x.shape[1]
+    if dim % 4 or not 4 <= dim <= 256:
+        raise RuntimeError("dense SpMM needs 4 <= dim <= 256 and dim % 4 == 0")
+    values = _check_values(g, values)
+    if out is None:
+        out = torch.empty((g.num_rows, dim), dtype=torch.float32, device=g.device)
+    else:
+        check_tensor(out, "output", torch.float32, dim=2)
+        if tuple(out.shape) != (g.num_rows, dim):
+            raise RuntimeError("output has the wrong shape")
+        _on_device(g, output=out)
+    L = _lib.load()
+    ws = g._workspace(("fwd", dim), L.maxk_forward_workspace_bytes(g.num_panels, dim))
+    _lib.check(L.maxk_spmm_dense_forward(g.sched.data_ptr(), g.num_panels, g.indptr.data_ptr(),
+                                         g.indices.data_ptr(), values.data_ptr(), x.data_ptr(),
+                                         g.num_rows, dim, out.data_ptr(), ws.data_ptr(), ws.numel(),
+                                         _stream(out)), "maxk_spmm_dense_forward")
     return out
 
 

@@ -667,3 +667,47 @@ def test_graph_validation(dev):
         S.MaxKGraph(T(np.array([0, 2, 4], np.int32), dev), T(np.array([0, 1, 1], np.int32), dev))
     g = S.MaxKGraph(ip, T(np.array([0, 1, 2], np.int32), dev), num_cols=3)
     assert g.num_cols == 3
+
+
+def test_call_validation(dev):
+    """Per-call operands are checked against the graph: edge values of the
+    wrong length or dtype and tensors on another device raise before launch."""
+    indptr, indices = small_csr(40, seed=5)
+    g = S.MaxKGraph(T(indptr, dev), T(indices, dev))
+    data, sel = random_cbsr(40, 8, 64, seed=2)
+    d, s = T(data, dev), T(sel, dev)
+    grad = torch.rand((40, 64), device=dev)
+    short = torch.rand(len(indices) - 1, device=dev)
+    with pytest.raises(RuntimeError, match="num_edges"):
+        g.forward(d, s, 64, values=short)
+    for algo in (_lib.MAXK_BWD_STAGED, _lib.MAXK_BWD_ATOMIC, _lib.MAXK_BWD_LOCAL):
+        with pytest.raises(RuntimeError, match="num_edges"):
+            g.backward(grad, s, values=short, algo=algo)
+    with pytest.raises(RuntimeError, match="float32"):
+        g.backward(grad, s, values=torch.ones(len(indices), dtype=torch.float64, device=dev))
+    with pytest.raises(RuntimeError, match="CUDA tensor"):
+        g.backward(grad.cpu(), s)
+    with pytest.raises(RuntimeError, match="CUDA tensor"):
+        g.forward(d, s, 64, values=short.cpu())
+    # the right operands still run after the rejected calls
+    y = g.forward(d, s, 64)
+    assert torch.isfinite(y).all()
+
+
+@pytest.mark.parametrize("h", [4, 8, 12, 64, 100, 252, 256])
+def test_spmm_dense_baseline(dev, oracle, h):
+    """Dense SpMM baseline (GNNAdvisor SAG / cuSPARSE stand-in) against the
+    fp64 oracle, over the degree mix and panel splits of small_csr."""
+    indptr, indices = small_csr(2500, seed=9)
+    rng = np.random.default_rng(h)
+    values = rng.random(len(indices), dtype=np.float32)
+    x = rng.random((len(indptr) - 1, h), dtype=np.float32)
+    g = S.MaxKGraph(T(indptr, dev), T(indices, dev), T(values, dev), panel_cost=300)
+    out = torch.full((len(indptr) - 1, h), float("nan"), device=dev)
+    y = g.spmm_dense(T(x, dev), out=out)
+    assert oracle.parity_error(y.cpu().numpy(), oracle.np_spmm_dense(indptr, indices, values, x)) <= TOL
+    ones = g.spmm_dense(T(x, dev), values=torch.ones(len(indices), device=dev))
+    assert oracle.parity_error(ones.cpu().numpy(),
+                               oracle.np_spmm_dense(indptr, indices, np.ones(len(indices)), x)) <= TOL
+    with pytest.raises(RuntimeError, match="dim % 4"):
+        g.spmm_dense(T(x[:, :3].copy(), dev))
