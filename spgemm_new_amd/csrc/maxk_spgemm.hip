@@ -264,8 +264,13 @@ __device__ __forceinline__ void fwd_edges_vec(int e0, int e1, const int32_t *__r
                         sb[u] = *reinterpret_cast<const SB *>(sel + off);
                     } else {  // data = record base, sel = record base + 4K bytes
                         const size_t rec = (size_t)c * RS;
+#if FWD_PACKED_NT
+                        d[u] = __builtin_nontemporal_load(reinterpret_cast<const D *>(reinterpret_cast<const uint8_t *>(data) + rec + 4 * sub * VEC));
+                        sb[u] = __builtin_nontemporal_load(reinterpret_cast<const SB *>(sel + rec + sub * VEC));
+#else
                         d[u] = *reinterpret_cast<const D *>(reinterpret_cast<const uint8_t *>(data) + rec + 4 * sub * VEC);
                         sb[u] = *reinterpret_cast<const SB *>(sel + rec + sub * VEC);
+#endif
                     }
                 }
             }
@@ -326,6 +331,13 @@ __device__ __forceinline__ void fwd_edges(int e0, int e1, int k, const int32_t *
 // Row flushes: sum the `copies` LDS row copies, zero them, and store / add.
 enum FlushOp { kStore = 0, kAtomic = 1, kAdd = 2 };
 
+#ifndef FWD_NT_OUT
+#define FWD_NT_OUT 1  // nt row stores: -1 % fwd on Reddit and products (tools/nt_sweep.sh)
+#endif
+#ifndef FWD_PACKED_NT
+#define FWD_PACKED_NT 0
+#endif
+
 template <int OP>
 __device__ __forceinline__ void flush_row(float *acc, int copies, float *__restrict__ dst, int dim)
 {
@@ -340,7 +352,11 @@ __device__ __forceinline__ void flush_row(float *acc, int copies, float *__restr
                 a += *q;
                 *q = f4{0.f, 0.f, 0.f, 0.f};
             }
+#if FWD_NT_OUT
+            __builtin_nontemporal_store(a, reinterpret_cast<f4 *>(dst) + c4);
+#else
             reinterpret_cast<f4 *>(dst)[c4] = a;
+#endif
         }
     } else {
         for (int c = lane; c < dim; c += kWave) {  // 256 contiguous bytes per instruction
@@ -907,6 +923,10 @@ __device__ __forceinline__ void stage_row(float *gs, const float *__restrict__ g
     wave_sync_lds();
 }
 
+#ifndef BWD_ATOMIC_U
+#define BWD_ATOMIC_U 8  // selector loads in flight (4 / 8 / 16 measured equal)
+#endif
+
 // ATOMIC push over one edge range of row r (G[r] already staged in gs).
 __device__ __forceinline__ void bwd_edges_atomic(int e0, int e1, int k,
                                                  const int32_t *__restrict__ idx,
@@ -948,7 +968,54 @@ __device__ __forceinline__ void bwd_edges_atomic(int e0, int e1, int k,
     }
 }
 
-// STAGED push: P[csc_pos[e], 0:K] = val[e] * G[r, sel[c, 0:K]].
+// ATOMIC push with the coalesced lane mapping of bwd_edges_atomic (lane l ->
+// column l of an edge, so one atomic instruction covers contiguous floats) and
+// U selector loads in flight (products k=16: 7.38 -> 6.08 ms, k=32: 13.2 ->
+// 12.6; at k >= 16 the chip's float-atomic rate, ~320 G/s, is the bound).
+template <int K>
+__device__ __forceinline__ void bwd_edges_atomic_u(int e0, int e1, const int32_t *__restrict__ idx,
+                                                   const float *__restrict__ val,
+                                                   const uint8_t *__restrict__ sel,
+                                                   const float *gs, float *__restrict__ dxs)
+{
+    constexpr int EPS = kWave / K;
+    constexpr int STEPS = kWave / EPS;
+    constexpr int U = STEPS < BWD_ATOMIC_U ? STEPS : BWD_ATOMIC_U;
+    const int lane = lane_id();
+    const int slot = lane / K, l = lane % K;
+    for (int base = e0; base < e1; base += kWave) {
+        const int n = (e1 - base) < kWave ? (e1 - base) : kWave;
+        int my_c = 0;
+        float my_v = 0.f;
+        if (lane < n) {
+            my_c = __builtin_nontemporal_load(idx + base + lane);
+            my_v = __builtin_nontemporal_load(val + base + lane);
+        }
+#pragma unroll
+        for (int s0 = 0; s0 < STEPS; s0 += U) {
+            if (s0 * EPS >= n) break;
+            uint32_t sb[U];
+            int cs[U];
+#pragma unroll
+            for (int u = 0; u < U; ++u) {
+                const int t = (s0 + u) * EPS + slot;
+                cs[u] = __shfl(my_c, t);
+                sb[u] = t < n ? sel[(size_t)cs[u] * K + l] : 0u;
+            }
+#pragma unroll
+            for (int u = 0; u < U; ++u) {
+                const int t = (s0 + u) * EPS + slot;
+                const float v = __shfl(my_v, t);
+                if (t < n) gbl_add(dxs + (size_t)cs[u] * K + l, v * gs[sb[u]]);
+            }
+        }
+    }
+}
+
+// STAGED push: P[csc_pos[e], 0:K] = val[e] * G[r, sel[c, 0:K]], K/4 lanes per
+// edge, 4 selected columns per lane, U selector loads in flight.
+// (The same lane mapping with 4 float atomics per lane for ATOMIC measured 4x
+// slower: lane-strided atomics do not coalesce.)
 template <int K>
 __device__ __forceinline__ void bwd_edges_stage_vec(int e0, int e1,
                                                     const int32_t *__restrict__ idx,
@@ -1048,7 +1115,10 @@ __global__ __launch_bounds__(kBlock) void bwd_panel_kernel(
             else
                 bwd_edges_stage_scalar(eb, ee, k, idx, val, csc_pos, sel, gs, P);
         } else {
-            bwd_edges_atomic(eb, ee, k, idx, val, sel, gs, dxs);
+            if constexpr (K >= 1 && K <= kWave)
+                bwd_edges_atomic_u<K>(eb, ee, idx, val, sel, gs, dxs);
+            else
+                bwd_edges_atomic(eb, ee, k, idx, val, sel, gs, dxs);
         }
     }
 }
