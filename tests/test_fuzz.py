@@ -1,0 +1,105 @@
+"""Randomised parity sweep (GPU): many small random problems, every kernel
+against the fp64 oracle.
+
+Each seed draws a graph (square or rectangular -- a multi-GPU rank's row block
+with halo columns --, zero-heavy / uniform / hub degree mixes), a panel
+schedule granularity, k and h, signed edge values, and checks the forward
+SpGEMM, all three backward SSpMM algorithms, the top-k CBSR producer, the
+dense SpMM baseline and (power-of-two k) the multi-relation forward and
+backward.  Sizes are small so the oracle finishes in milliseconds; the seeds
+are fixed so a failure is reproducible by its test id.
+"""
+import numpy as np
+import pytest
+import torch
+
+import spgemm_new_amd as S
+from spgemm_new_amd import _lib
+
+pytestmark = pytest.mark.gpu
+TOL = 1e-4
+KS = [1, 2, 3, 4, 5, 8, 12, 16, 24, 32, 48, 64, 100, 128, 256]
+
+
+def T(a, dev):
+    return torch.from_numpy(np.ascontiguousarray(a)).to(dev)
+
+
+def draw(seed):
+    rng = np.random.default_rng(1000 + seed)
+    V = int(rng.integers(1, 400))
+    C = V if rng.random() < 0.6 else int(rng.integers(1, 600))
+    mix = rng.integers(0, 3)
+    if mix == 0:      # zero-heavy
+        deg = np.where(rng.random(V) < 0.5, 0, rng.integers(1, 8, V))
+    elif mix == 1:    # uniform
+        deg = rng.integers(0, 40, V)
+    else:             # a few hubs
+        deg = rng.integers(0, 6, V)
+        deg[rng.integers(0, V, 3)] = rng.integers(100, 800, 3)
+    deg = np.minimum(deg, C)
+    indptr = np.zeros(V + 1, np.int64)
+    indptr[1:] = np.cumsum(deg)
+    indices = np.empty(int(indptr[-1]), np.int32)
+    for r in range(V):
+        if deg[r]:
+            indices[indptr[r]:indptr[r + 1]] = np.sort(rng.choice(C, int(deg[r]), replace=False))
+    values = rng.standard_normal(len(indices)).astype(np.float32)
+    k = int(rng.choice(KS))
+    h = int(rng.integers(k, 257)) if rng.random() < 0.7 else 256
+    panel_cost = int(rng.choice([8, 64, 300, 4096]))
+    row_cost = int(rng.choice([1, 4, 16]))
+    return rng, V, C, indptr.astype(np.int32), indices, values, k, h, panel_cost, row_cost
+
+
+@pytest.mark.parametrize("seed", range(128))
+def test_fuzz_parity(dev, oracle, seed):
+    rng, V, C, indptr, indices, values, k, h, pc, rc = draw(seed)
+    x = rng.standard_normal((C, h)).astype(np.float32)
+    grad = rng.standard_normal((V, h)).astype(np.float32)
+    g = S.MaxKGraph(T(indptr, dev), T(indices, dev), T(values, dev), num_cols=C,
+                    panel_cost=pc, row_cost=rc)
+    ctx = f"V={V} C={C} E={len(indices)} k={k} h={h} panel_cost={pc} row_cost={rc}"
+
+    # CBSR producer: exact top-k sets (continuous inputs, no ties)
+    data, sel = S.topk_cbsr(T(x, dev), k)
+    sel_np, data_np = sel.cpu().numpy(), data.cpu().numpy()
+    ref_idx = np.argsort(-x, axis=1, kind="stable")[:, :k]
+    assert np.array_equal(np.sort(sel_np.astype(np.int64), 1), np.sort(ref_idx, 1)), ctx
+    assert np.array_equal(data_np, np.take_along_axis(x, sel_np.astype(np.int64), 1)), ctx
+
+    # forward SpGEMM (stale output must not leak)
+    out = torch.full((V, h), float("nan"), device=dev)
+    y = g.forward(data, sel, h, out=out)
+    ref = oracle.np_forward(indptr, indices, values, data_np, sel_np, h)
+    assert oracle.parity_error(y.cpu().numpy(), ref) <= TOL, ctx
+
+    # backward SSpMM, every algorithm that supports the shape
+    ref_b = oracle.np_backward(indptr, indices, values, grad, sel_np)
+    algos = [_lib.MAXK_BWD_ATOMIC, _lib.MAXK_BWD_STAGED]
+    if g.local_plan(k) is not None:
+        algos.append(_lib.MAXK_BWD_LOCAL)
+    for a in algos:
+        dx = torch.full((C, k), float("nan"), device=dev)
+        g.backward(T(grad, dev), sel, out=dx, algo=a)
+        assert oracle.parity_error(dx.cpu().numpy(), ref_b) <= TOL, f"{ctx} algo={a}"
+
+    # dense SpMM baseline
+    if h % 4 == 0:
+        yd = g.spmm_dense(T(x, dev))
+        assert oracle.parity_error(yd.cpu().numpy(),
+                                   oracle.np_spmm_dense(indptr, indices, values, x)) <= TOL, ctx
+
+    # multi-relation forward / backward (R relations sharing CSR and CBSR)
+    if k >= 4 and k & (k - 1) == 0 and len(indices) > 0:
+        R = int(rng.integers(1, 17))
+        vals = rng.standard_normal((len(indices), R)).astype(np.float32)
+        ym = g.forward_multi(data, sel, T(vals, dev), h).cpu().numpy()
+        gm = rng.standard_normal((R, V, h)).astype(np.float32)
+        dxm = g.backward_multi(T(gm, dev), sel, T(vals, dev)).cpu().numpy()
+        ref_m = np.zeros((C, k))
+        for q in range(R):
+            refq = oracle.np_forward(indptr, indices, vals[:, q], data_np, sel_np, h)
+            assert oracle.parity_error(ym[q], refq) <= TOL, f"{ctx} R={R} q={q}"
+            ref_m += oracle.np_backward(indptr, indices, vals[:, q], gm[q], sel_np)
+        assert oracle.parity_error(dxm, ref_m) <= TOL, f"{ctx} R={R}"
