@@ -129,9 +129,17 @@ class MaxKGraph:
         self.num_rows = indptr.numel() - 1
         # A may be rectangular (a multi-GPU rank's row block with halo columns)
         self.num_cols = self.num_rows if num_cols is None else int(num_cols)
-        self.num_edges = indices.numel()
         if validate:
             _validate_csr(indptr, indices, self.num_cols)
+        # a row slice of a bigger CSR (indptr[0] != 0, or fewer edges than indices
+        # holds) is rebased once: the graph's edges are indices[indptr[0]:indptr[-1]],
+        # and every plan (CSC, LOCAL) and per-call values array refers to those
+        base, end = (int(v) for v in indptr[[0, -1]].tolist()) if indptr.numel() > 0 else (0, 0)
+        if base != 0 or end != indices.numel():
+            indptr = (indptr - base).contiguous()
+            indices = indices[base:end]
+            values = values[base:end]
+        self.num_edges = indices.numel()
         if self.num_edges == 0:  # the C ABI wants valid pointers even for an empty edge list
             indices = torch.zeros(1, dtype=torch.int32, device=indices.device)
             values = torch.zeros(1, dtype=torch.float32, device=indices.device)

@@ -227,6 +227,29 @@ def test_backward_local_bands(dev, oracle, monkeypatch, band_bytes, k):
     assert oracle.parity_error(dx.cpu().numpy(), ref) <= TOL
 
 
+@pytest.mark.parametrize("algo", [_lib.MAXK_BWD_ATOMIC, _lib.MAXK_BWD_STAGED, _lib.MAXK_BWD_LOCAL])
+def test_offset_csr_view_backward(dev, oracle, g_small, algo):
+    """A row slice of a bigger CSR (indptr[0] != 0, indices longer than the
+    slice's edges) through forward and every backward: the graph is rebased at
+    construction, so the CSC and LOCAL plans see only the slice's edges."""
+    indptr, indices, values = g_small
+    lo, hi = 500, 1700
+    V, h, k = len(indptr) - 1, 256, 32
+    g = S.MaxKGraph(T(indptr[lo:hi + 1], dev), T(indices, dev), T(values, dev), panel_cost=200,
+                    num_cols=V)
+    e0, e1 = indptr[lo], indptr[hi]
+    sub_ip, sub_ix, sub_v = indptr[lo:hi + 1] - e0, indices[e0:e1], values[e0:e1]
+    assert g.num_edges == e1 - e0
+    data, sel = random_cbsr(V, k, h, seed=3)
+    y = g.forward(T(data, dev), T(sel, dev), h)
+    assert oracle.parity_error(y.cpu().numpy(),
+                               oracle.np_forward(sub_ip, sub_ix, sub_v, data, sel, h)) <= TOL
+    grad = np.random.default_rng(4).random((hi - lo, h), dtype=np.float32)
+    dx = g.backward(T(grad, dev), T(sel, dev), algo=algo)
+    assert oracle.parity_error(dx.cpu().numpy(),
+                               oracle.np_backward(sub_ip, sub_ix, sub_v, grad, sel)) <= TOL
+
+
 def test_offset_csr_view(dev, oracle, g_small):
     """indptr[0] != 0 (a row slice of a bigger CSR) is honoured."""
     indptr, indices, values = g_small
