@@ -101,6 +101,37 @@ int maxk_spgemm_forward_packed(const int32_t *sched, int64_t num_panels, const i
                                void *workspace, size_t workspace_bytes, void *stream);
 
 /* ---------------------------------------------------------------------------
+ * Plan builders (once per graph; spgemm_new_amd/csrc/maxk_plan.hip).  The
+ * reference's backward reuses the forward's .warp4 chunks
+ * (kernels/spmm_maxk_backward.cu:117-139); the STAGED and LOCAL algorithms
+ * need these instead.  CSR with indptr[0] == 0, num_edges = indptr[num_rows].
+ *
+ * maxk_csc_build: csc_indptr int32[num_cols + 1] and csc_pos int32[num_edges]
+ *   (CSC slot of CSR edge e; edges of one column keep CSR order).
+ * maxk_local_plan_build: destinations cut into ranges of <= dmax (<= 256)
+ *   columns balanced by in-degree (about target_waves ranges); call once with
+ *   dstart == NULL to get *num_waves (W; synchronises the stream once), then
+ *   with dstart int32[W+1], woff int32[W+1], edge_rc int32[E] (row | c_local
+ *   << 24, each range's in-edges in source-row order), edge_perm int32[E]
+ *   (the CSR edge of each slot) and edge_val fp32[E] (values[edge_perm], or
+ *   NULL) -- the inputs of maxk_sspmm_backward_local.  num_rows < 2^24.
+ * maxk_local_bands_build: seg_edge_off int32[(num_bands + 1) * W], source
+ *   rows cut into num_bands equal bands (see maxk_sspmm_backward_local).
+ * ------------------------------------------------------------------------- */
+size_t maxk_csc_workspace_bytes(int64_t num_edges, int num_cols);
+int maxk_csc_build(const int32_t *indices, int64_t num_edges, int num_cols, int32_t *csc_indptr,
+                   int32_t *csc_pos, void *workspace, size_t workspace_bytes, void *stream);
+size_t maxk_local_plan_workspace_bytes(int64_t num_edges, int num_cols, int target_waves);
+int maxk_local_plan_build(const int32_t *indptr, const int32_t *indices, const float *values,
+                          int num_rows, int num_cols, int64_t num_edges,
+                          const int32_t *csc_indptr, int dmax, int target_waves,
+                          int32_t *dstart, int32_t *woff, int32_t *edge_rc, int32_t *edge_perm,
+                          float *edge_val, int32_t *num_waves, void *workspace,
+                          size_t workspace_bytes, void *stream);
+int maxk_local_bands_build(const int32_t *woff, const int32_t *edge_rc, int num_waves,
+                           int num_rows, int num_bands, int32_t *seg_edge_off, void *stream);
+
+/* ---------------------------------------------------------------------------
  * Dense SpMM baseline: out = A . x with x fp32[num_cols, dim] dense, 4 <= dim
  * <= 256, dim % 4 == 0 (the comparison kernels of the reference's speedup
  * table: GNNAdvisor SAG kernels/spmm_gnna.cu:60-140 -- unweighted, pass

@@ -56,6 +56,12 @@ SIGNATURES = {
     "maxk_cbsr_packed_row_bytes": (_S, [_I]),
     "maxk_cbsr_pack": (_I, [_P, _P, _I, _I, _P, _P]),
     "maxk_spgemm_forward_packed": (_I, [_P, _L, _P, _P, _P, _P, _I, _I, _I, _P, _P, _S, _P]),
+    "maxk_csc_workspace_bytes": (_S, [_L, _I]),
+    "maxk_csc_build": (_I, [_P, _L, _I, _P, _P, _P, _S, _P]),
+    "maxk_local_plan_workspace_bytes": (_S, [_L, _I, _I]),
+    "maxk_local_plan_build": (_I, [_P, _P, _P, _I, _I, _L, _P, _I, _I, _P, _P, _P, _P, _P, _P, _P,
+                                   _S, _P]),
+    "maxk_local_bands_build": (_I, [_P, _P, _I, _I, _I, _P, _P]),
     "maxk_spmm_dense_forward": (_I, [_P, _L, _P, _P, _P, _P, _I, _I, _P, _P, _S, _P]),
     "maxk_forward_multi_workspace_bytes": (_S, [_L, _I, _I]),
     "maxk_spgemm_forward_multi": (_I, [_P, _L, _P, _P, _P, _I, _P, _P, _I, _I, _I, _P, _P, _S, _P]),

@@ -15,8 +15,9 @@ Also here: the CBSR producer (top-k), the dense gradient scatter / MaxK mask,
 and the fused multi-relation forward.
 
 All compute goes through the C ABI (``_lib``); there is no CPU or PyTorch
-fallback for the kernels.  Building the transpose uses torch GPU sort/scan
-ops once per graph (plumbing, outside the hot path).
+fallback for the kernels.  The plans (panel schedules, CSC transpose, LOCAL
+ranges and bands) are built once per graph by the library's device builders
+(csrc/maxk_plan.hip); torch only allocates.
 """
 from __future__ import annotations
 
@@ -169,17 +170,20 @@ class MaxKGraph:
         return t
 
     def csc(self):
-        """(csc_pos, csc_indptr, csc_sched, csc_num_panels), built once."""
+        """(csc_pos, csc_indptr, csc_sched, csc_num_panels), built once on the
+        device (maxk_csc_build: stable radix sort of the columns)."""
         if self._csc is None:
-            idx = self.indices[: self.num_edges].long()
-            order = torch.argsort(idx, stable=True)
-            csc_pos = torch.empty(self.num_edges, dtype=torch.int32, device=self.device)
-            csc_pos[order] = torch.arange(self.num_edges, dtype=torch.int32, device=self.device)
-            counts = torch.bincount(idx, minlength=self.num_cols)[: self.num_cols]
-            csc_indptr = torch.zeros(self.num_cols + 1, dtype=torch.int32, device=self.device)
-            csc_indptr[1:] = torch.cumsum(counts, 0).to(torch.int32)
-            sched, P = _build_schedule(csc_indptr, self.num_cols, self.num_edges,
-                                       self.csc_panel_cost, self.row_cost)
+            L = _lib.load()
+            E, C = self.num_edges, self.num_cols
+            csc_pos = torch.empty(max(E, 1), dtype=torch.int32, device=self.device)
+            csc_indptr = torch.empty(C + 1, dtype=torch.int32, device=self.device)
+            ws = torch.empty(max(1, L.maxk_csc_workspace_bytes(E, C)), dtype=torch.uint8,
+                             device=self.device)
+            _lib.check(L.maxk_csc_build(self.indices.data_ptr(), E, C, csc_indptr.data_ptr(),
+                                        csc_pos.data_ptr(), ws.data_ptr(), ws.numel(),
+                                        _stream(csc_pos)), "maxk_csc_build")
+            del ws
+            sched, P = _build_schedule(csc_indptr, C, E, self.csc_panel_cost, self.row_cost)
             self._csc = (csc_pos, csc_indptr, sched, P)
         return self._csc
 
@@ -187,7 +191,8 @@ class MaxKGraph:
         """Plan of the LOCAL backward (maxk_sspmm_backward_local), or None when
         the shape does not suit it.  Destinations are cut into ranges of at
         most dmax nodes balanced by in-degree; each range's in-edges are listed
-        in source-row order (stable sort of the CSR edges by owner range)."""
+        in source-row order.  Built on the device (maxk_local_plan_build; one
+        host read of the range count)."""
         if dim_k in self._local:
             plan = self._local[dim_k]
             if plan is not None and plan["values_key"] != _tensor_key(self.values):
@@ -197,37 +202,33 @@ class MaxKGraph:
         plan = None
         V, E = self.num_cols, self.num_edges      # V: destinations (columns of A)
         if E > 0 and self.num_rows < (1 << 24) and 64 % dim_k == 0:
+            import ctypes
+            L = _lib.load()
             dmax = max(1, min(256, LOCAL_WAVE_LDS_BYTES // (5 * dim_k)))
             _, csc_indptr, _, _ = self.csc()
             cus = torch.cuda.get_device_properties(self.device).multi_processor_count
-            w_tgt = max(-(-V // dmax), min(cus * LOCAL_WAVES_PER_CU, V))
-            tgt = torch.linspace(0, E, w_tgt + 1, device=self.device, dtype=torch.float64)
-            cuts = torch.searchsorted(csc_indptr.double(), tgt, right=False).clamp_(0, V)
-            cuts[0], cuts[-1] = 0, V
-            cuts = torch.unique(cuts)
-            # split ranges longer than dmax (hub-free but wide stretches of low in-degree)
-            span = cuts[1:] - cuts[:-1]
-            extra = (span - 1) // dmax
-            if int(extra.sum()) > 0:
-                base = torch.repeat_interleave(cuts[:-1], extra)
-                step = torch.arange(int(extra.sum()), device=self.device) - \
-                    torch.repeat_interleave(torch.cumsum(extra, 0) - extra, extra)
-                cuts = torch.unique(torch.cat([cuts, base + (step + 1) * dmax]))
-            dstart = cuts.to(torch.int32).contiguous()
-            W = dstart.numel() - 1
-            idx = self.indices[:E].long()
-            owner = torch.searchsorted(dstart, self.indices[:E], right=True) - 1
-            rows = torch.repeat_interleave(torch.arange(self.num_rows, device=self.device),
-                                           (self.indptr[1:] - self.indptr[:-1]).long())
-            perm = torch.argsort(owner, stable=True)
-            erc = (rows[perm] | ((idx[perm] - dstart.long()[owner[perm]]) << 24)).to(torch.int32)
-            woff = torch.zeros(W + 1, dtype=torch.int32, device=self.device)
-            woff[1:] = torch.cumsum(torch.bincount(owner, minlength=W), 0).to(torch.int32)
-            perm32 = perm.to(torch.int32)
-            del rows, owner, idx, perm
+            T = max(-(-V // dmax), min(cus * LOCAL_WAVES_PER_CU, V))
+            ws = torch.empty(max(1, L.maxk_local_plan_workspace_bytes(E, V, T)),
+                             dtype=torch.uint8, device=self.device)
+            st = _stream(ws)
+            n = ctypes.c_int32(0)
+            args = (self.indptr.data_ptr(), self.indices.data_ptr(), self.values.data_ptr(),
+                    self.num_rows, V, E, csc_indptr.data_ptr(), dmax, T)
+            _lib.check(L.maxk_local_plan_build(*args, None, None, None, None, None,
+                                               ctypes.byref(n), ws.data_ptr(), ws.numel(), st),
+                       "maxk_local_plan_build(count)")
+            W = int(n.value)
+            i32 = dict(dtype=torch.int32, device=self.device)
+            dstart, woff = torch.empty(W + 1, **i32), torch.empty(W + 1, **i32)
+            erc, perm = torch.empty(E, **i32), torch.empty(E, **i32)
+            ev = torch.empty(E, dtype=torch.float32, device=self.device)
+            _lib.check(L.maxk_local_plan_build(*args, dstart.data_ptr(), woff.data_ptr(),
+                                               erc.data_ptr(), perm.data_ptr(), ev.data_ptr(),
+                                               ctypes.byref(n), ws.data_ptr(), ws.numel(), st),
+                       "maxk_local_plan_build")
+            del ws
             plan = {"dmax": dmax, "num_waves": W, "dstart": dstart, "woff": woff,
-                    "edge_rc": erc.contiguous(), "perm": perm32, "bands": {},
-                    "edge_val": self.values[:E][perm32.long()].contiguous(),
+                    "edge_rc": erc, "perm": perm, "bands": {}, "edge_val": ev,
                     "values_key": _tensor_key(self.values)}
         self._local[dim_k] = plan
         return plan
@@ -242,24 +243,13 @@ class MaxKGraph:
         hit = plan["bands"].get(ns)
         if hit is not None:
             return hit
-        W, woff = plan["num_waves"], plan["woff"]
-        if ns == 1:
-            seg = torch.cat([woff[:-1], woff[1:]])
-        else:
-            n = int(woff[-1])
-            owner = torch.repeat_interleave(torch.arange(W, device=self.device),
-                                            (woff[1:] - woff[:-1]).long(), output_size=n)
-            key = owner * self.num_rows + (plan["edge_rc"].long() & 0xFFFFFF)
-            del owner
-            cuts = torch.div(torch.arange(ns + 1, device=self.device) * self.num_rows, ns,
-                             rounding_mode="floor")
-            q = torch.arange(W, device=self.device)[None, :] * self.num_rows + cuts[:, None]
-            seg = torch.searchsorted(key, q.reshape(-1)).to(torch.int32)
-            seg = seg.view(ns + 1, W)
-            seg[-1] = woff[1:]
-            seg = seg.reshape(-1)
-            del key, q
-        hit = (seg.contiguous(), ns)
+        W = plan["num_waves"]
+        seg = torch.empty((ns + 1) * W, dtype=torch.int32, device=self.device)
+        L = _lib.load()
+        _lib.check(L.maxk_local_bands_build(plan["woff"].data_ptr(), plan["edge_rc"].data_ptr(), W,
+                                            self.num_rows, ns, seg.data_ptr(), _stream(seg)),
+                   "maxk_local_bands_build")
+        hit = (seg, ns)
         plan["bands"][ns] = hit
         return hit
 
