@@ -166,7 +166,9 @@ int maxk_spgemm_forward_multi(const int32_t *sched, int64_t num_panels, const in
  * Backward SSpMM  dXs[c,l] = sum_{e: idx[e]=c} val[e] * G[row(e), sel[c,l]]
  * (spmm_maxk_backward.cu:15-115, K2).  Writes every element of dxs (no
  * pre-zeroing needed).  Workspace: maxk_backward_workspace_bytes(...).
- * algo: MAXK_BWD_AUTO picks the fastest measured algorithm for the shape.
+ * algo: MAXK_BWD_AUTO = STAGED when the CSC inputs and a workspace are given,
+ * else ATOMIC (the measured per-shape choice, LOCAL included, is made above
+ * the ABI: MaxKGraph.autotune_backward, or the harness's timing loop).
  * ------------------------------------------------------------------------- */
 #define MAXK_BWD_AUTO 0
 #define MAXK_BWD_ATOMIC 1      /* push + global float atomics (reference's scheme) */
