@@ -1286,23 +1286,25 @@ __device__ __forceinline__ const float *g_at(const float *grad, uint32_t row_off
                                                ((row_off + col) << 2));
 }
 
-// One round of the LOCAL loop for K in {32, 64}: R = 16 edge records held in
-// SGPRs (wave-uniform loads), NG = R/EPS gathers issued back to back, then the
-// NG LDS read-modify-writes.  Row offsets, destination slots and the clash
-// test are scalar; per lane only the half-select (EPS = 2), the selector byte
-// and the gather remain.  All R records are valid (the tail round of a wave's
-// list takes the generic loop).
+// A round's gathered values and destination slots, between issue and commit.
+template <int K>
+struct LocalRound {
+    static constexpr int EPS = kWave / K;
+    static constexpr int NG = LOCAL_R / EPS;
+    float gv[NG], vv[NG];
+    int ai[NG];
+    uint32_t clash;
+};
+
 template <int K, bool WIDE>
-__device__ __forceinline__ void local_round(const int32_t *__restrict__ rec_rc,
+__device__ __forceinline__ void local_issue(const int32_t *__restrict__ rec_rc,
                                             const float *__restrict__ rec_v,
                                             const float *__restrict__ grad, uint32_t dim,
-                                            const uint8_t *sl, float *acc, int grp, int l)
+                                            const uint8_t *sl, int grp, int l, LocalRound<K> &rd)
 {
     constexpr int EPS = kWave / K;
     constexpr int R = LOCAL_R;
     constexpr int NG = R / EPS;
-    float gv[NG], vv[NG];
-    int ai[NG];
     uint32_t ro[NG], col[NG];
     uint32_t clash = 0;
     const bool hi = EPS == 2 && grp != 0;
@@ -1338,31 +1340,56 @@ __device__ __forceinline__ void local_round(const int32_t *__restrict__ rec_rc,
         uint32_t xs = sa ^ sb, xo = oa ^ ob, xv = va ^ vb;
         asm volatile("" : "+s"(sa), "+s"(oa), "+s"(va), "+s"(xs), "+s"(xo), "+s"(xv));
         if constexpr (EPS == 2) {
-            ai[u] = (int)(sa ^ (xs & m)) + l;
+            rd.ai[u] = (int)(sa ^ (xs & m)) + l;
             ro[u] = oa ^ (xo & m);
-            vv[u] = __builtin_bit_cast(float, va ^ (xv & m));
+            rd.vv[u] = __builtin_bit_cast(float, va ^ (xv & m));
         } else {
-            ai[u] = (int)sa + l;
+            rd.ai[u] = (int)sa + l;
             ro[u] = oa;
-            vv[u] = __builtin_bit_cast(float, va);
+            rd.vv[u] = __builtin_bit_cast(float, va);
         }
     }
+    rd.clash = clash;
     // selector bytes for all groups, then all gathers back to back
 #pragma unroll
-    for (int u = 0; u < NG; ++u) col[u] = sl[ai[u]];
+    for (int u = 0; u < NG; ++u) col[u] = sl[rd.ai[u]];
 #pragma unroll
-    for (int u = 0; u < NG; ++u) gv[u] = *g_at<WIDE>(grad, ro[u], col[u]);
+    for (int u = 0; u < NG; ++u) rd.gv[u] = *g_at<WIDE>(grad, ro[u], col[u]);
+}
+
+template <int K>
+__device__ __forceinline__ void local_commit(const LocalRound<K> &rd, float *acc, int grp)
+{
+    constexpr int EPS = kWave / K;
+    constexpr int NG = LocalRound<K>::NG;
 #pragma unroll
     for (int u = 0; u < NG; ++u) {
-        if (!((clash >> u) & 1u)) {
-            acc[ai[u]] = fmaf(vv[u], gv[u], acc[ai[u]]);
+        if (!((rd.clash >> u) & 1u)) {
+            acc[rd.ai[u]] = fmaf(rd.vv[u], rd.gv[u], acc[rd.ai[u]]);
         } else {  // both halves target one destination: one half at a time
             for (int gg = 0; gg < EPS; ++gg) {
-                if (grp == gg) acc[ai[u]] = fmaf(vv[u], gv[u], acc[ai[u]]);
+                if (grp == gg) acc[rd.ai[u]] = fmaf(rd.vv[u], rd.gv[u], acc[rd.ai[u]]);
                 wave_sync_lds();
             }
         }
     }
+}
+
+// One round of the LOCAL loop for K in {32, 64}: R = 16 edge records held in
+// SGPRs (wave-uniform loads), NG = R/EPS gathers issued back to back, then the
+// NG LDS read-modify-writes.  Row offsets, destination slots and the clash
+// test are scalar; per lane only the half-select (EPS = 2), the selector byte
+// and the gather remain.  All R records are valid (the tail round of a wave's
+// list takes the generic loop).
+template <int K, bool WIDE>
+__device__ __forceinline__ void local_round(const int32_t *__restrict__ rec_rc,
+                                            const float *__restrict__ rec_v,
+                                            const float *__restrict__ grad, uint32_t dim,
+                                            const uint8_t *sl, float *acc, int grp, int l)
+{
+    LocalRound<K> rd;
+    local_issue<K, WIDE>(rec_rc, rec_v, grad, dim, sl, grp, l, rd);
+    local_commit<K>(rd, acc, grp);
 }
 
 // The generic LOCAL loop (any K dividing 64): records shuffled out of VGPRs.
