@@ -193,11 +193,8 @@ def cuda_topk_maxk_float(input, k: int):
     if not (0 < k <= input.size(1)):
         raise RuntimeError("Invalid k value")
     x = input.float() if input.dtype != torch.float32 else input
-    if x.size(1) <= 256:
-        vals, idx = topk_cbsr(x.contiguous(), k, order="value")  # HIP producer
-        return vals, idx.to(torch.int32)
-    vals, idx = torch.topk(x, k, dim=1)  # dim > 256: outside the kernels' range
-    return vals.contiguous(), idx.to(torch.int32).contiguous()
+    vals, idx = topk_cbsr(x.contiguous(), k, order="value")  # HIP producer (dim <= 256)
+    return vals, idx.to(torch.int32)
 
 
 def cuda_topk_maxk(input, k: int):

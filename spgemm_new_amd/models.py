@@ -26,26 +26,17 @@ class MaxK(Function):
 
     @staticmethod
     def forward(ctx, input, k=1):
-        ctx.hip = input.is_cuda and input.dtype == torch.float32 and input.dim() == 2 \
-            and input.size(1) <= 256
-        if ctx.hip:
-            _, sel, out = topk_cbsr(input.contiguous(), k, dense=True)
-            ctx.save_for_backward(sel)
-            return out
-        # other dtypes / widths are outside the kernels' domain: the reference's
-        # own formulation (utils/models.py:44-50) on the tensor's device
-        _, indices = input.topk(k, dim=1)
-        mask = torch.zeros_like(input)
-        mask.scatter_(1, indices, 1)
-        ctx.save_for_backward(mask)
-        return input * mask
+        # the HIP producer's domain; no fallback outside it (a CPU or fp64 tensor raises)
+        if input.dim() != 2 or input.size(1) > 256:
+            raise RuntimeError("MaxK: input must be 2-D with at most 256 columns")
+        _, sel, out = topk_cbsr(input.contiguous(), k, dense=True)
+        ctx.save_for_backward(sel)
+        return out
 
     @staticmethod
     def backward(ctx, grad_output):
-        (saved,) = ctx.saved_tensors
-        if ctx.hip:
-            return cbsr_mask(grad_output.contiguous(), saved), None
-        return grad_output * saved, None
+        (sel,) = ctx.saved_tensors
+        return cbsr_mask(grad_output.contiguous(), sel), None
 
 
 def cbsr_topk(features: torch.Tensor, maxk: int, order: str = "value"):

@@ -136,6 +136,9 @@ class MaxKGraph:
         # holds) is rebased once: the graph's edges are indices[indptr[0]:indptr[-1]],
         # and every plan (CSC, LOCAL) and per-call values array refers to those
         base, end = (int(v) for v in indptr[[0, -1]].tolist()) if indptr.numel() > 0 else (0, 0)
+        # the caller's tensors stay referenced: graph caches key on their storage
+        # addresses, which must not be reused while this graph lives
+        self._src = (indptr, indices, values)
         if base != 0 or end != indices.numel():
             indptr = (indptr - base).contiguous()
             indices = indices[base:end]
