@@ -168,6 +168,63 @@ def vendor_baseline(g, indptr, indices, values, X, sel, y, fwd_ms, ev_ms):
     return out
 
 
+def bench_multi_partitioned(args, indptr, indices, vals, data, sel, V, E, h, k, R, dev, world,
+                            rank, dist, gen, b_fused):
+    """Config 5 on N GPUs: rows partitioned as in the single-relation path, one
+    halo exchange per step shared by the R relations, the fused local forward
+    (forward_multi) and the composed backward with one reverse exchange.
+    value = the whole-graph fused-forward bytes / the forward time (max over
+    ranks); the backward is reported beside it."""
+    from spgemm_new_amd.distributed import PartitionedMaxK
+    kw = {"panel_cost": args.panel_cost} if args.panel_cost else {}
+    model = PartitionedMaxK(indptr, indices, vals, rank, world, dev, **kw)
+    r0, r1 = model.bounds[rank], model.bounds[rank + 1]
+    data_l, sel_l = model.local_rows(data), model.local_rows(sel)
+    G_l = torch.rand((R, r1 - r0, h), generator=gen, device=dev)
+
+    def timed(fn):
+        for _ in range(args.warmup):
+            fn()
+        torch.cuda.synchronize()
+        dist.barrier()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for _ in range(args.steps):
+            fn()
+        torch.cuda.synchronize()
+        dist.barrier()
+        tt = torch.tensor([time.perf_counter() - t0], device=dev, dtype=torch.float64)
+        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+        return float(tt) / args.steps * 1e3
+    t_f = timed(lambda: model.forward_multi(data_l, sel_l, h))
+    t_b = timed(lambda: model.backward_multi(G_l, sel_l))
+    val = b_fused / (t_f / 1e3) / 1e9
+    b_rank = torch.tensor([float(model.algorithmic_bytes_multi(k, h))], device=dev,
+                          dtype=torch.float64)
+    dist.all_reduce(b_rank, op=dist.ReduceOp.MAX)
+    p = model.plan
+    result = {
+        "metric": f"fused {R}-relation SpGEMM forward GB/s, {args.graph} h={h} k={k}",
+        "value": round(val, 2), "unit": "GB/s", "n_gpus": world, "steps": args.steps,
+        "warmup": args.warmup, "ms_per_step": round(t_f, 4), "higher_is_better": True,
+        "scaling": "strong", "vs_baseline": None, "dtype": "fp32",
+        "data": "synthetic (power-law degrees, uniform columns, seed 123; values/X U(0,1))",
+        "config": {"workload": f"{args.graph} fused multi-relation forward", "graph": args.graph,
+                   "num_nodes": V, "num_edges": E, "hidden": h, "k": k, "relations": R,
+                   "parallelism": f"rowpart{world}", "halo_nodes_rank0": p.num_halo,
+                   "own_nodes_rank0": p.num_own},
+        "roofline": {"bound": "hbm", "achieved": round(float(b_rank) / (t_f / 1e3) / 1e9, 1),
+                     "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                     "frac": round(float(b_rank) / (t_f / 1e3) / 1e9 / HBM_PEAK_GBS, 4),
+                     "traffic": None,
+                     "kernel": "spgemm_forward_multi (per rank, incl. halo exchange)",
+                     "algorithmic_bytes_per_launch": int(float(b_rank))},
+        "bwd_multi_ms": round(t_b, 4),
+    }
+    if rank == 0:
+        print(json.dumps(result), flush=True)
+
+
 def _cpu_model():
     try:
         for line in open("/proc/cpuinfo"):
@@ -178,7 +235,7 @@ def _cpu_model():
     return "unknown"
 
 
-def bench_multi(args, S, indptr, indices, data, sel, V, E, h, k, dev, world):
+def bench_multi(args, S, indptr, indices, data, sel, V, E, h, k, dev, world, rank=0, dist=None):
     """BASELINE config 5 (ogbn-proteins, R edge-feature relations): the fused
     multi-relation forward Y[q] = A_q . X^ (one CSR + CBSR gather shared by R
     relations) timed against R single-relation forwards.  Bytes per fused call
@@ -187,6 +244,10 @@ def bench_multi(args, S, indptr, indices, data, sel, V, E, h, k, dev, world):
     gen = torch.Generator(device=dev)
     gen.manual_seed(args.seed + 7)
     vals = torch.rand((E, R), generator=gen, device=dev)
+    b_fused = E * (4 + 4 * R + 5 * k) + R * 4 * h * V
+    if dist is not None:
+        return bench_multi_partitioned(args, indptr, indices, vals, data, sel, V, E, h, k, R, dev,
+                                       world, rank, dist, gen, b_fused)
     cols = [vals[:, q].contiguous() for q in range(R)]
     g = S.MaxKGraph(indptr, indices, cols[0])
     y = torch.empty((R, V, h), device=dev)
@@ -216,7 +277,6 @@ def bench_multi(args, S, indptr, indices, data, sel, V, E, h, k, dev, world):
         g.backward_multi(G, sel, vals, out=dx)
     t_f, t_u = timed(fused), timed(unfused)
     t_b = timed(backward)
-    b_fused = E * (4 + 4 * R + 5 * k) + R * 4 * h * V
     b_unf = R * (8 * E + 5 * k * E + 4 * h * V)
     val = b_fused / (t_f / 1e3) / 1e9
     result = {
@@ -289,7 +349,8 @@ def main():
         kw["row_cost"] = args.row_cost
 
     if args.relations > 1:
-        return bench_multi(args, S, indptr, indices, data, sel, V, E, h, k, dev, world)
+        return bench_multi(args, S, indptr, indices, data, sel, V, E, h, k, dev, world, rank,
+                           dist if partitioned else None)
 
     if partitioned:
         from spgemm_new_amd.distributed import PartitionedMaxK

@@ -101,6 +101,26 @@ int maxk_spgemm_forward_packed(const int32_t *sched, int64_t num_panels, const i
                                void *workspace, size_t workspace_bytes, void *stream);
 
 /* ---------------------------------------------------------------------------
+ * Halo records (the multi-GPU path; the reference is
+ * single-GPU and has no counterpart).  maxk_cbsr_gather_records writes record
+ * i = CBSR row rows[i] (rows == NULL: row i) as dim_k fp32 values followed by
+ * dim_k selector bytes, 5*dim_k bytes per record, unpadded -- the all-to-all-v
+ * message of packed halo rows.  maxk_spgemm_forward_records is
+ * maxk_spgemm_forward reading its CBSR from such records in place (column c =
+ * record c; records 16-B aligned); with flags = MAXK_FWD_ACCUMULATE it adds
+ * A . X^ into out (out += ...) instead of overwriting it, so a rank's halo
+ * column block adds onto the rows its own block wrote.  dim_k a power of two
+ * in [4, 256]; same schedule and workspace as maxk_spgemm_forward.
+ * ------------------------------------------------------------------------- */
+#define MAXK_FWD_ACCUMULATE 1
+int maxk_cbsr_gather_records(const float *cbsr_data, const uint8_t *cbsr_sel, const int32_t *rows,
+                             int64_t num_records, int dim_k, void *records, void *stream);
+int maxk_spgemm_forward_records(const int32_t *sched, int64_t num_panels, const int32_t *indptr,
+                                const int32_t *indices, const float *values, const void *records,
+                                int num_rows, int dim_origin, int dim_k, int flags, float *out,
+                                void *workspace, size_t workspace_bytes, void *stream);
+
+/* ---------------------------------------------------------------------------
  * Plan builders (once per graph; spgemm_new_amd/csrc/maxk_plan.hip).  The
  * reference's backward reuses the forward's .warp4 chunks
  * (kernels/spmm_maxk_backward.cu:117-139); the STAGED and LOCAL algorithms

@@ -11,7 +11,7 @@ Host-side mirrors of the reference surface:
 * ``distributed``              1-D row partition + RCCL all-to-all-v halo
 """
 from ._lib import LIB_PATH, MaxKError, load  # noqa: F401
-from .ops import (MaxKGraph, cbsr_mask, cbsr_scatter, spgemm_forward, spmm_dense, sspmm_backward,  # noqa: F401
-                  topk_cbsr, warp4_build)
+from .ops import (MaxKGraph, cbsr_gather_records, cbsr_mask, cbsr_scatter, spgemm_forward,  # noqa: F401
+                  spgemm_forward_records, spmm_dense, sspmm_backward, topk_cbsr, warp4_build)
 
 __version__ = "0.1.0"

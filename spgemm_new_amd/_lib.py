@@ -30,6 +30,7 @@ MAXK_BWD_LOCAL = 3
 MAXK_TOPK_ORDER_COLUMN = 0
 MAXK_TOPK_ORDER_VALUE = 1
 MAXK_TOPK_ORDER_LANE = 2
+MAXK_FWD_ACCUMULATE = 1
 DEFAULT_PANEL_COST = 2048
 DEFAULT_ROW_COST = 16
 
@@ -65,6 +66,8 @@ SIGNATURES = {
     "maxk_spmm_dense_forward": (_I, [_P, _L, _P, _P, _P, _P, _I, _I, _P, _P, _S, _P]),
     "maxk_forward_multi_workspace_bytes": (_S, [_L, _I, _I]),
     "maxk_spgemm_forward_multi": (_I, [_P, _L, _P, _P, _P, _I, _P, _P, _I, _I, _I, _P, _P, _S, _P]),
+    "maxk_cbsr_gather_records": (_I, [_P, _P, _P, _L, _I, _P, _P]),
+    "maxk_spgemm_forward_records": (_I, [_P, _L, _P, _P, _P, _P, _I, _I, _I, _I, _P, _P, _S, _P]),
     "maxk_topk_cbsr": (_I, [_P, _I, _I, _L, _I, _I, _P, _P, _P, _P]),
     "maxk_cbsr_scatter": (_I, [_P, _P, _I, _I, _I, _P, _P]),
     "maxk_cbsr_mask": (_I, [_P, _P, _I, _I, _I, _P, _P]),

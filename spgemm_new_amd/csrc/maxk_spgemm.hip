@@ -343,7 +343,7 @@ __device__ __forceinline__ void flush_row(float *acc, int copies, float *__restr
 {
     const int lane = lane_id();
     wave_sync_lds();
-    if (OP == kStore && (dim & 3) == 0) {
+    if (OP != kAtomic && (dim & 3) == 0) {
         for (int c4 = lane; c4 < (dim >> 2); c4 += kWave) {
             f4 a = reinterpret_cast<f4 *>(acc)[c4];
             reinterpret_cast<f4 *>(acc)[c4] = f4{0.f, 0.f, 0.f, 0.f};
@@ -352,6 +352,7 @@ __device__ __forceinline__ void flush_row(float *acc, int copies, float *__restr
                 a += *q;
                 *q = f4{0.f, 0.f, 0.f, 0.f};
             }
+            if (OP == kAdd) a += reinterpret_cast<const f4 *>(dst)[c4];  // row owned by this wave
 #if FWD_NT_OUT
             __builtin_nontemporal_store(a, reinterpret_cast<f4 *>(dst) + c4);
 #else
@@ -382,7 +383,7 @@ __device__ __forceinline__ void zero_lds(float *acc, int n)
 
 // Panel-scheduled forward.  Rows [i0, i1) are finished and owned by this
 // wave (plain store); row i1 is in progress at the panel end -> carry.
-template <int K, int RS = 0>
+template <int K, int RS = 0, bool ACC = false>
 __global__ __launch_bounds__(kBlock) void fwd_panel_kernel(
     const int2 *__restrict__ sched, int64_t num_panels, const int32_t *__restrict__ indptr,
     const int32_t *__restrict__ idx, const float *__restrict__ val,
@@ -403,7 +404,7 @@ __global__ __launch_bounds__(kBlock) void fwd_panel_kernel(
     for (int r = i0; r < i1; ++r) {
         const int re = indptr[r + 1];
         if (e < re) fwd_edges<K, RS>(e, re, k, idx, val, data, sel, acc);
-        flush_row<kStore>(acc, copies, out + (size_t)r * dim, dim);
+        flush_row<ACC ? kAdd : kStore>(acc, copies, out + (size_t)r * dim, dim);
         e = re;
     }
     int has_carry = 0;
@@ -1540,6 +1541,27 @@ __global__ __launch_bounds__(kBlock) void cbsr_pack_kernel(const float *__restri
     reinterpret_cast<uint32_t *>(rec)[i] = v;
 }
 
+// Halo records (multi-GPU exchange): record i = the CBSR row rows[i] as k fp32
+// values then k selector bytes, 5k bytes unpadded (k a power of two >= 4, so
+// records stay 4-B aligned and, for k >= 32, 16-B aligned).  The receiver's
+// forward reads the records in place (fwd_panel_kernel<K, 5K>).
+template <int K>
+__global__ __launch_bounds__(kBlock) void cbsr_records_kernel(const float *__restrict__ data,
+                                                              const uint8_t *__restrict__ sel,
+                                                              const int32_t *__restrict__ rows,
+                                                              int64_t n, uint8_t *__restrict__ rec)
+{
+    constexpr int W = 5 * K / 4;  // dwords per record
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n * W) return;
+    const int64_t j = i / W;
+    const int w = (int)(i - j * W);
+    const int64_t c = rows ? rows[j] : j;
+    const uint32_t v = w < K ? __builtin_bit_cast(uint32_t, data[c * K + w])
+                             : *reinterpret_cast<const uint32_t *>(sel + c * K + 4 * (w - K));
+    reinterpret_cast<uint32_t *>(rec)[i] = v;
+}
+
 // dXs zeroing for the ATOMIC backward / empty graphs.  A kernel rather than
 // hipMemsetAsync: captured into a hipGraph, the memset node was not reliably
 // ordered before the following atomics (wrong results in about half of the
@@ -1633,6 +1655,47 @@ struct FwdPanelPacked {
             if (rc) return rc;
             hipLaunchKernelGGL(carry_fixup_kernel, dim3((unsigned)blocks), dim3(kBlock), 0, st, P,
                                carry, carry_row, out, dim, (dim + 3) & ~3, 1, (size_t)0);
+            return launch_status();
+        }
+    }
+};
+
+template <int K>
+struct FwdRecords {
+    static int run(const int32_t *sched, int64_t P, const int32_t *indptr, const int32_t *idx,
+                   const float *val, const uint8_t *rec, int V, int dim, int k, bool acc,
+                   float *out, float *carry, int32_t *carry_row, hipStream_t st)
+    {
+        if constexpr (K == 0) {
+            return MAXK_E_DIM;
+        } else {
+            constexpr int RS = 5 * K;
+            const int64_t blocks = ceil_div(P, kWavesPerBlock);
+            auto kern = acc ? fwd_panel_kernel<K, RS, true> : fwd_panel_kernel<K, RS, false>;
+            hipLaunchKernelGGL(kern, dim3((unsigned)blocks), dim3(kBlock), fwd_lds_bytes<K>(k), st,
+                               reinterpret_cast<const int2 *>(sched), P, indptr, idx, val,
+                               reinterpret_cast<const float *>(rec), rec + 4 * K, V, dim, k, out,
+                               carry, carry_row);
+            int rc = launch_status();
+            if (rc) return rc;
+            hipLaunchKernelGGL(carry_fixup_kernel, dim3((unsigned)blocks), dim3(kBlock), 0, st, P,
+                               carry, carry_row, out, dim, (dim + 3) & ~3, 1, (size_t)0);
+            return launch_status();
+        }
+    }
+};
+
+template <int K>
+struct CbsrRecords {
+    static int run(const float *data, const uint8_t *sel, const int32_t *rows, int64_t n,
+                   uint8_t *rec, hipStream_t st)
+    {
+        if constexpr (K == 0) {
+            return MAXK_E_DIM;
+        } else {
+            const int64_t words = n * (5 * K / 4);
+            hipLaunchKernelGGL(cbsr_records_kernel<K>, dim3((unsigned)ceil_div(words, kBlock)),
+                               dim3(kBlock), 0, st, data, sel, rows, n, rec);
             return launch_status();
         }
     }
@@ -1940,6 +2003,40 @@ int maxk_spgemm_forward_packed(const int32_t *sched, int64_t num_panels, const i
     case 8: return FwdPanelPacked<8>::run(sched, num_panels, indptr, indices, values, rec, num_rows, dim_origin, dim_k, out, carry, carry_row, st);
     default: return FwdPanelPacked<16>::run(sched, num_panels, indptr, indices, values, rec, num_rows, dim_origin, dim_k, out, carry, carry_row, st);
     }
+}
+
+int maxk_cbsr_gather_records(const float *cbsr_data, const uint8_t *cbsr_sel, const int32_t *rows,
+                             int64_t num_records, int dim_k, void *records, void *stream)
+{
+    if (dim_k < 4 || dim_k > kMaxDim || (dim_k & (dim_k - 1))) return MAXK_E_DIM;
+    if (num_records < 0 || (num_records > 0 && (!cbsr_data || !cbsr_sel || !records)))
+        return MAXK_E_ARG;
+    if (num_records == 0) return MAXK_OK;
+    return dispatch_k<CbsrRecords>(dim_k, cbsr_data, cbsr_sel, rows, num_records,
+                                   static_cast<uint8_t *>(records), as_stream(stream));
+}
+
+int maxk_spgemm_forward_records(const int32_t *sched, int64_t num_panels, const int32_t *indptr,
+                                const int32_t *indices, const float *values, const void *records,
+                                int num_rows, int dim_origin, int dim_k, int flags, float *out,
+                                void *workspace, size_t workspace_bytes, void *stream)
+{
+    if (!sched || !indptr || !out || num_panels < 1 || num_rows < 0) return MAXK_E_ARG;
+    if (flags & ~MAXK_FWD_ACCUMULATE) return MAXK_E_ARG;
+    if (!dims_ok(dim_origin, dim_k) || dim_k < 4 || (dim_k & (dim_k - 1))) return MAXK_E_DIM;
+    if (num_rows == 0) return MAXK_OK;
+    if (!indices || !values || !records) return MAXK_E_ARG;
+    if (reinterpret_cast<uintptr_t>(records) & 15) return MAXK_E_ARG;
+    if (!workspace || workspace_bytes < maxk_forward_workspace_bytes(num_panels, dim_origin))
+        return MAXK_E_WORKSPACE;
+    const size_t dimp = (size_t)((dim_origin + 3) & ~3);
+    float *carry = static_cast<float *>(workspace);
+    int32_t *carry_row = reinterpret_cast<int32_t *>(
+        static_cast<char *>(workspace) + align_up((size_t)num_panels * dimp * sizeof(float), 256));
+    return dispatch_k<FwdRecords>(dim_k, sched, num_panels, indptr, indices, values,
+                                  static_cast<const uint8_t *>(records), num_rows, dim_origin,
+                                  dim_k, (flags & MAXK_FWD_ACCUMULATE) != 0, out, carry, carry_row,
+                                  as_stream(stream));
 }
 
 size_t maxk_forward_multi_workspace_bytes(int64_t num_panels, int dim_origin, int num_rel)

@@ -107,24 +107,51 @@ def _default_engine(local_indptr, local_indices, local_values, num_cols, **kw):
     return MaxKGraph(local_indptr, local_indices, local_values, num_cols=num_cols, **kw)
 
 
+def _records_ok(k: int) -> bool:
+    """k for which the halo records (maxk_cbsr_gather_records) exist."""
+    return 4 <= k <= 256 and k & (k - 1) == 0
+
+
 class PartitionedMaxK:
     """A rank's share of the graph + its halo exchange.
 
     ``forward(data_own, sel_own, dim)`` returns Y for own rows;
     ``backward(G_own, sel_own)`` returns dXs for own nodes (halo sums added).
-    ``engine(indptr, indices, values, num_cols, **kw)`` builds the local compute
-    object (must provide ``forward(data, sel, dim)`` / ``backward(grad, sel)``).
+    With ``values`` fp32[E, R] (R edge-feature relations, BASELINE config 5)
+    ``forward_multi`` / ``backward_multi`` are the partitioned fused
+    multi-relation forward ([R, own rows, h]) and its backward.
+
+    The halo CBSR travels as records (k fp32 + k selector bytes, 5k B per node,
+    one all-to-all-v message) that the receiver's forward reads in place
+    (MaxKGraph.forward_records); with ``overlap`` the rank's block is split
+    by column into own | halo parts, the own part computes while the records
+    are in flight and the halo part accumulates onto it.
+
+    ``engine(indptr, indices, values, num_cols, **kw)`` builds the local
+    compute object: ``forward(data, sel, dim)``, ``backward(grad, sel)``,
+    optionally ``forward_records(records, k, dim, out=, accumulate=)`` (used
+    when present and k is a power of two in [4, 256]; otherwise the halo rows
+    are unpacked and concatenated), and ``forward_multi`` / ``backward_multi``
+    for relations.
     """
 
     def __init__(self, indptr, indices, values, rank: int, world: int, device,
-                 engine=None, row_cost: int = 16, overlap: bool = True, **engine_kw):
+                 engine=None, row_cost: int = 16, overlap: bool = True, records: bool = True,
+                 **engine_kw):
         self.rank, self.world, self.device = rank, world, torch.device(device)
         self.bounds = row_partition(indptr, world, row_cost)
         self.plan = HaloPlan(indptr, indices, self.bounds, rank, world, self.device)
         p = self.plan
         e0, e1 = p.edge_range
-        lv = values[e0:e1].to(self.device).contiguous()
+        if values.dim() not in (1, 2):
+            raise RuntimeError("values must be fp32[E] or fp32[E, R]")
+        self.num_rel = 1 if values.dim() == 1 else values.shape[1]
+        lv_all = values[e0:e1].to(self.device).contiguous()
+        self.values_local = lv_all                       # [E_local] or [E_local, R]
+        lv = lv_all if self.num_rel == 1 else lv_all[:, 0].contiguous()
         make = engine or _default_engine
+        self.send_rows = p.send_local.to(torch.int32).contiguous()
+        self.records = records
         # overlap (forward): the block is also split by column into own | halo
         # parts, so the own part computes while the halo CBSR is in flight.  The
         # backward keeps the single block: split, each part's LOCAL sweep visits
@@ -148,14 +175,22 @@ class PartitionedMaxK:
             self.local_halo = part(~is_own, p.num_own, p.num_halo)
         self.local = make(p.local_indptr, p.local_indices, lv, p.num_own + p.num_halo,
                           **engine_kw)
-        self._halo_sel = None
-        self._h_sel = None
+        self._bufs = {}
+        self._fwd_sel = None     # sel_own of the last forward
+        self._halo_part = None   # its halo selectors: [num_halo, k] (view of records or rows)
 
     # --------------------------------------------------------------- helpers
     def local_rows(self, t: torch.Tensor) -> torch.Tensor:
         """Slice of a global per-node tensor owned by this rank."""
         r0, r1 = self.bounds[self.rank], self.bounds[self.rank + 1]
         return t[r0:r1].to(self.device).contiguous()
+
+    def _buf(self, key, shape, dtype):
+        t = self._bufs.get(key)
+        if t is None or tuple(t.shape) != tuple(shape) or t.dtype != dtype:
+            t = torch.empty(shape, dtype=dtype, device=self.device)
+            self._bufs[key] = t
+        return t
 
     def _exchange(self, send_rows: torch.Tensor, width: int, dtype, reverse: bool = False):
         p = self.plan
@@ -164,63 +199,118 @@ class PartitionedMaxK:
         a2a(out, send_rows.contiguous(), rc, sc)
         return out
 
+    def _use_records(self, k: int, eng) -> bool:
+        return self.records and _records_ok(k) and hasattr(eng, "forward_records")
+
+    def _pack(self, data_own, sel_own):
+        """The rows my peers need, as one uint8 message [n_send, 5k]."""
+        k = data_own.shape[1]
+        if _records_ok(k) and data_own.is_cuda:
+            from .ops import cbsr_gather_records
+            return cbsr_gather_records(data_own, sel_own, self.send_rows,
+                                       out=self._buf(("send", k), (self.send_rows.numel(), 5 * k),
+                                                     torch.uint8))
+        rows = self.plan.send_local
+        return torch.cat([data_own[rows].view(torch.uint8).reshape(-1, 4 * k), sel_own[rows]],
+                         dim=1).contiguous()
+
+    @staticmethod
+    def _unpack(rec: torch.Tensor, k: int):
+        data = rec[:, : 4 * k].contiguous().view(torch.float32).reshape(-1, k)
+        return data, rec[:, 4 * k:]
+
     # --------------------------------------------------------------- compute
     def gather_halo_cbsr(self, data_own: torch.Tensor, sel_own: torch.Tensor):
         """All-to-all-v of packed CBSR rows -> (data, sel) for own + halo columns."""
-        p = self.plan
         k = data_own.shape[1]
-        packed = torch.cat([data_own[p.send_local].view(torch.uint8).reshape(-1, 4 * k),
-                            sel_own[p.send_local]], dim=1)
-        recv = self._exchange(packed, 5 * k, torch.uint8)
-        h_data = recv[:, : 4 * k].contiguous().view(torch.float32).reshape(-1, k)
-        h_sel = recv[:, 4 * k:].contiguous()
-        data = torch.cat([data_own, h_data]).contiguous()
-        sel = torch.cat([sel_own, h_sel]).contiguous()
-        return data, sel
+        recv = self._exchange(self._pack(data_own, sel_own), 5 * k, torch.uint8)
+        h_data, h_sel = self._unpack(recv, k)
+        self._fwd_sel, self._halo_part = sel_own, h_sel
+        return torch.cat([data_own, h_data]).contiguous(), torch.cat([sel_own, h_sel]).contiguous()
 
     def forward(self, data_own: torch.Tensor, sel_own: torch.Tensor, dim_origin: int = 256):
-        if self.overlap:
-            return self._forward_overlap(data_own, sel_own, dim_origin)
-        data, sel = self.gather_halo_cbsr(data_own, sel_own)
-        self._halo_sel = sel
-        return self.local.forward(data, sel, dim_origin)
-
-    def _forward_overlap(self, data_own, sel_own, dim_origin):
         p = self.plan
         k = data_own.shape[1]
-        packed = torch.cat([data_own[p.send_local].view(torch.uint8).reshape(-1, 4 * k),
-                            sel_own[p.send_local]], dim=1).contiguous()
-        recv = torch.empty((sum(p.recv_counts), 5 * k), dtype=torch.uint8, device=self.device)
-        work = a2a(recv, packed, p.recv_counts, p.send_counts, async_op=True)
+        if not self.overlap:
+            # single block: the halo rows are appended to the own rows (a table
+            # of whole 160-B records read in place measured slower than data +
+            # selector rows at full size: 3.63 vs 3.31 ms, tools/exp_rank_step.py)
+            data, sel = self.gather_halo_cbsr(data_own, sel_own)
+            return self.local.forward(data, sel, dim_origin)
+        if not self._use_records(k, self.local_halo):
+            return self._forward_overlap_rows(data_own, sel_own, dim_origin)
+        recv = self._buf(("recv", k), (p.num_halo, 5 * k), torch.uint8)
+        work = a2a(recv, self._pack(data_own, sel_own), p.recv_counts, p.send_counts,
+                   async_op=True)
         y = self.local_own.forward(data_own, sel_own, dim_origin)   # overlaps the exchange
         work.wait()
-        h_data = recv[:, : 4 * k].contiguous().view(torch.float32).reshape(-1, k)
-        h_sel = recv[:, 4 * k:].contiguous()
-        self._h_sel = h_sel
-        self._halo_sel = None
-        y += self.local_halo.forward(h_data, h_sel, dim_origin)
+        # the halo block reads the received records in place and adds onto y
+        self.local_halo.forward_records(recv, k, dim_origin, out=y, accumulate=True)
+        self._fwd_sel, self._halo_part = sel_own, recv[:, 4 * k:]
         return y
 
-    def backward(self, grad_own: torch.Tensor, sel_own: torch.Tensor | None = None):
+    def _forward_overlap_rows(self, data_own, sel_own, dim_origin):
         p = self.plan
-        if self._halo_sel is None and self._h_sel is not None and sel_own is not None:
-            self._halo_sel = torch.cat([sel_own, self._h_sel]).contiguous()
-        sel = self._halo_sel
-        if sel is None or (sel_own is not None and sel.shape[0] != p.num_own + p.num_halo):
-            if sel_own is None:
+        k = data_own.shape[1]
+        recv = torch.empty((p.num_halo, 5 * k), dtype=torch.uint8, device=self.device)
+        work = a2a(recv, self._pack(data_own, sel_own), p.recv_counts, p.send_counts,
+                   async_op=True)
+        y = self.local_own.forward(data_own, sel_own, dim_origin)   # overlaps the exchange
+        work.wait()
+        h_data, h_sel = self._unpack(recv, k)
+        self._fwd_sel, self._halo_part = sel_own, h_sel
+        y += self.local_halo.forward(h_data, h_sel.contiguous(), dim_origin)
+        return y
+
+    def _block_sel(self, sel_own: torch.Tensor | None) -> torch.Tensor:
+        """Selectors of the whole block (own + halo columns), contiguous."""
+        p = self.plan
+        if sel_own is None or sel_own is self._fwd_sel:
+            if self._halo_part is None:
                 raise RuntimeError("backward needs the forward's selectors (call forward first)")
-            k = sel_own.shape[1]
-            recv = self._exchange(sel_own[p.send_local], k, torch.uint8)
-            sel = torch.cat([sel_own, recv]).contiguous()
-        dxs = self.local.backward(grad_own, sel)
+            sel_own, halo = self._fwd_sel, self._halo_part
+        else:
+            halo = self._exchange(sel_own[p.send_local], sel_own.shape[1], torch.uint8)
+        k = sel_own.shape[1]
+        sel = self._buf(("sel_all", k), (p.num_own + p.num_halo, k), torch.uint8)
+        sel[: p.num_own] = sel_own
+        sel[p.num_own:] = halo
+        return sel
+
+    def _return_halo(self, dxs: torch.Tensor) -> torch.Tensor:
+        """Send the halo partial sums home and add the ones I receive."""
+        p = self.plan
         k = dxs.shape[1]
-        partial = dxs[p.num_own:]                               # halo partial sums, by owner
-        back = self._exchange(partial, k, torch.float32, reverse=True)
+        back = self._exchange(dxs[p.num_own:], k, torch.float32, reverse=True)
         own = dxs[: p.num_own]
         own.index_add_(0, p.send_local, back)
         return own
+
+    def backward(self, grad_own: torch.Tensor, sel_own: torch.Tensor | None = None):
+        return self._return_halo(self.local.backward(grad_own, self._block_sel(sel_own)))
+
+    # ------------------------------------------------- multi-relation (config 5)
+    def forward_multi(self, data_own: torch.Tensor, sel_own: torch.Tensor,
+                      dim_origin: int = 256) -> torch.Tensor:
+        """Y[q] = A_q . X^ for own rows, q < R (values fp32[E, R] at construction):
+        one halo exchange shared by all relations, then the fused local forward."""
+        if self.num_rel < 2 and self.values_local.dim() == 1:
+            raise RuntimeError("forward_multi needs values fp32[E, R] at construction")
+        data, sel = self.gather_halo_cbsr(data_own, sel_own)
+        return self.local.forward_multi(data, sel, self.values_local, dim_origin)
+
+    def backward_multi(self, grad_own: torch.Tensor, sel_own: torch.Tensor | None = None):
+        """dXs = sum_q (A_q^T G_q) at sel for own nodes; grad_own fp32[R, own rows, h]."""
+        dxs = self.local.backward_multi(grad_own, self._block_sel(sel_own), self.values_local)
+        return self._return_halo(dxs)
 
     def algorithmic_bytes(self, k: int, h: int) -> int:
         """This rank's share of 8E + 5kE + 4hV (fwd) = (bwd)."""
         e = self.plan.local_indices.numel()
         return 8 * e + 5 * k * e + 4 * h * self.plan.num_own
+
+    def algorithmic_bytes_multi(self, k: int, h: int) -> int:
+        """This rank's share of the fused multi-relation forward E(4 + 4R + 5k) + R*4hV."""
+        e = self.plan.local_indices.numel()
+        R = self.num_rel
+        return e * (4 + 4 * R + 5 * k) + R * 4 * h * self.plan.num_own

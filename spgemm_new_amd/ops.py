@@ -325,6 +325,13 @@ class MaxKGraph:
         """Y = A . scatter(CBSR)  (spmm_maxk.cu:17-106).  Returns fp32[V, dim_origin]."""
         return spgemm_forward(self, cbsr_data, cbsr_sel, dim_origin, out, values)
 
+    def forward_records(self, records: torch.Tensor, dim_k: int, dim_origin: int = 256,
+                        out: torch.Tensor | None = None, values: torch.Tensor | None = None,
+                        accumulate: bool = False) -> torch.Tensor:
+        """forward() with the CBSR read in place from halo records (uint8[num_cols, 5k],
+        see cbsr_gather_records); accumulate=True computes out += A . X^."""
+        return spgemm_forward_records(self, records, dim_k, dim_origin, out, values, accumulate)
+
     def forward_multi(self, cbsr_data: torch.Tensor, cbsr_sel: torch.Tensor,
                       values: torch.Tensor, dim_origin: int = 256,
                       out: torch.Tensor | None = None) -> torch.Tensor:
@@ -433,6 +440,63 @@ def spgemm_forward(g: MaxKGraph, data, sel, dim_origin: int = 256, out=None, val
                                      g.indices.data_ptr(), values.data_ptr(), data.data_ptr(),
                                      sel.data_ptr(), g.num_rows, dim_origin, k, out.data_ptr(),
                                      ws.data_ptr(), ws.numel(), _stream(out)), "maxk_spgemm_forward")
+    return out
+
+
+def cbsr_gather_records(data: torch.Tensor, sel: torch.Tensor, rows: torch.Tensor | None = None,
+                        out: torch.Tensor | None = None) -> torch.Tensor:
+    """Halo records: uint8[n, 5k], record i = (data[rows[i]] as k fp32, sel[rows[i]]).
+    The multi-GPU all-to-all-v message (maxk_cbsr_gather_records)."""
+    check_tensor(data, "input_data", torch.float32, dim=2)
+    check_tensor(sel, "sparse_selector", torch.uint8, dim=2)
+    if data.shape != sel.shape or data.device != sel.device:
+        raise RuntimeError("input_data and sparse_selector must have the same shape and device")
+    k = data.shape[1]
+    if k < 4 or k > 256 or k & (k - 1):
+        raise RuntimeError("records need k a power of two in [4, 256]")
+    if rows is not None:
+        check_tensor(rows, "rows", torch.int32, dim=1)
+        if rows.device != data.device:
+            raise RuntimeError("rows must be on the CBSR's device")
+        n = rows.numel()
+    else:
+        n = data.shape[0]
+    if out is None:
+        out = torch.empty((n, 5 * k), dtype=torch.uint8, device=data.device)
+    elif not out.is_contiguous() or out.dtype != torch.uint8 or out.numel() != n * 5 * k:
+        raise RuntimeError("out must be a contiguous uint8 tensor of n * 5k bytes")
+    L = _lib.load()
+    _lib.check(L.maxk_cbsr_gather_records(data.data_ptr(), sel.data_ptr(), _lib.ptr(rows), n, k,
+                                          out.data_ptr(), _stream(data)), "maxk_cbsr_gather_records")
+    return out
+
+
+def spgemm_forward_records(g: MaxKGraph, records: torch.Tensor, k: int, dim_origin: int = 256,
+                           out=None, values=None, accumulate: bool = False):
+    """Forward reading the CBSR from halo records (uint8[num_cols, 5k]);
+    accumulate=True adds into out (maxk_spgemm_forward_records)."""
+    check_tensor(records, "records", torch.uint8)
+    if records.numel() != g.num_cols * 5 * k:
+        raise RuntimeError(f"records must hold num_cols = {g.num_cols} records of 5k bytes")
+    _on_device(g, records=records)
+    values = _check_values(g, values)
+    if out is None:
+        if accumulate:
+            raise RuntimeError("accumulate needs an output")
+        out = torch.empty((g.num_rows, dim_origin), dtype=torch.float32, device=g.device)
+    else:
+        check_tensor(out, "output", torch.float32, dim=2)
+        if tuple(out.shape) != (g.num_rows, dim_origin):
+            raise RuntimeError("output has the wrong shape")
+        _on_device(g, output=out)
+    L = _lib.load()
+    nbytes = L.maxk_forward_workspace_bytes(g.num_panels, dim_origin)
+    ws = g._workspace(("fwd", dim_origin), nbytes)
+    flags = _lib.MAXK_FWD_ACCUMULATE if accumulate else 0
+    _lib.check(L.maxk_spgemm_forward_records(
+        g.sched.data_ptr(), g.num_panels, g.indptr.data_ptr(), g.indices.data_ptr(),
+        values.data_ptr(), records.data_ptr(), g.num_rows, dim_origin, k, flags, out.data_ptr(),
+        ws.data_ptr(), ws.numel(), _stream(out)), "maxk_spgemm_forward_records")
     return out
 
 

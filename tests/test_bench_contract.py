@@ -53,3 +53,19 @@ def test_bench_two_ranks_rehearsal():
     assert d["n_gpus"] == 2 and d["config"]["parallelism"] == "rowpart2"
     assert d["value"] > 0 and d["roofline"]["achieved"] > 0
     assert d["config"]["halo_nodes_rank0"] > 0 and d["config"]["overlap"] is True
+
+
+@pytest.mark.gpu
+def test_bench_two_ranks_multi_relation_rehearsal():
+    """Config 5's N>1 path (bench.py --relations R under torch.distributed.run):
+    partitioned fused multi-relation forward + backward, 2 ranks on one GPU, gloo."""
+    env = dict(os.environ, BENCH_BACKEND="gloo")
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
+           "--master-addr", "127.0.0.1", "--master-port", "29617", os.path.join(ROOT, "bench.py"),
+           "--gpus", "2", "--steps", "2", "--warmup", "1", "--graph", "flickr", "--h", "64",
+           "--k", "16", "--relations", "8"]
+    out = subprocess.run(cmd, cwd=ROOT, capture_output=True, text=True, timeout=600, env=env)
+    assert out.returncode == 0, out.stderr[-3000:]
+    d = json.loads(out.stdout.strip().splitlines()[-1])
+    assert d["n_gpus"] == 2 and d["config"]["parallelism"] == "rowpart2"
+    assert d["config"]["relations"] == 8 and d["value"] > 0 and d["bwd_multi_ms"] > 0

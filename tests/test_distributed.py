@@ -31,10 +31,47 @@ class OracleEngine:
         y = self.O.np_forward(self.indptr, self.indices, self.values, data.numpy(), sel.numpy(), dim)
         return torch.from_numpy(y.astype(np.float32))
 
-    def backward(self, grad, sel):
+    def backward(self, grad, sel, values=None):
         assert sel.shape[0] == self.num_cols
-        d = self.O.np_backward(self.indptr, self.indices, self.values, grad.numpy(), sel.numpy())
+        vals = self.values if values is None else values.numpy()
+        d = self.O.np_backward(self.indptr, self.indices, vals, grad.numpy(), sel.numpy())
         return torch.from_numpy(d.astype(np.float32))
+
+    def forward_records(self, records, k, dim, out=None, accumulate=False):
+        assert records.shape == (self.num_cols, 5 * k) and records.dtype == torch.uint8
+        data = records[:, : 4 * k].contiguous().view(torch.float32)
+        y = self.forward(data, records[:, 4 * k:].contiguous(), dim)
+        if out is None:
+            return y
+        if accumulate:
+            out += y
+        else:
+            out.copy_(y)
+        return out
+
+    def forward_multi(self, data, sel, values, dim):
+        ys = []
+        for q in range(values.shape[1]):
+            y = self.O.np_forward(self.indptr, self.indices, values[:, q].numpy(), data.numpy(),
+                                  sel.numpy(), dim)
+            ys.append(torch.from_numpy(y.astype(np.float32)))
+        return torch.stack(ys)
+
+    def backward_multi(self, grad, sel, values):
+        out = None
+        for q in range(values.shape[1]):
+            d = self.backward(grad[q], sel, values[:, q].contiguous())
+            out = d if out is None else out + d
+        return out
+
+
+class RowsOnlyEngine(OracleEngine):
+    """An engine without forward_records: the halo rows are unpacked and concatenated."""
+
+    def __getattribute__(self, name):
+        if name == "forward_records":
+            raise AttributeError(name)
+        return object.__getattribute__(self, name)
 
 
 def _free_port():
@@ -45,23 +82,28 @@ def _free_port():
     return p
 
 
-def _worker(rank, world, port, q, overlap=True):
+def _worker(rank, world, port, q, overlap=True, engine="records", k=8):
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
         from spgemm_new_amd.distributed import PartitionedMaxK
         indptr, indices = small_csr(900, seed=4)
-        v, h, k = len(indptr) - 1, 64, 8
+        v, h = len(indptr) - 1, 64
         values = np.random.default_rng(1).random(len(indices), dtype=np.float32)
         data, sel = random_cbsr(v, k, h, seed=2)
         grad = np.random.default_rng(3).random((v, h), dtype=np.float32)
+        eng = OracleEngine if engine == "records" else RowsOnlyEngine
         m = PartitionedMaxK(torch.from_numpy(indptr), torch.from_numpy(indices),
-                            torch.from_numpy(values), rank, world, "cpu", engine=OracleEngine,
+                            torch.from_numpy(values), rank, world, "cpu", engine=eng,
                             overlap=overlap)
         assert m.overlap == (overlap and m.plan.num_halo > 0)
-        y = m.forward(m.local_rows(torch.from_numpy(data)), m.local_rows(torch.from_numpy(sel)), h)
-        dx = m.backward(m.local_rows(torch.from_numpy(grad)), m.local_rows(torch.from_numpy(sel)))
+        sel_l = m.local_rows(torch.from_numpy(sel))
+        y = m.forward(m.local_rows(torch.from_numpy(data)), sel_l, h)
+        # the forward's selectors are reused; a different tensor is exchanged again
+        dx = m.backward(m.local_rows(torch.from_numpy(grad)), sel_l)
+        dx2 = m.backward(m.local_rows(torch.from_numpy(grad)), sel_l.clone())
+        assert torch.equal(dx, dx2)
         # gather to rank 0
         ys = [None] * world
         dxs = [None] * world
@@ -78,14 +120,20 @@ def _worker(rank, world, port, q, overlap=True):
         dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("world,overlap", [(2, True), (3, True), (2, False), (3, False)])
-def test_partitioned_matches_single(world, overlap):
+@pytest.mark.parametrize("world,overlap,engine,k", [
+    (2, True, "records", 8), (3, True, "records", 8), (2, False, "records", 8),
+    (3, False, "records", 8), (2, True, "rows", 8), (3, False, "rows", 8),
+    (2, True, "records", 5), (3, False, "records", 5)])
+def test_partitioned_matches_single(world, overlap, engine, k):
     """overlap=True splits each block into own | halo column parts and runs the
-    exchange asynchronously; overlap=False is the single-block path."""
+    exchange asynchronously; overlap=False is the single-block path.  The halo
+    travels as records read in place ("records"; k = 5 has none and takes the
+    rows path) or is unpacked into rows ("rows")."""
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, world, port, q, overlap)) for r in range(world)]
+    procs = [ctx.Process(target=_worker, args=(r, world, port, q, overlap, engine, k))
+             for r in range(world)]
     for p in procs:
         p.start()
     for p in procs:
@@ -93,6 +141,55 @@ def test_partitioned_matches_single(world, overlap):
     assert all(p.exitcode == 0 for p in procs), [p.exitcode for p in procs]
     ey, ed, nh, bounds = q.get(timeout=5)
     assert nh > 0 and bounds[0] == 0 and bounds[-1] == 900
+    assert ey <= 1e-5 and ed <= 1e-5, (ey, ed)
+
+
+def _multi_worker(rank, world, port, q, R):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from spgemm_new_amd.distributed import PartitionedMaxK
+        indptr, indices = small_csr(700, seed=9)
+        v, h, k = len(indptr) - 1, 64, 16
+        values = np.random.default_rng(5).random((len(indices), R), dtype=np.float32)
+        data, sel = random_cbsr(v, k, h, seed=6)
+        grad = np.random.default_rng(7).random((R, v, h), dtype=np.float32)
+        m = PartitionedMaxK(torch.from_numpy(indptr), torch.from_numpy(indices),
+                            torch.from_numpy(values), rank, world, "cpu", engine=OracleEngine)
+        sel_l = m.local_rows(torch.from_numpy(sel))
+        y = m.forward_multi(m.local_rows(torch.from_numpy(data)), sel_l, h)
+        r0, r1 = m.bounds[rank], m.bounds[rank + 1]
+        dx = m.backward_multi(torch.from_numpy(grad[:, r0:r1]).contiguous(), sel_l)
+        ys, dxs = [None] * world, [None] * world
+        dist.all_gather_object(ys, y.numpy())
+        dist.all_gather_object(dxs, dx.numpy())
+        if rank == 0:
+            from oracle import oracle as O
+            yr = np.stack([O.np_forward(indptr, indices, values[:, j].copy(), data, sel, h)
+                           for j in range(R)])
+            dr = sum(O.np_backward(indptr, indices, values[:, j].copy(), grad[j], sel)
+                     for j in range(R))
+            q.put((O.parity_error(np.concatenate(ys, axis=1), yr),
+                   O.parity_error(np.concatenate(dxs), dr)))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world,R", [(2, 8), (3, 3)])
+def test_partitioned_multi_relation(world, R):
+    """Config 5 on N ranks: one halo exchange shared by R relations, fused local
+    forward, composed backward with one reverse exchange."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_multi_worker, args=(r, world, port, q, R)) for r in range(world)]
+    for p in procs:
+        p.start()
+    for p in procs:
+        p.join(timeout=240)
+    assert all(p.exitcode == 0 for p in procs), [p.exitcode for p in procs]
+    ey, ed = q.get(timeout=5)
     assert ey <= 1e-5 and ed <= 1e-5, (ey, ed)
 
 
@@ -107,7 +204,7 @@ def test_row_partition_balance():
         assert max(cost) - min(cost) <= int(np.diff(indptr).max()) + 16 + 1
 
 
-def _gpu_worker(rank, world, port, q, overlap=True):
+def _gpu_worker(rank, world, port, q, overlap=True, records=True, R=1):
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
     dist.init_process_group("gloo", rank=rank, world_size=world)
@@ -116,37 +213,59 @@ def _gpu_worker(rank, world, port, q, overlap=True):
         dev = torch.device("cuda:0")
         indptr, indices = small_csr(2500, seed=6)
         v, h, k = len(indptr) - 1, 256, 32
-        values = np.random.default_rng(1).random(len(indices), dtype=np.float32)
+        shape = (len(indices),) if R == 1 else (len(indices), R)
+        values = np.random.default_rng(1).random(shape, dtype=np.float32)
         data, sel = random_cbsr(v, k, h, seed=2)
-        grad = np.random.default_rng(3).random((v, h), dtype=np.float32)
+        gshape = (v, h) if R == 1 else (R, v, h)
+        grad = np.random.default_rng(3).random(gshape, dtype=np.float32)
         m = PartitionedMaxK(torch.from_numpy(indptr).to(dev), torch.from_numpy(indices).to(dev),
                             torch.from_numpy(values).to(dev), rank, world, dev, panel_cost=256,
-                            overlap=overlap)
+                            overlap=overlap, records=records)
         td = lambda a: m.local_rows(torch.from_numpy(a).to(dev))  # noqa: E731
-        y = m.forward(td(data), td(sel), h)
-        dx = m.backward(td(grad), td(sel))
+        r0, r1 = m.bounds[rank], m.bounds[rank + 1]
+        sel_l = td(sel)
+        if R == 1:
+            for _ in range(2):   # the second step reuses the exchange buffers
+                y = m.forward(td(data), sel_l, h)
+                dx = m.backward(td(grad), sel_l)
+        else:
+            y = m.forward_multi(td(data), sel_l, h)
+            dx = m.backward_multi(torch.from_numpy(grad[:, r0:r1]).contiguous().to(dev), sel_l)
         torch.cuda.synchronize()
         ys, dxs = [None] * world, [None] * world
         dist.all_gather_object(ys, y.cpu().numpy())
         dist.all_gather_object(dxs, dx.cpu().numpy())
         if rank == 0:
             from oracle import oracle as O
-            ey = O.parity_error(np.concatenate(ys), O.np_forward(indptr, indices, values, data, sel, h))
-            ed = O.parity_error(np.concatenate(dxs), O.np_backward(indptr, indices, values, grad, sel))
+            if R == 1:
+                yr = O.np_forward(indptr, indices, values, data, sel, h)
+                dr = O.np_backward(indptr, indices, values, grad, sel)
+                ey = O.parity_error(np.concatenate(ys), yr)
+            else:
+                yr = np.stack([O.np_forward(indptr, indices, values[:, j].copy(), data, sel, h)
+                               for j in range(R)])
+                dr = sum(O.np_backward(indptr, indices, values[:, j].copy(), grad[j], sel)
+                         for j in range(R))
+                ey = O.parity_error(np.concatenate(ys, axis=1), yr)
+            ed = O.parity_error(np.concatenate(dxs), dr)
             q.put((ey, ed))
     finally:
         dist.destroy_process_group()
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("overlap", [True, False])
-def test_partitioned_hip_engine_two_ranks_one_gpu(overlap):
-    """2 ranks share cuda:0; HIP kernels on rectangular row blocks with halo columns;
+@pytest.mark.parametrize("overlap,records,R", [(True, True, 1), (False, True, 1),
+                                               (True, False, 1), (False, False, 1),
+                                               (True, True, 8)])
+def test_partitioned_hip_engine_two_ranks_one_gpu(overlap, records, R):
+    """2 ranks share cuda:0; HIP kernels on rectangular row blocks with halo columns
+    (halo records read in place, or unpacked rows; R = 8: the multi-relation path);
     exchange over gloo (staged through host)."""
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_gpu_worker, args=(r, 2, port, q, overlap)) for r in range(2)]
+    procs = [ctx.Process(target=_gpu_worker, args=(r, 2, port, q, overlap, records, R))
+             for r in range(2)]
     for p in procs:
         p.start()
     for p in procs:

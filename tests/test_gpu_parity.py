@@ -741,3 +741,60 @@ def test_spmm_dense_baseline(dev, oracle, h):
                                oracle.np_spmm_dense(indptr, indices, np.ones(len(indices)), x)) <= TOL
     with pytest.raises(RuntimeError, match="dim % 4"):
         g.spmm_dense(T(x[:, :3].copy(), dev))
+
+
+# ------------------------------------------------- halo records (multi-GPU path)
+@pytest.mark.parametrize("k", [4, 8, 16, 32, 64, 128, 256])
+def test_cbsr_gather_records(dev, k):
+    """Records are bit-exact copies: k fp32 values then k selector bytes, 5k B each."""
+    v, h = 700, 256
+    data, sel = random_cbsr(v, k, h, seed=k)
+    rows = np.random.default_rng(k).integers(0, v, 1234).astype(np.int32)
+    rec = S.cbsr_gather_records(T(data, dev), T(sel, dev), T(rows, dev)).cpu().numpy()
+    assert rec.shape == (1234, 5 * k)
+    assert np.array_equal(rec[:, : 4 * k].copy().view(np.float32), data[rows])
+    assert np.array_equal(rec[:, 4 * k:], sel[rows])
+    allrec = S.cbsr_gather_records(T(data, dev), T(sel, dev)).cpu().numpy()
+    assert np.array_equal(allrec[:, 4 * k:], sel)
+
+
+@pytest.mark.parametrize("k,h", [(32, 256), (8, 256), (16, 64), (64, 256), (4, 100), (256, 256)])
+@pytest.mark.parametrize("accumulate", [False, True])
+def test_forward_records(dev, oracle, g_small, k, h, accumulate):
+    """The forward reading halo records in place equals the plain forward; with
+    accumulate it adds onto the output (out += A . X^)."""
+    indptr, indices, values = g_small
+    data, sel = random_cbsr(len(indptr) - 1, k, h, seed=k + 3)
+    g = S.MaxKGraph(T(indptr, dev), T(indices, dev), T(values, dev), panel_cost=300)
+    rec = S.cbsr_gather_records(T(data, dev), T(sel, dev))
+    base = np.random.default_rng(4).random((len(indptr) - 1, h), dtype=np.float32)
+    out = T(base, dev) if accumulate else torch.full((len(indptr) - 1, h), float("nan"), device=dev)
+    g.forward_records(rec, k, h, out=out, accumulate=accumulate)
+    ref = oracle.np_forward(indptr, indices, values, data, sel, h) + (base if accumulate else 0)
+    assert oracle.parity_error(out.cpu().numpy(), ref) <= TOL
+
+
+def test_forward_records_errors(dev, g_small):
+    indptr, indices, values = g_small
+    g = S.MaxKGraph(T(indptr, dev), T(indices, dev), T(values, dev))
+    data, sel = random_cbsr(len(indptr) - 1, 24, 256, seed=1)
+    with pytest.raises(RuntimeError):   # k = 24 has no record layout
+        S.cbsr_gather_records(T(data, dev), T(sel, dev))
+    rec = torch.zeros((len(indptr) - 1, 160), dtype=torch.uint8, device=dev)
+    with pytest.raises(RuntimeError):   # accumulate needs an output
+        g.forward_records(rec, 32, 256, accumulate=True)
+    with pytest.raises(RuntimeError):   # wrong record count
+        g.forward_records(rec[:-1], 32, 256)
+    L = _lib.load()
+    ws = torch.empty(1 << 20, dtype=torch.uint8, device=dev)
+    # unaligned records / unknown flags are refused at the ABI, nothing launched
+    rc = L.maxk_spgemm_forward_records(g.sched.data_ptr(), g.num_panels, g.indptr.data_ptr(),
+                                       g.indices.data_ptr(), g.values.data_ptr(),
+                                       rec.data_ptr() + 4, g.num_rows, 256, 32, 0, ws.data_ptr(),
+                                       ws.data_ptr(), ws.numel(), None)
+    assert rc == _lib.MAXK_E_ARG
+    rc = L.maxk_spgemm_forward_records(g.sched.data_ptr(), g.num_panels, g.indptr.data_ptr(),
+                                       g.indices.data_ptr(), g.values.data_ptr(), rec.data_ptr(),
+                                       g.num_rows, 256, 32, 6, ws.data_ptr(), ws.data_ptr(),
+                                       ws.numel(), None)
+    assert rc == _lib.MAXK_E_ARG

@@ -1,0 +1,116 @@
+#!/usr/bin/env python3
+"""One rank's whole partitioned step (PartitionedMaxK: pack, exchange, forward
+with overlap split, backward, reverse exchange, index_add) at world sizes
+2/4/8 on ONE GPU, with the all-to-all-v replaced by a loopback that delivers
+exactly what the peers would send (computed from the global graph).  Measures
+everything a rank does except the xGMI wire time.  Development tool.
+
+usage: tools/exp_rank_step.py [--graph reddit] [--k 32] [--worlds 1,2,4,8] [--rows]
+"""
+import argparse
+import os
+import sys
+
+import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+import spgemm_new_amd.distributed as D  # noqa: E402
+from spgemm_new_amd.graphs import CONFIGS, synthetic_csr_gpu  # noqa: E402
+from spgemm_new_amd.ops import topk_cbsr  # noqa: E402
+
+
+class Loopback:
+    """Stands in for torch.distributed.all_to_all_single for rank p."""
+
+    def __init__(self, indptr, indices, bounds, p, data, sel):
+        self.data, self.sel, self.k = data, sel, data.shape[1]
+        world = len(bounds) - 1
+        r0, r1 = bounds[p], bounds[p + 1]
+        reqs = []
+        for q in range(world):   # what peer q needs from me: its halo within my range
+            if q == p:
+                reqs.append(torch.empty(0, dtype=torch.int64, device=indices.device))
+                continue
+            e0, e1 = int(indptr[bounds[q]]), int(indptr[bounds[q + 1]])
+            c = indices[e0:e1].long()
+            reqs.append(torch.unique(c[(c >= r0) & (c < r1)]))
+        self.counts = torch.tensor([r.numel() for r in reqs], dtype=torch.int64,
+                                   device=indices.device)
+        self.req = torch.cat(reqs)
+        self.calls = 0
+        self.halo = None
+
+    def __call__(self, out, inp, out_split=None, in_split=None, async_op=False):
+        self.calls += 1
+        if self.calls == 1:                      # HaloPlan: request counts
+            out.copy_(self.counts)
+        elif self.calls == 2:                    # HaloPlan: requested ids
+            out.copy_(self.req)
+            self.halo = inp.clone()              # my halo ids, grouped by owner
+            self.halo32 = self.halo.to(torch.int32)
+        elif out.dtype == torch.uint8 and out.shape[1] == 5 * self.k:   # halo CBSR rows
+            D_ops.cbsr_gather_records(self.data, self.sel, self.halo32, out=out)
+        elif out.dtype == torch.uint8:           # halo selectors only
+            out.copy_(self.sel[self.halo])
+        else:                                    # reverse: partial sums from the peers
+            out.copy_(inp[: out.shape[0]] if inp.shape[0] >= out.shape[0] else
+                      torch.ones_like(out))
+        return D._Done() if async_op else out
+
+
+import spgemm_new_amd.ops as D_ops  # noqa: E402
+
+
+def timed(fn, reps=20):
+    for _ in range(3):
+        fn()
+    torch.cuda.synchronize()
+    a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    a.record()
+    for _ in range(reps):
+        fn()
+    b.record()
+    b.synchronize()
+    return a.elapsed_time(b) / reps
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--graph", default="reddit")
+    ap.add_argument("--k", type=int, default=32)
+    ap.add_argument("--h", type=int, default=256)
+    ap.add_argument("--worlds", default="1,2,4,8")
+    ap.add_argument("--rows", action="store_true", help="unpacked-rows halo path (no records)")
+    a = ap.parse_args()
+    dev = torch.device("cuda:0")
+    V, E = CONFIGS[a.graph]
+    h, k = a.h, a.k
+    indptr, indices = synthetic_csr_gpu(V, E, device=dev)
+    gen = torch.Generator(device=dev)
+    gen.manual_seed(5)
+    values = torch.rand(E, generator=gen, device=dev)
+    X = torch.rand((V, h), generator=gen, device=dev)
+    G = torch.rand((V, h), generator=gen, device=dev)
+    data, sel = topk_cbsr(X, k)
+    for world in [int(w) for w in a.worlds.split(",")]:
+        bounds = D.row_partition(indptr, world)
+        for p in sorted({0, world - 1}):
+            lb = Loopback(indptr, indices, bounds, p, data, sel)
+            D.a2a = lb
+            m = D.PartitionedMaxK(indptr, indices, values, p, world, dev, records=not a.rows)
+            d_l, s_l, g_l = m.local_rows(data), m.local_rows(sel), m.local_rows(G)
+            tf = timed(lambda: m.forward(d_l, s_l, h))
+            tb = timed(lambda: m.backward(g_l, s_l))
+            ts = timed(lambda: (m.forward(d_l, s_l, h), m.backward(g_l, s_l)))
+            pl = m.plan
+            print(f"world={world} rank={p}: own={pl.num_own} halo={pl.num_halo} "
+                  f"send={m.send_rows.numel()} edges={pl.local_indices.numel()} | fwd {tf:.3f} "
+                  f"bwd {tb:.3f} step {ts:.3f} ms (no wire time) | halo fwd "
+                  f"{pl.num_halo * 5 * k / 1e6:.1f} MB in, {m.send_rows.numel() * 5 * k / 1e6:.1f}"
+                  f" MB out; bwd algo {m.local.last_bwd_algo}", flush=True)
+            del m, lb, d_l, s_l, g_l
+            torch.cuda.empty_cache()
+
+
+if __name__ == "__main__":
+    main()
