@@ -10,6 +10,15 @@ and the node labels are synthetic (labels are a function of the features, so
 the loss can fall).
 
     python examples/train_maxk_sage.py --graph reddit --steps 20
+
+Multi-GPU (one process per GPU, RCCL): the graph is 1-D row-partitioned
+(spgemm_new_amd.distributed.PartitionedMaxK), each rank trains on its own rows
+with PartitionedSpGEMMFunction (halo CBSR exchange in the forward, halo partial
+sums back in the backward) and the replicated Linear weights' gradients are
+all-reduced:
+
+    python -m torch.distributed.run --nproc-per-node 8 --master-addr 127.0.0.1 \
+        examples/train_maxk_sage.py --graph reddit --steps 20
 """
 import argparse
 import os
@@ -22,7 +31,7 @@ import torch.nn.functional as F
 
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 from spgemm_new_amd.graphs import CONFIGS, synthetic_csr_gpu  # noqa: E402
-from spgemm_new_amd.models import SpGEMMFunction  # noqa: E402
+from spgemm_new_amd.models import PartitionedSpGEMMFunction, SpGEMMFunction  # noqa: E402
 
 
 class MaxKSAGE(nn.Module):
@@ -37,9 +46,14 @@ class MaxKSAGE(nn.Module):
         self.lin_out = nn.Linear(hid_size, out_size)
 
     def forward(self, graph, x):
+        """graph: the (indptr, indices, values) tuple, or a rank's PartitionedMaxK
+        (x then holds the rank's own rows)."""
         x = self.lin_in(x)
         for fs, fn, norm in zip(self.fc_self, self.fc_neigh, self.norms):
-            x_agg = SpGEMMFunction.apply(x, graph, self.maxk)   # MaxK + SpGEMM (HIP)
+            if isinstance(graph, tuple):
+                x_agg = SpGEMMFunction.apply(x, graph, self.maxk)   # MaxK + SpGEMM (HIP)
+            else:
+                x_agg = PartitionedSpGEMMFunction.apply(x, graph, self.maxk)
             x = norm(self.drop(fs(x) + fn(x_agg)))
         return self.lin_out(x)
 
@@ -55,8 +69,21 @@ def main(argv=None):
     p.add_argument("--classes", type=int, default=41)
     p.add_argument("--steps", type=int, default=20)
     p.add_argument("--lr", type=float, default=1e-2)
+    p.add_argument("--backend", default=os.environ.get("BENCH_BACKEND", "nccl"),
+                   help="torch.distributed backend when WORLD_SIZE > 1 (nccl = RCCL)")
     args = p.parse_args(argv)
-    dev = torch.device("cuda:0")
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    dist = None
+    dev = torch.device("cuda", int(os.environ.get("LOCAL_RANK", "0")) %
+                       max(1, torch.cuda.device_count()))
+    torch.cuda.set_device(dev)
+    if world > 1:
+        import torch.distributed as dist
+        if args.backend == "nccl":
+            dist.init_process_group("nccl", device_id=dev)
+        else:
+            dist.init_process_group(args.backend)
     V, E = CONFIGS[args.graph]
     if args.nodes:
         E, V = int(E * args.nodes / V), args.nodes
@@ -67,25 +94,45 @@ def main(argv=None):
     feats = torch.randn((V, args.feat), generator=gen, device=dev)
     w = torch.randn((args.feat, args.classes), generator=gen, device=dev)
     labels = (feats @ w).argmax(1)                              # learnable synthetic labels
+    torch.manual_seed(0)                                          # same initial weights on every rank
     model = MaxKSAGE(args.feat, args.hidden, args.classes, args.layers, args.maxk).to(dev)
     opt = torch.optim.Adam(model.parameters(), lr=args.lr)
     graph = (indptr, indices, values)
+    if dist is not None:
+        from spgemm_new_amd.distributed import PartitionedMaxK
+        graph = PartitionedMaxK(indptr, indices, values, rank, world, dev)
+        feats, labels = graph.local_rows(feats), graph.local_rows(labels)
     losses, times = [], []
     for step in range(args.steps):
         torch.cuda.synchronize()
         t0 = time.perf_counter()
         opt.zero_grad(set_to_none=True)
-        loss = F.cross_entropy(model(graph, feats), labels)
+        # mean over ALL nodes: each rank sums its own rows' losses, divided by V
+        loss = F.cross_entropy(model(graph, feats), labels, reduction="sum") / V
         loss.backward()
+        if dist is not None:   # replicated weights: sum the ranks' gradients
+            grads = [q.grad for q in model.parameters() if q.grad is not None]
+            flat = torch.cat([g.reshape(-1) for g in grads])
+            dist.all_reduce(flat)
+            off = 0
+            for g in grads:
+                g.copy_(flat[off:off + g.numel()].view_as(g))
+                off += g.numel()
+            loss = loss.detach().clone()
+            dist.all_reduce(loss)
         opt.step()
         torch.cuda.synchronize()
         times.append(time.perf_counter() - t0)
         losses.append(float(loss))
-        print(f"step {step:3d}  loss {losses[-1]:.4f}  {times[-1] * 1e3:.1f} ms", flush=True)
+        if rank == 0:
+            print(f"step {step:3d}  loss {losses[-1]:.4f}  {times[-1] * 1e3:.1f} ms", flush=True)
     steady = times[2:] or times
-    print(f"{args.graph}: V={V} E={indices.numel()} layers={args.layers} hidden={args.hidden} "
-          f"k={args.maxk}: {sum(steady) / len(steady) * 1e3:.1f} ms/step, "
-          f"loss {losses[0]:.3f} -> {losses[-1]:.3f}")
+    if rank == 0:
+        print(f"{args.graph}: V={V} E={indices.numel()} layers={args.layers} hidden={args.hidden} "
+              f"k={args.maxk} gpus={world}: {sum(steady) / len(steady) * 1e3:.1f} ms/step, "
+              f"loss {losses[0]:.3f} -> {losses[-1]:.3f}")
+    if dist is not None:
+        dist.destroy_process_group()
     return losses
 
 

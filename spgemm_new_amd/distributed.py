@@ -262,10 +262,21 @@ class PartitionedMaxK:
         y += self.local_halo.forward(h_data, h_sel.contiguous(), dim_origin)
         return y
 
-    def _block_sel(self, sel_own: torch.Tensor | None) -> torch.Tensor:
+    def last_halo_selectors(self) -> torch.Tensor:
+        """The halo nodes' selectors received by the last forward (a copy: the
+        exchange buffers are reused by the next forward)."""
+        if self._halo_part is None:
+            raise RuntimeError("no forward has run")
+        return self._halo_part.contiguous().clone()
+
+    def _block_sel(self, sel_own: torch.Tensor | None, halo_sel=None) -> torch.Tensor:
         """Selectors of the whole block (own + halo columns), contiguous."""
         p = self.plan
-        if sel_own is None or sel_own is self._fwd_sel:
+        if halo_sel is not None:
+            if sel_own is None:
+                raise RuntimeError("halo_sel needs sel_own")
+            halo = halo_sel
+        elif sel_own is None or sel_own is self._fwd_sel:
             if self._halo_part is None:
                 raise RuntimeError("backward needs the forward's selectors (call forward first)")
             sel_own, halo = self._fwd_sel, self._halo_part
@@ -286,8 +297,12 @@ class PartitionedMaxK:
         own.index_add_(0, p.send_local, back)
         return own
 
-    def backward(self, grad_own: torch.Tensor, sel_own: torch.Tensor | None = None):
-        return self._return_halo(self.local.backward(grad_own, self._block_sel(sel_own)))
+    def backward(self, grad_own: torch.Tensor, sel_own: torch.Tensor | None = None,
+                 halo_sel: torch.Tensor | None = None):
+        """dXs of the own nodes.  The block's selectors: sel_own + halo_sel when
+        given (last_halo_selectors() of that forward), else the last forward's
+        when sel_own is its tensor (or None), else exchanged again."""
+        return self._return_halo(self.local.backward(grad_own, self._block_sel(sel_own, halo_sel)))
 
     # ------------------------------------------------- multi-relation (config 5)
     def forward_multi(self, data_own: torch.Tensor, sel_own: torch.Tensor,

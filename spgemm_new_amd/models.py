@@ -95,3 +95,32 @@ class SpGEMMMultiFunction(Function):
         g, sel = ctx.graph, ctx.sparse_selector
         dxs = g.backward_multi(grad_output.contiguous(), sel, ctx.values)
         return cbsr_scatter(dxs, sel, ctx.features_shape[1]), None, None, None
+
+
+class PartitionedSpGEMMFunction(Function):
+    """SpGEMMFunction for one rank of a 1-D row-partitioned graph
+    (spgemm_new_amd.distributed.PartitionedMaxK): the rank holds
+    its own rows' features; forward = top-k of the own rows, halo exchange of
+    their CBSR, local SpGEMM -> Y for the own rows; backward = local SSpMM,
+    reverse exchange of the halo partial sums, dense scatter of the own rows'
+    dXs.  Every rank calls it in the same order (the exchanges are collective).
+
+        y_own = PartitionedSpGEMMFunction.apply(x_own, model, maxk)
+    """
+
+    @staticmethod
+    def forward(ctx, features_own, model, maxk):
+        if features_own.dim() != 2 or features_own.shape[0] != model.plan.num_own:
+            raise RuntimeError("features must be the rank's own rows [num_own, h]")
+        x = features_own.contiguous()
+        data, sel = topk_cbsr(x, maxk, order="column")
+        out = model.forward(data, sel, x.size(1))
+        # the halo selectors of THIS forward (a later layer's forward reuses the buffers)
+        ctx.model, ctx.sel, ctx.h = model, sel, x.size(1)
+        ctx.halo_sel = model.last_halo_selectors()
+        return out
+
+    @staticmethod
+    def backward(ctx, grad_output):
+        dxs = ctx.model.backward(grad_output.contiguous(), ctx.sel, halo_sel=ctx.halo_sel)
+        return cbsr_scatter(dxs, ctx.sel, ctx.h), None, None

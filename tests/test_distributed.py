@@ -273,3 +273,65 @@ def test_partitioned_hip_engine_two_ranks_one_gpu(overlap, records, R):
     assert all(p.exitcode == 0 for p in procs), [p.exitcode for p in procs]
     ey, ed = q.get(timeout=5)
     assert ey <= 1e-4 and ed <= 1e-4, (ey, ed)
+
+
+def _autograd_worker(rank, world, port, q):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from spgemm_new_amd.distributed import PartitionedMaxK
+        from spgemm_new_amd.models import PartitionedSpGEMMFunction
+        dev = torch.device("cuda:0")
+        indptr, indices = small_csr(1200, seed=12)
+        v, h, k = len(indptr) - 1, 64, 8
+        values = np.random.default_rng(2).random(len(indices), dtype=np.float32)
+        x = np.random.default_rng(3).random((v, h), dtype=np.float32)
+        G = np.random.default_rng(4).random((v, h), dtype=np.float32)
+        m = PartitionedMaxK(torch.from_numpy(indptr).to(dev), torch.from_numpy(indices).to(dev),
+                            torch.from_numpy(values).to(dev), rank, world, dev, panel_cost=128)
+        xo = m.local_rows(torch.from_numpy(x).to(dev)).requires_grad_(True)
+        # two layers through one partitioned graph: the second forward reuses the
+        # exchange buffers before the first layer's backward runs
+        y1 = PartitionedSpGEMMFunction.apply(xo, m, k)
+        y2 = PartitionedSpGEMMFunction.apply(0.5 * y1 + xo, m, k)
+        (y2 * m.local_rows(torch.from_numpy(G).to(dev))).sum().backward()
+        torch.cuda.synchronize()
+        ys, gs = [None] * world, [None] * world
+        dist.all_gather_object(ys, y2.detach().cpu().numpy())
+        dist.all_gather_object(gs, xo.grad.cpu().numpy())
+        if rank == 0:
+            q.put((np.concatenate(ys), np.concatenate(gs)))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.gpu
+def test_partitioned_autograd_two_layers():
+    """PartitionedSpGEMMFunction (2 ranks on cuda:0, gloo) through two layers
+    equals SpGEMMFunction on the whole graph: outputs and input gradients."""
+    from spgemm_new_amd.models import SpGEMMFunction
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_autograd_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    # read before joining: rank 0 cannot exit until its (large) result has left the queue
+    y_part, g_part = q.get(timeout=300)
+    for p in procs:
+        p.join(timeout=300)
+    assert all(p.exitcode == 0 for p in procs), [p.exitcode for p in procs]
+    dev = torch.device("cuda:0")
+    indptr, indices = small_csr(1200, seed=12)
+    v, h, k = len(indptr) - 1, 64, 8
+    values = np.random.default_rng(2).random(len(indices), dtype=np.float32)
+    x = torch.from_numpy(np.random.default_rng(3).random((v, h), dtype=np.float32)).to(dev)
+    G = torch.from_numpy(np.random.default_rng(4).random((v, h), dtype=np.float32)).to(dev)
+    graph = tuple(torch.from_numpy(a).to(dev) for a in (indptr, indices, values))
+    xg = x.clone().requires_grad_(True)
+    y2 = SpGEMMFunction.apply(0.5 * SpGEMMFunction.apply(xg, graph, k) + xg, graph, k)
+    (y2 * G).sum().backward()
+    ey = np.abs(y_part - y2.detach().cpu().numpy()) / np.maximum(1, np.abs(y2.detach().cpu().numpy()))
+    eg = np.abs(g_part - xg.grad.cpu().numpy()) / np.maximum(1, np.abs(xg.grad.cpu().numpy()))
+    assert ey.max() <= 1e-4 and eg.max() <= 1e-4, (ey.max(), eg.max())

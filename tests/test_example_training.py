@@ -17,3 +17,20 @@ def test_training_loss_falls():
                                    "--feat", "50", "--classes", "7"])
     assert all(l == l for l in losses)                  # finite
     assert min(losses[-5:]) < 0.8 * losses[0], losses
+
+
+@pytest.mark.gpu
+def test_training_two_ranks_rehearsal():
+    """The example's multi-GPU mode (torch.distributed.run, PartitionedSpGEMMFunction,
+    gradient all-reduce) with 2 ranks on one GPU; gloo stands in for RCCL."""
+    import subprocess
+    env = dict(os.environ, BENCH_BACKEND="gloo")
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
+           "--master-addr", "127.0.0.1", "--master-port", "29621",
+           os.path.join(ROOT, "examples", "train_maxk_sage.py"), "--graph", "flickr",
+           "--nodes", "4000", "--steps", "30", "--hidden", "64", "--maxk", "16", "--layers", "2",
+           "--feat", "50", "--classes", "7"]
+    out = subprocess.run(cmd, cwd=ROOT, capture_output=True, text=True, timeout=600, env=env)
+    assert out.returncode == 0, out.stderr[-3000:]
+    losses = [float(l.split()[3]) for l in out.stdout.splitlines() if l.startswith("step")]
+    assert len(losses) == 30 and min(losses[-5:]) < 0.8 * losses[0], losses
