@@ -1271,6 +1271,9 @@ __global__ __launch_bounds__(kBlock) void bwd_warp4_kernel(
 #ifndef LOCAL_U
 #define LOCAL_U 8
 #endif
+#ifndef LOCAL_ABLATE
+#define LOCAL_ABLATE 0
+#endif
 #ifndef LOCAL_R
 #define LOCAL_R 16  // edge records per SGPR round (k = 32, 64)
 #endif
@@ -1353,7 +1356,13 @@ __device__ __forceinline__ void local_issue(const int32_t *__restrict__ rec_rc,
     rd.clash = clash;
     // selector bytes for all groups, then all gathers back to back
 #pragma unroll
-    for (int u = 0; u < NG; ++u) col[u] = sl[rd.ai[u]];
+    for (int u = 0; u < NG; ++u) {
+#if LOCAL_ABLATE & 2  // development ablation: computed column instead of the LDS selector
+        col[u] = (uint32_t)((l * 8 + rd.ai[u]) & 255);
+#else
+        col[u] = sl[rd.ai[u]];
+#endif
+    }
 #pragma unroll
     for (int u = 0; u < NG; ++u) rd.gv[u] = *g_at<WIDE>(grad, ro[u], col[u]);
 }
@@ -1363,6 +1372,13 @@ __device__ __forceinline__ void local_commit(const LocalRound<K> &rd, float *acc
 {
     constexpr int EPS = kWave / K;
     constexpr int NG = LocalRound<K>::NG;
+#if LOCAL_ABLATE & 1  // development ablation: no LDS update (sum kept in a register)
+    float t = 0.f;
+#pragma unroll
+    for (int u = 0; u < NG; ++u) t = fmaf(rd.vv[u], rd.gv[u], t);
+    if (t == 12345.f) acc[rd.ai[0]] = t;
+    return;
+#endif
 #pragma unroll
     for (int u = 0; u < NG; ++u) {
         if (!((rd.clash >> u) & 1u)) {
