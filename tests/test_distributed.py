@@ -123,7 +123,7 @@ def _worker(rank, world, port, q, overlap=True, engine="records", k=8):
 @pytest.mark.parametrize("world,overlap,engine,k", [
     (2, True, "records", 8), (3, True, "records", 8), (2, False, "records", 8),
     (3, False, "records", 8), (2, True, "rows", 8), (3, False, "rows", 8),
-    (2, True, "records", 5), (3, False, "records", 5)])
+    (2, True, "records", 5), (3, False, "records", 5), (8, True, "records", 8)])
 def test_partitioned_matches_single(world, overlap, engine, k):
     """overlap=True splits each block into own | halo column parts and runs the
     exchange asynchronously; overlap=False is the single-block path.  The halo
