@@ -1537,6 +1537,54 @@ __global__ __launch_bounds__(kBlock) void bwd_local_kernel(
     for (int i = lane; i < nent; i += kWave) dst[i] = srow[i] < dim ? acc[i] : 0.f;
 }
 
+// Bank-aware CBSR order for the fused multi-relation forward (relation-vector
+// kernel: lane = entry j + 32 * relation quad, accumulator word col * S + 4 *
+// quad with S / 4 odd).  Its ds_write_b128 goes in groups of 8 contiguous
+// lanes = 8 consecutive entries, bank = 16-B unit mod 8 (MI355X_MICROARCH.md
+// §LDS), so a group is conflict-free iff its 8 columns differ mod 8.  Rows are
+// ordered by (occurrence of the column's residue mod 8, residue): the first 8
+// entries take one column of each residue present, and so on.  Measured on
+// proteins R=8: LDS bank-conflict cycles -19 %, forward 5.43 -> 5.23 ms; a
+// pattern that also spreads the ds_read_b128 16-lane groups over residues mod
+// 16 measured the same (random rows rarely have two columns per class).  Any
+// entry order is a valid CBSR and the forward's result is bit-identical.
+// One wave per row, k <= 64.
+__global__ __launch_bounds__(kBlock) void cbsr_bank_order_kernel(const float *__restrict__ data,
+                                                                 const uint8_t *__restrict__ sel,
+                                                                 int num_rows, int k,
+                                                                 float *__restrict__ odata,
+                                                                 uint8_t *__restrict__ osel)
+{
+    const int lane = lane_id();
+    const int64_t nwaves = (int64_t)gridDim.x * kWavesPerBlock;
+    const uint64_t below = (1ull << lane) - 1ull;
+    for (int64_t r = (int64_t)blockIdx.x * kWavesPerBlock + threadIdx.x / kWave; r < num_rows;
+         r += nwaves) {
+        const bool on = lane < k;
+        const int c = on ? sel[r * k + lane] : 0;
+        const float d = on ? data[r * k + lane] : 0.f;
+        const int res = c & 7;
+        uint64_t mine = 0;
+        int cnt[8];
+#pragma unroll
+        for (int q = 0; q < 8; ++q) {
+            const uint64_t m = __ballot(on && res == q);
+            cnt[q] = __builtin_popcountll(m);
+            if (q == res) mine = m;
+        }
+        const int occ = __builtin_popcountll(mine & below);
+        // entries before this one: all of occurrence < occ, plus occurrence ==
+        // occ of a smaller residue
+        int pos = 0;
+#pragma unroll
+        for (int q = 0; q < 8; ++q) pos += (cnt[q] < occ ? cnt[q] : occ) + (q < res && cnt[q] > occ);
+        if (on) {
+            odata[r * k + pos] = d;
+            osel[r * k + pos] = (uint8_t)c;
+        }
+    }
+}
+
 template <int K>
 __global__ __launch_bounds__(kBlock) void cbsr_pack_kernel(const float *__restrict__ data,
                                                            const uint8_t *__restrict__ sel,
@@ -2053,6 +2101,20 @@ int maxk_spgemm_forward_records(const int32_t *sched, int64_t num_panels, const 
                                   static_cast<const uint8_t *>(records), num_rows, dim_origin,
                                   dim_k, (flags & MAXK_FWD_ACCUMULATE) != 0, out, carry, carry_row,
                                   as_stream(stream));
+}
+
+int maxk_cbsr_bank_order(const float *cbsr_data, const uint8_t *cbsr_sel, int num_rows,
+                         int dim_k, float *out_data, uint8_t *out_sel, void *stream)
+{
+    if (dim_k < 1 || dim_k > kWave) return MAXK_E_DIM;
+    if (num_rows < 0 || (num_rows > 0 && (!cbsr_data || !cbsr_sel || !out_data || !out_sel)))
+        return MAXK_E_ARG;
+    if (num_rows == 0) return MAXK_OK;
+    const int64_t blocks = ceil_div(num_rows, kWavesPerBlock);
+    hipLaunchKernelGGL(cbsr_bank_order_kernel, dim3((unsigned)(blocks < 4096 ? blocks : 4096)),
+                       dim3(kBlock), 0, as_stream(stream), cbsr_data, cbsr_sel, num_rows, dim_k,
+                       out_data, out_sel);
+    return launch_status();
 }
 
 size_t maxk_forward_multi_workspace_bytes(int64_t num_panels, int dim_origin, int num_rel)

@@ -63,6 +63,8 @@ LOCAL_WAVES_PER_CU = int(os.environ.get("MAXK_LOCAL_WAVES_PER_CU", 16))
 LOCAL_BAND_BYTES = int(os.environ.get("MAXK_LOCAL_BAND_BYTES", 32 << 20))
 # forward at k in {4, 8, 16}: pack CBSR into one record per node (MAXK_FWD_PACKED=0 disables)
 FWD_PACKED = os.environ.get("MAXK_FWD_PACKED", "1") != "0"
+# fused multi-relation forward: reorder CBSR entries against LDS store conflicts
+MULTI_BANK_ORDER = os.environ.get("MAXK_MULTI_BANK_ORDER", "1") != "0"
 
 
 def _build_schedule(indptr: torch.Tensor, num_rows: int, num_edges: int, panel_cost: int,
@@ -521,6 +523,16 @@ def spgemm_forward_multi(g: MaxKGraph, data, sel, values, dim_origin: int = 256,
         _on_device(g, output=out)
     vals = values if g.num_edges > 0 else torch.zeros((1, R), device=g.device)
     L = _lib.load()
+    if MULTI_BANK_ORDER and R % 4 == 0 and k % 8 == 0 and k <= 64:
+        # bank-aware entry order for the relation-vector kernel's LDS stores
+        # (same CBSR set, bit-identical result)
+        od = g._workspace(("bank_data", k), g.num_cols * k * 4).view(torch.float32)
+        os_ = g._workspace(("bank_sel", k), g.num_cols * k)
+        od, os_ = od[: g.num_cols * k].view(g.num_cols, k), os_[: g.num_cols * k].view(g.num_cols, k)
+        _lib.check(L.maxk_cbsr_bank_order(data.data_ptr(), sel.data_ptr(), g.num_cols, k,
+                                          od.data_ptr(), os_.data_ptr(), _stream(out)),
+                   "maxk_cbsr_bank_order")
+        data, sel = od, os_
     nbytes = L.maxk_forward_multi_workspace_bytes(g.num_panels, dim_origin, R)
     ws = g._workspace(("fwd_multi", dim_origin, R), nbytes)
     _lib.check(L.maxk_spgemm_forward_multi(

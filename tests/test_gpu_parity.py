@@ -798,3 +798,52 @@ def test_forward_records_errors(dev, g_small):
                                        g.num_rows, 256, 32, 6, ws.data_ptr(), ws.data_ptr(),
                                        ws.numel(), None)
     assert rc == _lib.MAXK_E_ARG
+
+
+def _lds_conflicts(cols):
+    """Extra LDS cycles of the relation-vector kernel's accesses for one row's entry
+    order: ds_write_b128 groups of 8 contiguous entries (bank unit = col mod 8) and
+    ds_read_b128 16-lane groups (col mod 16) -- S / 4 is odd, so col residues decide."""
+    cols = np.asarray(cols, dtype=int)
+    extra = 0
+    for g0 in range(0, len(cols) - len(cols) % 8, 8):
+        extra += np.bincount(cols[g0:g0 + 8] % 8, minlength=8).max() - 1
+    rg = [list(range(0, 4)) + list(range(12, 16)) + list(range(20, 28)),
+          list(range(4, 12)) + list(range(16, 20)) + list(range(28, 32))]
+    for b in range(0, len(cols) - len(cols) % 32, 32):
+        for g in rg:
+            extra += np.bincount(cols[[b + i for i in g]] % 16, minlength=16).max() - 1
+    return extra
+
+
+@pytest.mark.parametrize("k", [8, 16, 32, 64, 5])
+def test_cbsr_bank_order(dev, k):
+    """maxk_cbsr_bank_order permutes each row's (value, column) pairs (same set) and
+    lowers the LDS conflicts of the fused multi-relation forward's accesses; a row
+    with four columns per residue mod 8 (k = 32) has conflict-free store groups."""
+    v, h = 500, 256
+    data, sel = random_cbsr(v, k, h, seed=k)
+    if k == 32:   # a few rows balanced mod 8
+        for r in range(0, 40):
+            rng = np.random.default_rng(r)
+            sel[r] = np.array([q + 8 * b for q in range(8)
+                               for b in rng.choice(32, 4, replace=False)], dtype=np.uint8)
+    L = _lib.load()
+    od = torch.empty((v, k), device=dev)
+    os_ = torch.empty((v, k), dtype=torch.uint8, device=dev)
+    td, ts = T(data, dev), T(sel, dev)   # held: the call reads them asynchronously
+    _lib.check(L.maxk_cbsr_bank_order(td.data_ptr(), ts.data_ptr(), v, k, od.data_ptr(),
+                                      os_.data_ptr(), None), "bank_order")
+    torch.cuda.synchronize()
+    od, os_ = od.cpu().numpy(), os_.cpu().numpy()
+    before = after = 0
+    for r in range(v):
+        assert sorted(zip(os_[r], od[r])) == sorted(zip(sel[r], data[r]))
+        before += _lds_conflicts(np.sort(sel[r]))
+        after += _lds_conflicts(os_[r])
+        if k == 32 and r < 40:
+            for g0 in range(0, 32, 8):
+                assert len(set(os_[r][g0:g0 + 8] % 8)) == 8
+    assert after <= before, (before, after)
+    if k >= 16:   # (k = 8: one store group, its set of columns is fixed)
+        assert after < before, (before, after)
