@@ -423,8 +423,13 @@ __global__ __launch_bounds__(kBlock) void fwd_panel_kernel(
     }
 }
 
-// Adds each panel's carry row(s) into the output (after the owner stored it):
-// nrel relations, carry rows carry_stride apart, output relations rel_stride apart.
+// Adds the panels' carry rows into the output (after the owners stored their
+// rows): nrel relations, carry rows carry_stride apart, output relations
+// rel_stride apart.  The carries of one row come from consecutive panels (a
+// row split by merge-path spans panels w1..w2, w2 its owner), so the wave of
+// the first such panel sums them all and updates the row with a plain
+// read-add-store -- every row has one writer, no atomics (the atomic form
+// cost ~2x: 64-B memory-side atomic requests).
 __global__ __launch_bounds__(kBlock) void carry_fixup_kernel(
     int64_t num_panels, const float *__restrict__ carry, const int32_t *__restrict__ carry_row,
     float *__restrict__ out, int dim, int carry_stride, int nrel = 1, size_t rel_stride = 0)
@@ -432,11 +437,16 @@ __global__ __launch_bounds__(kBlock) void carry_fixup_kernel(
     const int64_t w = (int64_t)blockIdx.x * kWavesPerBlock + threadIdx.x / kWave;
     if (w >= num_panels) return;
     const int r = carry_row[w];
-    if (r < 0) return;
+    if (r < 0 || (w > 0 && carry_row[w - 1] == r)) return;
+    int64_t w_end = w + 1;
+    while (w_end < num_panels && carry_row[w_end] == r) ++w_end;
     for (int q = 0; q < nrel; ++q) {
-        const float *src = carry + ((size_t)w * nrel + q) * carry_stride;
         float *dst = out + q * rel_stride + (size_t)r * dim;
-        for (int c = lane_id(); c < dim; c += kWave) gbl_add(dst + c, src[c]);
+        for (int c = lane_id(); c < dim; c += kWave) {
+            float a = dst[c];
+            for (int64_t v = w; v < w_end; ++v) a += carry[((size_t)v * nrel + q) * carry_stride + c];
+            dst[c] = a;
+        }
     }
 }
 

@@ -847,3 +847,19 @@ def test_cbsr_bank_order(dev, k):
     assert after <= before, (before, after)
     if k >= 16:   # (k = 8: one store group, its set of columns is fixed)
         assert after < before, (before, after)
+
+
+@pytest.mark.parametrize("algo", [_lib.MAXK_BWD_STAGED, _lib.MAXK_BWD_LOCAL])
+def test_bitwise_deterministic(dev, g_small, algo):
+    """No atomics on the forward, STAGED or LOCAL paths (a split row's carries are
+    summed in panel order by one wave): repeated calls are bitwise identical,
+    with rows split over many small panels."""
+    indptr, indices, values = g_small
+    data, sel = random_cbsr(len(indptr) - 1, 32, 256, seed=11)
+    grad = np.random.default_rng(12).random((len(indptr) - 1, 256), dtype=np.float32)
+    g = S.MaxKGraph(T(indptr, dev), T(indices, dev), T(values, dev), panel_cost=40)
+    d, s_, G = T(data, dev), T(sel, dev), T(grad, dev)
+    ys = [g.forward(d, s_, 256).cpu() for _ in range(3)]
+    dxs = [g.backward(G, s_, algo=algo).cpu() for _ in range(3)]
+    assert all(torch.equal(ys[0], y) for y in ys[1:])
+    assert all(torch.equal(dxs[0], x) for x in dxs[1:])
