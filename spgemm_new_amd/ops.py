@@ -12,7 +12,8 @@ need that the reference kept in files or rebuilt per call:
 * cached workspaces (carry rows, staging rows, packed CBSR records).
 
 Also here: the CBSR producer (top-k), the dense gradient scatter / MaxK mask,
-and the fused multi-relation forward.
+the fused multi-relation forward, and the halo records of the multi-GPU path
+(packed CBSR rows read in place, accumulating forward).
 
 All compute goes through the C ABI (``_lib``); there is no CPU or PyTorch
 fallback for the kernels.  The plans (panel schedules, CSC transpose, LOCAL
@@ -28,8 +29,8 @@ import torch
 from . import _lib
 
 __all__ = ["MaxKGraph", "check_tensor", "spgemm_forward", "spgemm_forward_multi",
-           "sspmm_backward", "spmm_dense", "warp4_build",
-           "topk_cbsr", "cbsr_scatter", "cbsr_mask"]
+           "spgemm_forward_records", "cbsr_gather_records", "sspmm_backward", "spmm_dense",
+           "warp4_build", "topk_cbsr", "cbsr_scatter", "cbsr_mask"]
 
 
 def check_tensor(t, name: str, dtype=None, cuda: bool = True, dim: int | None = None):
