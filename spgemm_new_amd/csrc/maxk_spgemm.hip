@@ -388,7 +388,8 @@ __global__ __launch_bounds__(kBlock) void fwd_panel_kernel(
     const int2 *__restrict__ sched, int64_t num_panels, const int32_t *__restrict__ indptr,
     const int32_t *__restrict__ idx, const float *__restrict__ val,
     const float *__restrict__ data, const uint8_t *__restrict__ sel, int num_rows, int dim,
-    int k, float *__restrict__ out, float *__restrict__ carry, int32_t *__restrict__ carry_row)
+    int k, float *__restrict__ out, float *__restrict__ carry, int32_t *__restrict__ carry_row,
+    float *__restrict__ owner)
 {
     extern __shared__ __attribute__((aligned(16))) float lds[];
     const int dimp = (dim + 3) & ~3;
@@ -401,10 +402,17 @@ __global__ __launch_bounds__(kBlock) void fwd_panel_kernel(
     const int2 a = sched[w], b = sched[w + 1];
     const int i0 = a.x, j0 = a.y, i1 = b.x, j1 = b.y;
     int e = j0;
+    // a first row that began in an earlier panel is split: its part goes to
+    // this panel's owner slot, and carry_fixup_owner_kernel adds the parts up
+    // in panel order (one writer per row, no atomics, bitwise deterministic)
+    const bool split_first = i0 < i1 && j0 > indptr[i0];
     for (int r = i0; r < i1; ++r) {
         const int re = indptr[r + 1];
         if (e < re) fwd_edges<K, RS>(e, re, k, idx, val, data, sel, acc);
-        flush_row<ACC ? kAdd : kStore>(acc, copies, out + (size_t)r * dim, dim);
+        if (r == i0 && split_first)
+            flush_row<kStore>(acc, copies, owner + (size_t)w * dimp, dim);
+        else
+            flush_row<ACC ? kAdd : kStore>(acc, copies, out + (size_t)r * dim, dim);
         e = re;
     }
     int has_carry = 0;
@@ -446,6 +454,45 @@ __global__ __launch_bounds__(kBlock) void carry_fixup_kernel(
             float a = dst[c];
             for (int64_t v = w; v < w_end; ++v) a += carry[((size_t)v * nrel + q) * carry_stride + c];
             dst[c] = a;
+        }
+    }
+}
+
+// Forward fixup: row r split over panels w .. w_end (carries of w .. w_end-1,
+// the owner's part in owner slot w_end) is summed in panel order by the wave
+// of its first panel and stored (ACC: added) -- the output row is not read
+// unless accumulating.
+// The carrying panels are consecutive; between the last of them and the
+// owner (the first panel whose end lies past row r) there can be empty panels
+// (panel_cost < row_cost: boundaries inside a row's end cost), which carry
+// nothing and have no owner slot.
+template <bool ACC>
+__global__ __launch_bounds__(kBlock) void carry_fixup_owner_kernel(
+    const int2 *__restrict__ sched, int64_t num_panels, const float *__restrict__ carry,
+    const float *__restrict__ owner, const int32_t *__restrict__ carry_row,
+    float *__restrict__ out, int dim, int dimp)
+{
+    const int64_t w = (int64_t)blockIdx.x * kWavesPerBlock + threadIdx.x / kWave;
+    if (w >= num_panels) return;
+    const int r = carry_row[w];
+    if (r < 0 || (w > 0 && carry_row[w - 1] == r)) return;
+    int64_t w_end = w + 1;
+    while (w_end < num_panels && carry_row[w_end] == r) ++w_end;
+    int64_t own = w_end;
+    while (sched[own + 1].x <= r) ++own;   // the panel that owns row r (exists: r < num_rows)
+    float *dst = out + (size_t)r * dim;
+    if ((dim & 3) == 0) {
+        for (int c4 = lane_id(); c4 < (dim >> 2); c4 += kWave) {
+            f4 a = reinterpret_cast<const f4 *>(owner + (size_t)own * dimp)[c4];
+            for (int64_t v = w; v < w_end; ++v) a += reinterpret_cast<const f4 *>(carry + (size_t)v * dimp)[c4];
+            if (ACC) a += reinterpret_cast<const f4 *>(dst)[c4];
+            __builtin_nontemporal_store(a, reinterpret_cast<f4 *>(dst) + c4);
+        }
+    } else {
+        for (int c = lane_id(); c < dim; c += kWave) {
+            float a = owner[(size_t)own * dimp + c];
+            for (int64_t v = w; v < w_end; ++v) a += carry[(size_t)v * dimp + c];
+            dst[c] = ACC ? dst[c] + a : a;
         }
     }
 }
@@ -1692,21 +1739,34 @@ size_t row_lds_bytes() { return (size_t)kWavesPerBlock * kMaxDim * sizeof(float)
 template <int K>
 size_t fwd_lds_bytes(int k) { return (size_t)kWavesPerBlock * fwd_copies<K>(k) * kMaxDim * sizeof(float); }
 
+inline int fwd_fixup(const int32_t *sched, int64_t P, const float *carry, const float *owner,
+                     const int32_t *carry_row, float *out, int dim, bool acc, hipStream_t st)
+{
+    const int64_t blocks = ceil_div(P, kWavesPerBlock);
+    const int dimp = (dim + 3) & ~3;
+    const int2 *sc = reinterpret_cast<const int2 *>(sched);
+    if (acc)
+        hipLaunchKernelGGL(carry_fixup_owner_kernel<true>, dim3((unsigned)blocks), dim3(kBlock), 0,
+                           st, sc, P, carry, owner, carry_row, out, dim, dimp);
+    else
+        hipLaunchKernelGGL(carry_fixup_owner_kernel<false>, dim3((unsigned)blocks), dim3(kBlock), 0,
+                           st, sc, P, carry, owner, carry_row, out, dim, dimp);
+    return launch_status();
+}
+
 template <int K>
 struct FwdPanel {
     static int run(const int32_t *sched, int64_t P, const int32_t *indptr, const int32_t *idx,
                    const float *val, const float *data, const uint8_t *sel, int V, int dim, int k,
-                   float *out, float *carry, int32_t *carry_row, hipStream_t st)
+                   float *out, float *carry, int32_t *carry_row, float *owner, hipStream_t st)
     {
         const int64_t blocks = ceil_div(P, kWavesPerBlock);
         hipLaunchKernelGGL(fwd_panel_kernel<K>, dim3((unsigned)blocks), dim3(kBlock),
                            fwd_lds_bytes<K>(k), st, reinterpret_cast<const int2 *>(sched), P,
-                           indptr, idx, val, data, sel, V, dim, k, out, carry, carry_row);
+                           indptr, idx, val, data, sel, V, dim, k, out, carry, carry_row, owner);
         int rc = launch_status();
         if (rc) return rc;
-        hipLaunchKernelGGL(carry_fixup_kernel, dim3((unsigned)blocks), dim3(kBlock), 0, st, P,
-                           carry, carry_row, out, dim, (dim + 3) & ~3);
-        return launch_status();
+        return fwd_fixup(sched, P, carry, owner, carry_row, out, dim, false, st);
     }
 };
 
@@ -1714,7 +1774,7 @@ template <int K>
 struct FwdPanelPacked {
     static int run(const int32_t *sched, int64_t P, const int32_t *indptr, const int32_t *idx,
                    const float *val, const uint8_t *rec, int V, int dim, int k, float *out,
-                   float *carry, int32_t *carry_row, hipStream_t st)
+                   float *carry, int32_t *carry_row, float *owner, hipStream_t st)
     {
         if constexpr (Packed<K>::RS == 0) {
             return MAXK_E_DIM;
@@ -1724,12 +1784,10 @@ struct FwdPanelPacked {
             hipLaunchKernelGGL((fwd_panel_kernel<K, RS>), dim3((unsigned)blocks), dim3(kBlock),
                                fwd_lds_bytes<K>(k), st, reinterpret_cast<const int2 *>(sched), P,
                                indptr, idx, val, reinterpret_cast<const float *>(rec),
-                               rec + 4 * K, V, dim, k, out, carry, carry_row);
+                               rec + 4 * K, V, dim, k, out, carry, carry_row, owner);
             int rc = launch_status();
             if (rc) return rc;
-            hipLaunchKernelGGL(carry_fixup_kernel, dim3((unsigned)blocks), dim3(kBlock), 0, st, P,
-                               carry, carry_row, out, dim, (dim + 3) & ~3, 1, (size_t)0);
-            return launch_status();
+            return fwd_fixup(sched, P, carry, owner, carry_row, out, dim, false, st);
         }
     }
 };
@@ -1738,7 +1796,7 @@ template <int K>
 struct FwdRecords {
     static int run(const int32_t *sched, int64_t P, const int32_t *indptr, const int32_t *idx,
                    const float *val, const uint8_t *rec, int V, int dim, int k, bool acc,
-                   float *out, float *carry, int32_t *carry_row, hipStream_t st)
+                   float *out, float *carry, int32_t *carry_row, float *owner, hipStream_t st)
     {
         if constexpr (K == 0) {
             return MAXK_E_DIM;
@@ -1749,12 +1807,10 @@ struct FwdRecords {
             hipLaunchKernelGGL(kern, dim3((unsigned)blocks), dim3(kBlock), fwd_lds_bytes<K>(k), st,
                                reinterpret_cast<const int2 *>(sched), P, indptr, idx, val,
                                reinterpret_cast<const float *>(rec), rec + 4 * K, V, dim, k, out,
-                               carry, carry_row);
+                               carry, carry_row, owner);
             int rc = launch_status();
             if (rc) return rc;
-            hipLaunchKernelGGL(carry_fixup_kernel, dim3((unsigned)blocks), dim3(kBlock), 0, st, P,
-                               carry, carry_row, out, dim, (dim + 3) & ~3, 1, (size_t)0);
-            return launch_status();
+            return fwd_fixup(sched, P, carry, owner, carry_row, out, dim, acc, st);
         }
     }
 };
@@ -1980,10 +2036,21 @@ int maxk_warp4_build(const int32_t *indptr, int num_rows, int warp_max_nz, int32
 
 size_t maxk_forward_workspace_bytes(int64_t num_panels, int dim_origin)
 {
+    // carry rows | carry row ids | owner parts of split rows
     const size_t dimp = (size_t)((dim_origin + 3) & ~3);
-    return align_up((size_t)num_panels * dimp * sizeof(float), 256) +
+    return 2 * align_up((size_t)num_panels * dimp * sizeof(float), 256) +
            align_up((size_t)num_panels * sizeof(int32_t), 256);
 }
+
+namespace {
+inline float *fwd_owner_slots(void *workspace, int64_t num_panels, int dim_origin)
+{
+    const size_t dimp = (size_t)((dim_origin + 3) & ~3);
+    return reinterpret_cast<float *>(static_cast<char *>(workspace) +
+                                     align_up((size_t)num_panels * dimp * sizeof(float), 256) +
+                                     align_up((size_t)num_panels * sizeof(int32_t), 256));
+}
+}  // namespace
 
 int maxk_spgemm_forward(const int32_t *sched, int64_t num_panels, const int32_t *indptr,
                         const int32_t *indices, const float *values, const float *cbsr_data,
@@ -2002,6 +2069,7 @@ int maxk_spgemm_forward(const int32_t *sched, int64_t num_panels, const int32_t 
         static_cast<char *>(workspace) + align_up((size_t)num_panels * dimp * sizeof(float), 256));
     return dispatch_k<FwdPanel>(dim_k, sched, num_panels, indptr, indices, values, cbsr_data,
                                 cbsr_sel, num_rows, dim_origin, dim_k, out, carry, carry_row,
+                                fwd_owner_slots(workspace, num_panels, dim_origin),
                                 as_stream(stream));
 }
 
@@ -2071,11 +2139,12 @@ int maxk_spgemm_forward_packed(const int32_t *sched, int64_t num_panels, const i
     int32_t *carry_row = reinterpret_cast<int32_t *>(
         static_cast<char *>(workspace) + align_up((size_t)num_panels * dimp * sizeof(float), 256));
     const uint8_t *rec = static_cast<const uint8_t *>(packed);
+    float *owner = fwd_owner_slots(workspace, num_panels, dim_origin);
     hipStream_t st = as_stream(stream);
     switch (dim_k) {
-    case 4: return FwdPanelPacked<4>::run(sched, num_panels, indptr, indices, values, rec, num_rows, dim_origin, dim_k, out, carry, carry_row, st);
-    case 8: return FwdPanelPacked<8>::run(sched, num_panels, indptr, indices, values, rec, num_rows, dim_origin, dim_k, out, carry, carry_row, st);
-    default: return FwdPanelPacked<16>::run(sched, num_panels, indptr, indices, values, rec, num_rows, dim_origin, dim_k, out, carry, carry_row, st);
+    case 4: return FwdPanelPacked<4>::run(sched, num_panels, indptr, indices, values, rec, num_rows, dim_origin, dim_k, out, carry, carry_row, owner, st);
+    case 8: return FwdPanelPacked<8>::run(sched, num_panels, indptr, indices, values, rec, num_rows, dim_origin, dim_k, out, carry, carry_row, owner, st);
+    default: return FwdPanelPacked<16>::run(sched, num_panels, indptr, indices, values, rec, num_rows, dim_origin, dim_k, out, carry, carry_row, owner, st);
     }
 }
 
@@ -2110,6 +2179,7 @@ int maxk_spgemm_forward_records(const int32_t *sched, int64_t num_panels, const 
     return dispatch_k<FwdRecords>(dim_k, sched, num_panels, indptr, indices, values,
                                   static_cast<const uint8_t *>(records), num_rows, dim_origin,
                                   dim_k, (flags & MAXK_FWD_ACCUMULATE) != 0, out, carry, carry_row,
+                                  fwd_owner_slots(workspace, num_panels, dim_origin),
                                   as_stream(stream));
 }
 
