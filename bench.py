@@ -126,7 +126,7 @@ def pmc_traffic(key, call, algo=None, bands=1):
         return None, None
     fix = k.get("carry_fixup_kernel", 0.0)
     if call == "spgemm_forward":
-        parts = [k.get("fwd_panel_kernel"), fix]
+        parts = [k.get("fwd_panel_kernel"), k.get("carry_fixup_owner_kernel", fix)]
     elif algo == "local":
         parts = [None if "bwd_local_kernel" not in k else k["bwd_local_kernel"] * bands]
     elif algo == "staged":

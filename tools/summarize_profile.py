@@ -18,8 +18,8 @@ import os
 import shutil
 import sys
 
-HOT = ("fwd_panel_kernel", "carry_fixup_kernel", "bwd_panel_kernel", "bwd_segsum_kernel",
-       "bwd_local_kernel", "fwd_warp4_kernel", "bwd_warp4_kernel")
+HOT = ("fwd_panel_kernel", "carry_fixup_kernel", "carry_fixup_owner_kernel", "bwd_panel_kernel",
+       "bwd_segsum_kernel", "bwd_local_kernel", "fwd_warp4_kernel", "bwd_warp4_kernel")
 
 
 def main(tag: str, root: str = ".", workload: str | None = None):
