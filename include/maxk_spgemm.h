@@ -232,6 +232,23 @@ int maxk_sspmm_backward_local(const int32_t *seg_edge_off, int num_segments,
                               const uint8_t *cbsr_sel, int num_rows, int dim_origin, int dim_k,
                               float *dxs, void *stream);
 
+/* Multi-relation LOCAL backward for 8 relations, dim_k = 32 (the backward of
+ * maxk_spgemm_forward_multi at ogbn-proteins' R = 8): dxs[c,l] = sum_q sum_e
+ * val[e,q] * grad[q, row(e), sel[c,l]].  maxk_grad_interleave turns grad
+ * fp32[num_rel, num_rows, dim] into fp32[num_rows, dim, num_rel] (relation
+ * innermost); the kernel then fetches an edge's 8 relations at a selected
+ * column as 32 contiguous bytes.  edge_val: fp32[E, 8] in the plan's edge
+ * order (values[edge_perm, :]), 16-B aligned; same plan as
+ * maxk_sspmm_backward_local, bands sized for 8 gradient rows per source row. */
+int maxk_grad_interleave(const float *grad, int num_rel, int num_rows, int dim, float *out,
+                         void *stream);
+int maxk_sspmm_backward_local_rel8(const int32_t *seg_edge_off, int num_segments,
+                                   const int32_t *wave_dst_start, int num_waves, int dmax,
+                                   const int32_t *edge_rc, const float *edge_val,
+                                   const float *grad_interleaved, const uint8_t *cbsr_sel,
+                                   int num_rows, int dim_origin, int dim_k, float *dxs,
+                                   void *stream);
+
 /* ---------------------------------------------------------------------------
  * CBSR producer (MaxK top-k) and dense-gradient scatter.
  * Replace torch.topk in the CBSR producers (direct_kernel_interface.py:58-85,

@@ -54,6 +54,9 @@ SIGNATURES = {
                                  _L, _P, _P, _S, _P]),
     "maxk_backward_local_lds_bytes": (_S, [_I, _I]),
     "maxk_sspmm_backward_local": (_I, [_P, _I, _P, _I, _I, _P, _P, _P, _P, _I, _I, _I, _P, _P]),
+    "maxk_grad_interleave": (_I, [_P, _I, _I, _I, _P, _P]),
+    "maxk_sspmm_backward_local_rel8": (_I, [_P, _I, _P, _I, _I, _P, _P, _P, _P, _I, _I, _I, _P,
+                                            _P]),
     "maxk_cbsr_packed_row_bytes": (_S, [_I]),
     "maxk_cbsr_pack": (_I, [_P, _P, _I, _I, _P, _P]),
     "maxk_spgemm_forward_packed": (_I, [_P, _L, _P, _P, _P, _P, _I, _I, _I, _P, _P, _S, _P]),

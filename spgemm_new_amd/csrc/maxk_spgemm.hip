@@ -1642,6 +1642,110 @@ __global__ __launch_bounds__(kBlock) void cbsr_bank_order_kernel(const float *__
     }
 }
 
+// ---------------------------------------------------------------------------
+// Multi-relation LOCAL backward for R = 8 relations, k = 32, on the gradient
+// interleaved by relation: gt[row][col][q] (fp32[V, h, 8], from
+// grad_interleave_kernel).  One edge per wave-instruction: lane (entry l,
+// half) loads the 16 B of relations 4*half..4*half+3 at (row, sel[c, l]), so
+// an edge's 8 relations cost one 64-lane dwordx4 gather touching ~29 64-B
+// sectors, where 8 single-relation calls issue 4 dword gathers touching
+// ~112.  The two halves' partial sums meet by a lane swap and lanes 0..31
+// update dXs in LDS.  Plan, bands (sized for 8 gradient rows per source row)
+// and LDS block are the single-relation LOCAL's; the edge's record and its 8
+// values are wave-uniform (scalar loads).
+// ---------------------------------------------------------------------------
+__global__ __launch_bounds__(kBlock) void grad_interleave_kernel(const float *__restrict__ grad,
+                                                                 int R, int64_t plane, int64_t n,
+                                                                 float *__restrict__ out)
+{
+    // out[i * R + q] = grad[q * plane + i], i < n = V * h
+    const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
+        float v[16];
+#pragma unroll
+        for (int q = 0; q < 16; ++q)
+            if (q < R) v[q] = grad[q * plane + i];
+        if (R == 8) {
+            f4 *o = reinterpret_cast<f4 *>(out + i * 8);
+            o[0] = f4{v[0], v[1], v[2], v[3]};
+            o[1] = f4{v[4], v[5], v[6], v[7]};
+        } else {
+            for (int q = 0; q < R; ++q) out[i * R + q] = v[q];
+        }
+    }
+}
+
+__device__ __forceinline__ void local_rel8_edges(int e_beg, int e_end,
+                                                 const int32_t *__restrict__ erc,
+                                                 const float *__restrict__ evl,
+                                                 const float *__restrict__ gt, uint32_t dim,
+                                                 const uint8_t *sl, float *acc)
+{
+    constexpr int K = 32, U = 8;
+    const int lane = lane_id();
+    const int l = lane & 31, half = lane >> 5;
+    for (int base = e_beg; base < e_end; base += U) {
+        const int n = (e_end - base) < U ? (e_end - base) : U;   // wave-uniform
+        f4 g[U];
+        f4 v[U];
+        int ai[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            if (u >= n) break;
+            const int e = base + u;
+            const int rc = erc[e];                                 // uniform: scalar load
+            const uint32_t row = (uint32_t)rc & 0xffffffu;
+            ai[u] = (int)(((uint32_t)rc >> 24) * K) + l;
+            const uint32_t col = sl[ai[u]];
+            const f4 *vp = reinterpret_cast<const f4 *>(evl + (size_t)e * 8);
+            const f4 va = vp[0], vb = vp[1];
+            v[u] = half ? vb : va;
+            g[u] = *reinterpret_cast<const f4 *>(gt + ((size_t)row * dim + col) * 8 + 4 * half);
+        }
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            if (u >= n) break;
+            float p = v[u].x * g[u].x + v[u].y * g[u].y + v[u].z * g[u].z + v[u].w * g[u].w;
+            p += __shfl_xor(p, 32);
+            if (half == 0) acc[ai[u]] += p;
+        }
+    }
+}
+
+__global__ __launch_bounds__(kBlock) void bwd_local_rel8_kernel(
+    const int32_t *__restrict__ seg_beg, const int32_t *__restrict__ seg_end, bool first,
+    const int32_t *__restrict__ dstart, int num_waves, int dmax,
+    const int32_t *__restrict__ erc, const float *__restrict__ evl,
+    const float *__restrict__ gt, const uint8_t *__restrict__ sel, int dim,
+    float *__restrict__ dxs)
+{
+    constexpr int K = 32;
+    extern __shared__ __attribute__((aligned(16))) float lds[];
+    const int wl = __builtin_amdgcn_readfirstlane(threadIdx.x / kWave);
+    const int region = (dmax * K * 5 + 15) & ~15;
+    float *acc = reinterpret_cast<float *>(reinterpret_cast<char *>(lds) + wl * region);
+    uint8_t *sl = reinterpret_cast<uint8_t *>(acc + dmax * K);
+    const int w = blockIdx.x * kWavesPerBlock + wl;
+    if (w >= num_waves) return;
+    const int lane = lane_id();
+    const int e_beg = __builtin_amdgcn_readfirstlane(seg_beg[w]);
+    const int e_end = __builtin_amdgcn_readfirstlane(seg_end[w]);
+    if (!first && e_beg == e_end) return;
+    const int d0 = dstart[w], D = dstart[w + 1] - d0;
+    const int nent = D * K;
+    float *dst = dxs + (size_t)d0 * K;
+    const uint8_t *srow = sel + (size_t)d0 * K;
+    for (int i = lane; i < nent; i += kWave) {
+        acc[i] = first ? 0.f : dst[i];
+        const int c = srow[i];
+        sl[i] = (uint8_t)(c < dim ? c : dim - 1);
+    }
+    wave_sync_lds();
+    local_rel8_edges(e_beg, e_end, erc, evl, gt, (uint32_t)dim, sl, acc);
+    wave_sync_lds();
+    for (int i = lane; i < nent; i += kWave) dst[i] = srow[i] < dim ? acc[i] : 0.f;
+}
+
 template <int K>
 __global__ __launch_bounds__(kBlock) void cbsr_pack_kernel(const float *__restrict__ data,
                                                            const uint8_t *__restrict__ sel,
@@ -2311,6 +2415,49 @@ int maxk_sspmm_backward_local(const int32_t *seg_edge_off, int num_segments,
     default: return BwdLocal<64>::run(LOCAL_ARGS);
     }
 #undef LOCAL_ARGS
+}
+
+int maxk_grad_interleave(const float *grad, int num_rel, int num_rows, int dim, float *out,
+                         void *stream)
+{
+    if (num_rel < 1 || num_rel > 16 || num_rows < 0 || dim < 1) return MAXK_E_ARG;
+    if (num_rows == 0) return MAXK_OK;
+    if (!grad || !out) return MAXK_E_ARG;
+    const int64_t n = (int64_t)num_rows * dim;
+    const int64_t blocks = ceil_div(n, kBlock);
+    hipLaunchKernelGGL(grad_interleave_kernel, dim3((unsigned)(blocks < 8192 ? blocks : 8192)),
+                       dim3(kBlock), 0, as_stream(stream), grad, num_rel, n, n, out);
+    return launch_status();
+}
+
+int maxk_sspmm_backward_local_rel8(const int32_t *seg_edge_off, int num_segments,
+                                   const int32_t *wave_dst_start, int num_waves, int dmax,
+                                   const int32_t *edge_rc, const float *edge_val,
+                                   const float *grad_interleaved, const uint8_t *cbsr_sel,
+                                   int num_rows, int dim_origin, int dim_k, float *dxs,
+                                   void *stream)
+{
+    if (!seg_edge_off || !wave_dst_start || !dxs || num_waves < 1 || num_segments < 1 ||
+        num_rows < 1 || num_rows >= (1 << 24) || dmax < 1 || dmax > 256)
+        return MAXK_E_ARG;
+    if (dim_k != 32 || !dims_ok(dim_origin, dim_k)) return MAXK_E_DIM;
+    if (!edge_rc || !edge_val || !grad_interleaved || !cbsr_sel) return MAXK_E_ARG;
+    if ((reinterpret_cast<uintptr_t>(edge_val) | reinterpret_cast<uintptr_t>(grad_interleaved)) & 15)
+        return MAXK_E_ARG;
+    if (maxk_backward_local_lds_bytes(dmax, dim_k) > 160 * 1024) return MAXK_E_WORKSPACE;
+    hipStream_t st = as_stream(stream);
+    const size_t region = (size_t)((dmax * 32 * 5 + 15) & ~15);
+    for (int s = 0; s < num_segments; ++s) {
+        hipLaunchKernelGGL(bwd_local_rel8_kernel, dim3((unsigned)ceil_div(num_waves, kWavesPerBlock)),
+                           dim3(kBlock), region * kWavesPerBlock, st,
+                           seg_edge_off + (size_t)s * num_waves,
+                           seg_edge_off + (size_t)(s + 1) * num_waves, s == 0, wave_dst_start,
+                           num_waves, dmax, edge_rc, edge_val, grad_interleaved, cbsr_sel,
+                           dim_origin, dxs);
+        const int rc = launch_status();
+        if (rc) return rc;
+    }
+    return MAXK_OK;
 }
 
 int maxk_spmm_forward_warp4(const int32_t *warp4, const int32_t *idx, const float *val,

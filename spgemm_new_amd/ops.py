@@ -349,21 +349,73 @@ class MaxKGraph:
         """Backward of forward_multi: dXs = sum_q (A_q^T G_q) sampled at sel,
         with grad fp32[R, V, h] and values fp32[E, R].  Returns fp32[V, k].
         Composed from R single-relation backward calls (per-relation value
-        columns cached), summed on the device."""
+        columns cached), summed on the device; for R = 8 and k = 32 (ogbn-proteins)
+        one LOCAL pass over the gradient interleaved by relation instead
+        (algo AUTO or LOCAL)."""
         check_tensor(grad, "grad_output", torch.float32, dim=3)
         check_tensor(values, "values", torch.float32, dim=2)
         R = values.shape[1]
         if grad.shape[0] != R or values.shape[0] != self.num_edges:
             raise RuntimeError("grad must be [R, V, h] and values [E, R]")
-        cols = self._multi_cols(values)
+        check_tensor(cbsr_sel, "sparse_selector", torch.uint8, dim=2)
+        if grad.shape[1] != self.num_rows or cbsr_sel.shape[0] != self.num_cols:
+            raise RuntimeError("grad must be [R, num_rows, h] and sparse_selector [num_cols, k]")
+        _on_device(self, grad_output=grad, sparse_selector=cbsr_sel, values=values)
         k = cbsr_sel.shape[1]
         if out is None:
             out = torch.empty((self.num_cols, k), dtype=torch.float32, device=self.device)
+        rel8_ok = (R == 8 and k == 32 and self.num_edges > 0 and self.local_plan(k) is not None)
+        if algo == _lib.MAXK_BWD_AUTO and rel8_ok:
+            # measured once per (h, R): the interleaved pass vs R composed calls
+            key = ("multi", k, grad.shape[2], R)
+            if key not in self._bwd_choice and not torch.cuda.is_current_stream_capturing():
+                ms = []
+                for fn in (lambda: self._backward_rel8(grad, cbsr_sel, values, out),
+                           lambda: self._backward_composed(grad, cbsr_sel, values, out,
+                                                           _lib.MAXK_BWD_AUTO)):
+                    fn()
+                    e0 = torch.cuda.Event(enable_timing=True)
+                    e1 = torch.cuda.Event(enable_timing=True)
+                    e0.record()
+                    fn()
+                    e1.record()
+                    e1.synchronize()
+                    ms.append(e0.elapsed_time(e1))
+                self._bwd_choice[key] = "rel8" if ms[0] <= ms[1] else "composed"
+            if self._bwd_choice.get(key, "rel8") == "rel8":
+                algo = _lib.MAXK_BWD_LOCAL
+        if algo == _lib.MAXK_BWD_LOCAL and rel8_ok:
+            return self._backward_rel8(grad, cbsr_sel, values, out)
+        return self._backward_composed(grad, cbsr_sel, values, out, algo)
+
+    def _backward_composed(self, grad, cbsr_sel, values, out, algo):
+        R = values.shape[1]
+        cols = self._multi_cols(values)
         tmp = torch.empty_like(out) if R > 1 else None
         for q in range(R):
             sspmm_backward(self, grad[q], cbsr_sel, out if q == 0 else tmp, cols[q], algo)
             if q > 0:
                 out.add_(tmp)
+        return out
+
+    def _backward_rel8(self, grad, sel, values, out):
+        """R = 8, k = 32: the gradient interleaved by relation ([V, h, 8]) and one
+        dwordx4 gather per lane covering an edge's 8 relations
+        (maxk_sspmm_backward_local_rel8)."""
+        h = grad.shape[2]
+        L = _lib.load()
+        gt = self._workspace(("grad_rel8", h), self.num_rows * h * 8 * 4)
+        gt = gt[: self.num_rows * h * 8 * 4].view(torch.float32)
+        _lib.check(L.maxk_grad_interleave(grad.data_ptr(), 8, self.num_rows, h, gt.data_ptr(),
+                                          _stream(out)), "maxk_grad_interleave")
+        plan = self.local_plan(32)
+        seg, ns = self.local_bands(plan, h * 8)       # 8 gradient rows per source row
+        ev = self.local_values(plan, values)          # [E, 8] in plan order
+        _lib.check(L.maxk_sspmm_backward_local_rel8(
+            seg.data_ptr(), ns, plan["dstart"].data_ptr(), plan["num_waves"], plan["dmax"],
+            plan["edge_rc"].data_ptr(), ev.data_ptr(), gt.data_ptr(), sel.data_ptr(),
+            self.num_rows, h, 32, out.data_ptr(), _stream(out)), "maxk_sspmm_backward_local_rel8")
+        self.last_bwd_algo = "local_rel8"
         return out
 
     def _multi_cols(self, values: torch.Tensor):

@@ -863,3 +863,24 @@ def test_bitwise_deterministic(dev, g_small, algo):
     dxs = [g.backward(G, s_, algo=algo).cpu() for _ in range(3)]
     assert all(torch.equal(ys[0], y) for y in ys[1:])
     assert all(torch.equal(dxs[0], x) for x in dxs[1:])
+
+
+@pytest.mark.parametrize("h", [256, 64, 100])
+@pytest.mark.parametrize("band_bytes", [None, 1024 * 40])
+def test_backward_multi_rel8(dev, oracle, monkeypatch, h, band_bytes):
+    """R = 8, k = 32: the relation-interleaved LOCAL backward (one dwordx4 gather per
+    lane covers an edge's 8 relations) vs the sum of 8 oracle backward calls."""
+    import spgemm_new_amd.ops as ops
+    if band_bytes:
+        monkeypatch.setattr(ops, "LOCAL_BAND_BYTES", band_bytes)
+    indptr, indices = small_csr(900, seed=h)
+    v, e, R, k = len(indptr) - 1, len(indices), 8, 32
+    vals = np.random.default_rng(9).random((e, R), dtype=np.float32)
+    _, sel = random_cbsr(v, k, h, seed=6)
+    grad = np.random.default_rng(10).random((R, v, h), dtype=np.float32)
+    g = S.MaxKGraph(T(indptr, dev), T(indices, dev), panel_cost=512)
+    out = torch.full((v, k), float("nan"), device=dev)
+    dx = g.backward_multi(T(grad, dev), T(sel, dev), T(vals, dev), out=out, algo=_lib.MAXK_BWD_LOCAL)
+    assert g.last_bwd_algo == "local_rel8"
+    ref = sum(oracle.np_backward(indptr, indices, vals[:, q].copy(), grad[q], sel) for q in range(R))
+    assert oracle.parity_error(dx.cpu().numpy(), ref) <= TOL
