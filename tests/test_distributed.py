@@ -100,10 +100,17 @@ def _worker(rank, world, port, q, overlap=True, engine="records", k=8):
         assert m.overlap == (overlap and m.plan.num_halo > 0)
         sel_l = m.local_rows(torch.from_numpy(sel))
         y = m.forward(m.local_rows(torch.from_numpy(data)), sel_l, h)
+        hs = m.last_halo_selectors()
         # the forward's selectors are reused; a different tensor is exchanged again
         dx = m.backward(m.local_rows(torch.from_numpy(grad)), sel_l)
         dx2 = m.backward(m.local_rows(torch.from_numpy(grad)), sel_l.clone())
         assert torch.equal(dx, dx2)
+        # after another forward (other selectors) the saved halo selectors still
+        # give the first forward's backward (what PartitionedSpGEMMFunction does)
+        d2, s2 = random_cbsr(v, k, h, seed=9)
+        m.forward(m.local_rows(torch.from_numpy(d2)), m.local_rows(torch.from_numpy(s2)), h)
+        dx3 = m.backward(m.local_rows(torch.from_numpy(grad)), sel_l, halo_sel=hs)
+        assert torch.equal(dx, dx3)
         # gather to rank 0
         ys = [None] * world
         dxs = [None] * world
