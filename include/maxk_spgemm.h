@@ -113,6 +113,13 @@ int maxk_spgemm_forward_packed(const int32_t *sched, int64_t num_panels, const i
  * in [4, 256]; same schedule and workspace as maxk_spgemm_forward.
  * ------------------------------------------------------------------------- */
 #define MAXK_FWD_ACCUMULATE 1
+/* dst[seg_row[s], :] += sum_{j in [seg_off[s], seg_off[s+1])} src[order[j], :] for
+ * rows of `width` floats: the owners' add of the halo partial sums returned by
+ * the peers (reverse exchange of the partitioned backward), in a fixed order
+ * (no atomics).  seg_row distinct. */
+int maxk_segment_rows_add(const float *src, int width, const int64_t *order,
+                          const int64_t *seg_off, const int64_t *seg_row, int64_t num_segments,
+                          float *dst, void *stream);
 int maxk_cbsr_gather_records(const float *cbsr_data, const uint8_t *cbsr_sel, const int32_t *rows,
                              int64_t num_records, int dim_k, void *records, void *stream);
 int maxk_spgemm_forward_records(const int32_t *sched, int64_t num_panels, const int32_t *indptr,

@@ -151,6 +151,13 @@ class PartitionedMaxK:
         lv = lv_all if self.num_rel == 1 else lv_all[:, 0].contiguous()
         make = engine or _default_engine
         self.send_rows = p.send_local.to(torch.int32).contiguous()
+        # reverse exchange: the partial sums come back in send order; the owners'
+        # add runs per own node over its (sorted) returns -- no atomics
+        order = torch.sort(p.send_local, stable=True).indices
+        nodes, counts = torch.unique_consecutive(p.send_local[order], return_counts=True)
+        seg_off = torch.zeros(nodes.numel() + 1, dtype=torch.int64, device=self.device)
+        seg_off[1:] = torch.cumsum(counts, 0)
+        self._ret = (order.contiguous(), seg_off, nodes.to(torch.int64).contiguous())
         self.records = records
         # overlap (forward): the block is also split by column into own | halo
         # parts, so the own part computes while the halo CBSR is in flight.  The
@@ -294,7 +301,14 @@ class PartitionedMaxK:
         k = dxs.shape[1]
         back = self._exchange(dxs[p.num_own:], k, torch.float32, reverse=True)
         own = dxs[: p.num_own]
-        own.index_add_(0, p.send_local, back)
+        order, seg_off, nodes = self._ret
+        if own.is_cuda and nodes.numel() > 0:
+            from . import _lib
+            _lib.check(_lib.load().maxk_segment_rows_add(
+                back.data_ptr(), k, order.data_ptr(), seg_off.data_ptr(), nodes.data_ptr(),
+                nodes.numel(), own.data_ptr(), _lib.stream_ptr(own.device)), "maxk_segment_rows_add")
+        else:
+            own.index_add_(0, p.send_local, back)
         return own
 
     def backward(self, grad_own: torch.Tensor, sel_own: torch.Tensor | None = None,

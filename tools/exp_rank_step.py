@@ -112,5 +112,57 @@ def main():
             torch.cuda.empty_cache()
 
 
+
+
+def breakdown(graph="products", k=32, world=8, rank=0):
+    """Per-component times of one rank's step (loopback exchange)."""
+    dev = torch.device("cuda:0")
+    V, E = CONFIGS[graph]
+    h = 256
+    indptr, indices = synthetic_csr_gpu(V, E, device=dev)
+    gen = torch.Generator(device=dev)
+    gen.manual_seed(5)
+    values = torch.rand(E, generator=gen, device=dev)
+    X = torch.rand((V, h), generator=gen, device=dev)
+    G = torch.rand((V, h), generator=gen, device=dev)
+    data, sel = topk_cbsr(X, k)
+    bounds = D.row_partition(indptr, world)
+    lb = Loopback(indptr, indices, bounds, rank, data, sel)
+    D.a2a = lb
+    m = D.PartitionedMaxK(indptr, indices, values, rank, world, dev)
+    d_l, s_l, g_l = m.local_rows(data), m.local_rows(sel), m.local_rows(G)
+    m.forward(d_l, s_l, h)
+    m.backward(g_l, s_l)
+    p = m.plan
+    send = m._pack(d_l, s_l)
+    recv = torch.empty((p.num_halo, 5 * k), dtype=torch.uint8, device=dev)
+    y = torch.empty((p.num_own, h), device=dev)
+    rows = {
+        "pack": lambda: m._pack(d_l, s_l),
+        "exchange (loopback)": lambda: lb(recv, send),
+        "own-column forward": lambda: m.local_own.forward(d_l, s_l, h, out=y),
+        "halo-column forward (records, +=)": lambda: m.local_halo.forward_records(recv, k, h, out=y,
+                                                                                accumulate=True),
+        "single-block forward": lambda: m.local.forward(*m.gather_halo_cbsr(d_l, s_l), h),
+        "block selectors": lambda: m._block_sel(s_l),
+        "local backward": lambda: m.local.backward(g_l, m._block_sel(s_l)),
+        "whole forward": lambda: m.forward(d_l, s_l, h),
+        "whole backward": lambda: m.backward(g_l, s_l),
+    }
+    dx = m.local.backward(g_l, m._block_sel(s_l))
+    back = torch.empty((m.send_rows.numel(), k), device=dev)
+    rows["reverse exchange (loopback)"] = lambda: lb(back, dx[p.num_own:])
+    own = dx[: p.num_own]
+    rows["index_add"] = lambda: own.index_add_(0, p.send_local, back)
+    rows["return (whole)"] = lambda: m._return_halo(dx)
+    print(f"{graph} k={k} world={world} rank={rank}: own={p.num_own} halo={p.num_halo} "
+          f"bwd algo {m.local.last_bwd_algo}")
+    for name, fn in rows.items():
+        print(f"  {name:36s} {timed(fn, reps=10):.3f} ms", flush=True)
+
+
 if __name__ == "__main__":
-    main()
+    if len(sys.argv) > 1 and sys.argv[1] == "breakdown":
+        breakdown(*(sys.argv[2:3] or ["products"]))
+    else:
+        main()
