@@ -103,3 +103,19 @@ def test_fuzz_parity(dev, oracle, seed):
             assert oracle.parity_error(ym[q], refq) <= TOL, f"{ctx} R={R} q={q}"
             ref_m += oracle.np_backward(indptr, indices, vals[:, q], gm[q], sel_np)
         assert oracle.parity_error(dxm, ref_m) <= TOL, f"{ctx} R={R}"
+
+    # halo-record forward (multi-GPU path), accumulating onto a random base
+    if k >= 4 and k & (k - 1) == 0 and C > 0:
+        rec = S.cbsr_gather_records(data, sel)
+        base = rng.standard_normal((V, h)).astype(np.float32)
+        yr = g.forward_records(rec, k, h, out=T(base, dev), accumulate=True)
+        assert oracle.parity_error(yr.cpu().numpy(), ref + base) <= TOL, f"{ctx} records"
+
+    # relation-interleaved multi-relation backward (R = 8, k = 32)
+    if k == 32 and len(indices) > 0 and g.local_plan(32) is not None:
+        vals8 = rng.standard_normal((len(indices), 8)).astype(np.float32)
+        g8 = rng.standard_normal((8, V, h)).astype(np.float32)
+        dx8 = torch.full((C, k), float("nan"), device=dev)
+        g.backward_multi(T(g8, dev), sel, T(vals8, dev), out=dx8, algo=_lib.MAXK_BWD_LOCAL)
+        ref8 = sum(oracle.np_backward(indptr, indices, vals8[:, q], g8[q], sel_np) for q in range(8))
+        assert oracle.parity_error(dx8.cpu().numpy(), ref8) <= TOL, f"{ctx} rel8"
