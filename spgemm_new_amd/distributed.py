@@ -24,8 +24,6 @@ can be tested on CPU with gloo; the default engine is the HIP MaxKGraph.
 """
 from __future__ import annotations
 
-import os
-
 import torch
 import torch.distributed as dist
 
@@ -105,17 +103,8 @@ class HaloPlan:
         return self.num_halo * 5
 
 
-# waves the panel schedule should give a rank's (smaller) blocks: a block of a
-# few million edges at the default 2048-cost panels has too few panels to fill
-# 256 CUs x 16 waves
-_MIN_PANELS = int(os.environ.get("MAXK_PART_MIN_PANELS", 16384))
-
-
 def _default_engine(local_indptr, local_indices, local_values, num_cols, **kw):
-    if "panel_cost" not in kw and _MIN_PANELS > 0:
-        rows = local_indptr.numel() - 1
-        cost = local_indices.numel() + 16 * rows
-        kw = dict(kw, panel_cost=int(min(2048, max(256, cost // _MIN_PANELS))))
+    # (a rank's blocks are small: MaxKGraph's default panel cost gives them enough panels)
     return MaxKGraph(local_indptr, local_indices, local_values, num_cols=num_cols, **kw)
 
 

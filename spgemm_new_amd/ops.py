@@ -62,6 +62,9 @@ LOCAL_WAVES_PER_CU = int(os.environ.get("MAXK_LOCAL_WAVES_PER_CU", 16))
 # LOCAL backward: gradient-row bytes per source band (one launch each); about 32 MB keeps a
 # band's G rows resident in the Infinity Cache (tools/exp_local_window.py)
 LOCAL_BAND_BYTES = int(os.environ.get("MAXK_LOCAL_BAND_BYTES", 32 << 20))
+# panel schedule: at least this many panels (waves) per graph when the default
+# 2048-cost panels would give fewer
+MIN_PANELS = int(os.environ.get("MAXK_MIN_PANELS", 16384))
 # forward at k in {4, 8, 16}: pack CBSR into one record per node (MAXK_FWD_PACKED=0 disables)
 FWD_PACKED = os.environ.get("MAXK_FWD_PACKED", "1") != "0"
 # fused multi-relation forward: reorder CBSR entries against LDS store conflicts
@@ -117,7 +120,7 @@ class MaxKGraph:
     """
 
     def __init__(self, indptr: torch.Tensor, indices: torch.Tensor,
-                 values: torch.Tensor | None = None, *, panel_cost: int = _lib.DEFAULT_PANEL_COST,
+                 values: torch.Tensor | None = None, *, panel_cost: int | None = None,
                  row_cost: int = _lib.DEFAULT_ROW_COST, bwd_panel_cost: int | None = None,
                  csc_panel_cost: int | None = None, num_cols: int | None = None,
                  validate: bool = True):
@@ -152,6 +155,13 @@ class MaxKGraph:
             values = torch.zeros(1, dtype=torch.float32, device=indices.device)
         self.indptr, self.indices, self.values = indptr, indices, values
         self.device = indices.device
+        if panel_cost is None:
+            # 2048 (MAXK_DEFAULT_PANEL_COST) for big graphs; smaller panels when
+            # that would leave fewer than MIN_PANELS waves (a rank's block, a
+            # small graph): the own-column block of a Reddit rank at N=8 took
+            # 0.137 ms with 2048-cost panels, 0.089 ms with >= 16 K panels
+            cost = self.num_edges + row_cost * self.num_rows
+            panel_cost = int(min(_lib.DEFAULT_PANEL_COST, max(256, cost // max(MIN_PANELS, 1))))
         self.panel_cost, self.row_cost = panel_cost, row_cost
         self.sched, self.num_panels = _build_schedule(indptr, self.num_rows, self.num_edges,
                                                       panel_cost, row_cost)

@@ -18,7 +18,8 @@ def test_pmc_traffic_composition():
     assert t == int(kern["bwd_local_kernel"] * 8)
     assert src == f"profiles/{ent['profile']}_summary.json" and os.path.exists(os.path.join(ROOT, src))
     t, _ = bench.pmc_traffic("reddit_h256_k32_local", "spgemm_forward", "local", 8)
-    assert t == int(kern["fwd_panel_kernel"] + kern.get("carry_fixup_kernel", 0.0))
+    fix = kern.get("carry_fixup_owner_kernel", kern.get("carry_fixup_kernel", 0.0))
+    assert t == int(kern["fwd_panel_kernel"] + fix)
     assert bench.pmc_traffic("no_such_workload", "sspmm_backward", "local", 1) == (None, None)
 
 
