@@ -104,7 +104,6 @@ class HaloPlan:
 
 
 def _default_engine(local_indptr, local_indices, local_values, num_cols, **kw):
-    # (a rank's blocks are small: MaxKGraph's default panel cost gives them enough panels)
     return MaxKGraph(local_indptr, local_indices, local_values, num_cols=num_cols, **kw)
 
 
