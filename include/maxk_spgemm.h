@@ -46,6 +46,7 @@ extern "C" {
  * MAXK_DEFAULT_ROW_COST; a panel (one wavefront's work item) costs
  * MAXK_DEFAULT_PANEL_COST. */
 #define MAXK_DEFAULT_PANEL_COST 2048
+#define MAXK_FWD_ACCUMULATE 1  /* forward flag: out += A . X^ instead of out = A . X^ */
 #define MAXK_DEFAULT_ROW_COST 16
 
 /* Library build identification (string, host memory, static). */
@@ -83,6 +84,12 @@ int maxk_spgemm_forward(const int32_t *sched, int64_t num_panels, const int32_t 
                         const float *cbsr_data, const uint8_t *cbsr_sel, int num_rows,
                         int dim_origin, int dim_k, float *out, void *workspace,
                         size_t workspace_bytes, void *stream);
+/* The same with flags: MAXK_FWD_ACCUMULATE adds A . X^ into out. */
+int maxk_spgemm_forward_ex(const int32_t *sched, int64_t num_panels, const int32_t *indptr,
+                           const int32_t *indices, const float *values, const float *cbsr_data,
+                           const uint8_t *cbsr_sel, int num_rows, int dim_origin, int dim_k,
+                           int flags, float *out, void *workspace, size_t workspace_bytes,
+                           void *stream);
 
 /* ---------------------------------------------------------------------------
  * Packed CBSR forward (k = 4, 8, 16).  maxk_cbsr_pack writes one record per
@@ -112,7 +119,6 @@ int maxk_spgemm_forward_packed(const int32_t *sched, int64_t num_panels, const i
  * column block adds onto the rows its own block wrote.  dim_k a power of two
  * in [4, 256]; same schedule and workspace as maxk_spgemm_forward.
  * ------------------------------------------------------------------------- */
-#define MAXK_FWD_ACCUMULATE 1
 /* dst[seg_row[s], :] += sum_{j in [seg_off[s], seg_off[s+1])} src[order[j], :] for
  * rows of `width` floats: the owners' add of the halo partial sums returned by
  * the peers (reverse exchange of the partitioned backward), in a fixed order

@@ -49,6 +49,7 @@ SIGNATURES = {
     "maxk_warp4_build": (_I, [_P, _I, _I, _P, _P, _L, ctypes.POINTER(ctypes.c_int64), _P]),
     "maxk_forward_workspace_bytes": (_S, [_L, _I]),
     "maxk_spgemm_forward": (_I, [_P, _L, _P, _P, _P, _P, _P, _I, _I, _I, _P, _P, _S, _P]),
+    "maxk_spgemm_forward_ex": (_I, [_P, _L, _P, _P, _P, _P, _P, _I, _I, _I, _I, _P, _P, _S, _P]),
     "maxk_backward_workspace_bytes": (_S, [_I, _L, _I, _L]),
     "maxk_sspmm_backward": (_I, [_I, _P, _L, _P, _P, _P, _P, _P, _I, _I, _L, _I, _I, _P, _P, _P,
                                  _L, _P, _P, _S, _P]),

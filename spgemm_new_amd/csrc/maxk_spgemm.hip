@@ -1907,15 +1907,17 @@ template <int K>
 struct FwdPanel {
     static int run(const int32_t *sched, int64_t P, const int32_t *indptr, const int32_t *idx,
                    const float *val, const float *data, const uint8_t *sel, int V, int dim, int k,
-                   float *out, float *carry, int32_t *carry_row, float *owner, hipStream_t st)
+                   float *out, float *carry, int32_t *carry_row, float *owner, bool acc,
+                   hipStream_t st)
     {
         const int64_t blocks = ceil_div(P, kWavesPerBlock);
-        hipLaunchKernelGGL(fwd_panel_kernel<K>, dim3((unsigned)blocks), dim3(kBlock),
-                           fwd_lds_bytes<K>(k), st, reinterpret_cast<const int2 *>(sched), P,
-                           indptr, idx, val, data, sel, V, dim, k, out, carry, carry_row, owner);
+        auto kern = acc ? fwd_panel_kernel<K, 0, true> : fwd_panel_kernel<K, 0, false>;
+        hipLaunchKernelGGL(kern, dim3((unsigned)blocks), dim3(kBlock), fwd_lds_bytes<K>(k), st,
+                           reinterpret_cast<const int2 *>(sched), P, indptr, idx, val, data, sel,
+                           V, dim, k, out, carry, carry_row, owner);
         int rc = launch_status();
         if (rc) return rc;
-        return fwd_fixup(sched, P, carry, owner, carry_row, out, dim, false, st);
+        return fwd_fixup(sched, P, carry, owner, carry_row, out, dim, acc, st);
     }
 };
 
@@ -2206,6 +2208,18 @@ int maxk_spgemm_forward(const int32_t *sched, int64_t num_panels, const int32_t 
                         const uint8_t *cbsr_sel, int num_rows, int dim_origin, int dim_k,
                         float *out, void *workspace, size_t workspace_bytes, void *stream)
 {
+    return maxk_spgemm_forward_ex(sched, num_panels, indptr, indices, values, cbsr_data, cbsr_sel,
+                                  num_rows, dim_origin, dim_k, 0, out, workspace, workspace_bytes,
+                                  stream);
+}
+
+int maxk_spgemm_forward_ex(const int32_t *sched, int64_t num_panels, const int32_t *indptr,
+                           const int32_t *indices, const float *values, const float *cbsr_data,
+                           const uint8_t *cbsr_sel, int num_rows, int dim_origin, int dim_k,
+                           int flags, float *out, void *workspace, size_t workspace_bytes,
+                           void *stream)
+{
+    if (flags & ~MAXK_FWD_ACCUMULATE) return MAXK_E_ARG;
     if (!sched || !indptr || !out || num_panels < 1 || num_rows < 0) return MAXK_E_ARG;
     if (!dims_ok(dim_origin, dim_k)) return MAXK_E_DIM;
     if (num_rows == 0) return MAXK_OK;
@@ -2219,7 +2233,7 @@ int maxk_spgemm_forward(const int32_t *sched, int64_t num_panels, const int32_t 
     return dispatch_k<FwdPanel>(dim_k, sched, num_panels, indptr, indices, values, cbsr_data,
                                 cbsr_sel, num_rows, dim_origin, dim_k, out, carry, carry_row,
                                 fwd_owner_slots(workspace, num_panels, dim_origin),
-                                as_stream(stream));
+                                (flags & MAXK_FWD_ACCUMULATE) != 0, as_stream(stream));
 }
 
 int maxk_spmm_dense_forward(const int32_t *sched, int64_t num_panels, const int32_t *indptr,

@@ -265,8 +265,12 @@ class PartitionedMaxK:
         y = self.local_own.forward(data_own, sel_own, dim_origin)   # overlaps the exchange
         work.wait()
         h_data, h_sel = self._unpack(recv, k)
+        h_sel = h_sel.contiguous()
         self._fwd_sel, self._halo_part = sel_own, h_sel
-        y += self.local_halo.forward(h_data, h_sel.contiguous(), dim_origin)
+        if isinstance(self.local_halo, MaxKGraph):
+            self.local_halo.forward(h_data, h_sel, dim_origin, out=y, accumulate=True)
+        else:
+            y += self.local_halo.forward(h_data, h_sel, dim_origin)
         return y
 
     def last_halo_selectors(self) -> torch.Tensor:

@@ -334,9 +334,11 @@ class MaxKGraph:
 
     # ---------------------------------------------------------------- compute
     def forward(self, cbsr_data: torch.Tensor, cbsr_sel: torch.Tensor, dim_origin: int = 256,
-                out: torch.Tensor | None = None, values: torch.Tensor | None = None) -> torch.Tensor:
-        """Y = A . scatter(CBSR)  (spmm_maxk.cu:17-106).  Returns fp32[V, dim_origin]."""
-        return spgemm_forward(self, cbsr_data, cbsr_sel, dim_origin, out, values)
+                out: torch.Tensor | None = None, values: torch.Tensor | None = None,
+                accumulate: bool = False) -> torch.Tensor:
+        """Y = A . scatter(CBSR)  (spmm_maxk.cu:17-106).  Returns fp32[V, dim_origin];
+        accumulate=True adds into out instead."""
+        return spgemm_forward(self, cbsr_data, cbsr_sel, dim_origin, out, values, accumulate)
 
     def forward_records(self, records: torch.Tensor, dim_k: int, dim_origin: int = 256,
                         out: torch.Tensor | None = None, values: torch.Tensor | None = None,
@@ -477,11 +479,14 @@ def _check_cbsr(g: MaxKGraph, data, sel):
         raise RuntimeError("CBSR tensors must be on the graph's device")
 
 
-def spgemm_forward(g: MaxKGraph, data, sel, dim_origin: int = 256, out=None, values=None):
+def spgemm_forward(g: MaxKGraph, data, sel, dim_origin: int = 256, out=None, values=None,
+                   accumulate: bool = False):
     _check_cbsr(g, data, sel)
     k = data.shape[1]
     values = _check_values(g, values)
     if out is None:
+        if accumulate:
+            raise RuntimeError("accumulate needs an output")
         out = torch.empty((g.num_rows, dim_origin), dtype=torch.float32, device=g.device)
     else:
         check_tensor(out, "output", torch.float32, dim=2)
@@ -491,7 +496,7 @@ def spgemm_forward(g: MaxKGraph, data, sel, dim_origin: int = 256, out=None, val
     L = _lib.load()
     nbytes = L.maxk_forward_workspace_bytes(g.num_panels, dim_origin)
     ws = g._workspace(("fwd", dim_origin), nbytes)
-    rs = L.maxk_cbsr_packed_row_bytes(k) if FWD_PACKED else 0
+    rs = L.maxk_cbsr_packed_row_bytes(k) if FWD_PACKED and not accumulate else 0
     if rs:  # k in {4, 8, 16}: one cache line per gathered neighbour (packed records)
         rec = g._workspace(("packed", k), g.num_cols * rs)
         _lib.check(L.maxk_cbsr_pack(data.data_ptr(), sel.data_ptr(), g.num_cols, k, rec.data_ptr(),
@@ -501,10 +506,12 @@ def spgemm_forward(g: MaxKGraph, data, sel, dim_origin: int = 256, out=None, val
             values.data_ptr(), rec.data_ptr(), g.num_rows, dim_origin, k, out.data_ptr(),
             ws.data_ptr(), ws.numel(), _stream(out)), "maxk_spgemm_forward_packed")
         return out
-    _lib.check(L.maxk_spgemm_forward(g.sched.data_ptr(), g.num_panels, g.indptr.data_ptr(),
-                                     g.indices.data_ptr(), values.data_ptr(), data.data_ptr(),
-                                     sel.data_ptr(), g.num_rows, dim_origin, k, out.data_ptr(),
-                                     ws.data_ptr(), ws.numel(), _stream(out)), "maxk_spgemm_forward")
+    flags = _lib.MAXK_FWD_ACCUMULATE if accumulate else 0
+    _lib.check(L.maxk_spgemm_forward_ex(g.sched.data_ptr(), g.num_panels, g.indptr.data_ptr(),
+                                        g.indices.data_ptr(), values.data_ptr(), data.data_ptr(),
+                                        sel.data_ptr(), g.num_rows, dim_origin, k, flags,
+                                        out.data_ptr(), ws.data_ptr(), ws.numel(), _stream(out)),
+               "maxk_spgemm_forward")
     return out
 
 

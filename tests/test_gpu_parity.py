@@ -884,3 +884,17 @@ def test_backward_multi_rel8(dev, oracle, monkeypatch, h, band_bytes):
     assert g.last_bwd_algo == "local_rel8"
     ref = sum(oracle.np_backward(indptr, indices, vals[:, q].copy(), grad[q], sel) for q in range(R))
     assert oracle.parity_error(dx.cpu().numpy(), ref) <= TOL
+
+
+@pytest.mark.parametrize("k,h", [(32, 256), (8, 256), (16, 64), (5, 100)])
+def test_forward_accumulate(dev, oracle, g_small, k, h):
+    """maxk_spgemm_forward_ex with MAXK_FWD_ACCUMULATE: out += A . X^ (any k; the
+    packed k <= 16 path is bypassed)."""
+    indptr, indices, values = g_small
+    data, sel = random_cbsr(len(indptr) - 1, k, h, seed=k + 9)
+    g = S.MaxKGraph(T(indptr, dev), T(indices, dev), T(values, dev), panel_cost=300)
+    base = np.random.default_rng(7).random((len(indptr) - 1, h), dtype=np.float32)
+    out = T(base, dev)
+    g.forward(T(data, dev), T(sel, dev), h, out=out, accumulate=True)
+    ref = oracle.np_forward(indptr, indices, values, data, sel, h) + base
+    assert oracle.parity_error(out.cpu().numpy(), ref) <= TOL
