@@ -361,9 +361,9 @@ class MaxKGraph:
         """Backward of forward_multi: dXs = sum_q (A_q^T G_q) sampled at sel,
         with grad fp32[R, V, h] and values fp32[E, R].  Returns fp32[V, k].
         Composed from R single-relation backward calls (per-relation value
-        columns cached), summed on the device; for R = 8 and k = 32 (ogbn-proteins)
-        one LOCAL pass over the gradient interleaved by relation instead
-        (algo AUTO or LOCAL)."""
+        columns cached), summed on the device; for R a multiple of 8 and k = 32
+        (ogbn-proteins: R = 8) one LOCAL pass per 8 relations over the gradient
+        interleaved by relation instead (algo AUTO or LOCAL)."""
         check_tensor(grad, "grad_output", torch.float32, dim=3)
         check_tensor(values, "values", torch.float32, dim=2)
         R = values.shape[1]
@@ -376,7 +376,7 @@ class MaxKGraph:
         k = cbsr_sel.shape[1]
         if out is None:
             out = torch.empty((self.num_cols, k), dtype=torch.float32, device=self.device)
-        rel8_ok = (R == 8 and k == 32 and self.num_edges > 0 and self.local_plan(k) is not None)
+        rel8_ok = (R % 8 == 0 and k == 32 and self.num_edges > 0 and self.local_plan(k) is not None)
         if algo == _lib.MAXK_BWD_AUTO and rel8_ok:
             # measured once per (h, R): the interleaved pass vs R composed calls
             key = ("multi", k, grad.shape[2], R)
@@ -411,24 +411,42 @@ class MaxKGraph:
         return out
 
     def _backward_rel8(self, grad, sel, values, out):
-        """R = 8, k = 32: the gradient interleaved by relation ([V, h, 8]) and one
-        dwordx4 gather per lane covering an edge's 8 relations
-        (maxk_sspmm_backward_local_rel8)."""
-        h = grad.shape[2]
+        """R = 8g, k = 32: per group of 8 relations, the gradient interleaved by
+        relation ([V, h, 8]) and one dwordx4 gather per lane covering an edge's 8
+        relations (maxk_sspmm_backward_local_rel8); groups summed on the device."""
+        h, R = grad.shape[2], values.shape[1]
         L = _lib.load()
         gt = self._workspace(("grad_rel8", h), self.num_rows * h * 8 * 4)
         gt = gt[: self.num_rows * h * 8 * 4].view(torch.float32)
-        _lib.check(L.maxk_grad_interleave(grad.data_ptr(), 8, self.num_rows, h, gt.data_ptr(),
-                                          _stream(out)), "maxk_grad_interleave")
         plan = self.local_plan(32)
         seg, ns = self.local_bands(plan, h * 8)       # 8 gradient rows per source row
-        ev = self.local_values(plan, values)          # [E, 8] in plan order
-        _lib.check(L.maxk_sspmm_backward_local_rel8(
-            seg.data_ptr(), ns, plan["dstart"].data_ptr(), plan["num_waves"], plan["dmax"],
-            plan["edge_rc"].data_ptr(), ev.data_ptr(), gt.data_ptr(), sel.data_ptr(),
-            self.num_rows, h, 32, out.data_ptr(), _stream(out)), "maxk_sspmm_backward_local_rel8")
+        ev = self.local_values(plan, values)          # [E, R] in plan order
+        tmp = torch.empty_like(out) if R > 8 else None
+        for g0 in range(0, R, 8):
+            evg = ev if R == 8 else self._rel_group_values(plan, values, ev, g0)
+            dst = out if g0 == 0 else tmp
+            _lib.check(L.maxk_grad_interleave(grad[g0:g0 + 8].data_ptr(), 8, self.num_rows, h,
+                                              gt.data_ptr(), _stream(out)), "maxk_grad_interleave")
+            _lib.check(L.maxk_sspmm_backward_local_rel8(
+                seg.data_ptr(), ns, plan["dstart"].data_ptr(), plan["num_waves"], plan["dmax"],
+                plan["edge_rc"].data_ptr(), evg.data_ptr(), gt.data_ptr(), sel.data_ptr(),
+                self.num_rows, h, 32, dst.data_ptr(), _stream(out)),
+                "maxk_sspmm_backward_local_rel8")
+            if g0 > 0:
+                out.add_(tmp)
         self.last_bwd_algo = "local_rel8"
         return out
+
+    def _rel_group_values(self, plan, values, ev, g0):
+        """Columns g0..g0+7 of the plan-ordered values [E, R], contiguous (cached)."""
+        cache = plan.setdefault("rel_group_cache", {})
+        key = (_tensor_key(values), g0)
+        hit = cache.get(key)
+        if hit is None:
+            if len(cache) >= 16:
+                cache.clear()
+            hit = cache[key] = (ev[:, g0:g0 + 8].contiguous(), values)
+        return hit[0]
 
     def _multi_cols(self, values: torch.Tensor):
         key = _tensor_key(values)

@@ -865,16 +865,16 @@ def test_bitwise_deterministic(dev, g_small, algo):
     assert all(torch.equal(dxs[0], x) for x in dxs[1:])
 
 
-@pytest.mark.parametrize("h", [256, 64, 100])
+@pytest.mark.parametrize("h,R", [(256, 8), (64, 8), (100, 8), (256, 16), (64, 24)])
 @pytest.mark.parametrize("band_bytes", [None, 1024 * 40])
-def test_backward_multi_rel8(dev, oracle, monkeypatch, h, band_bytes):
+def test_backward_multi_rel8(dev, oracle, monkeypatch, h, R, band_bytes):
     """R = 8, k = 32: the relation-interleaved LOCAL backward (one dwordx4 gather per
     lane covers an edge's 8 relations) vs the sum of 8 oracle backward calls."""
     import spgemm_new_amd.ops as ops
     if band_bytes:
         monkeypatch.setattr(ops, "LOCAL_BAND_BYTES", band_bytes)
     indptr, indices = small_csr(900, seed=h)
-    v, e, R, k = len(indptr) - 1, len(indices), 8, 32
+    v, e, k = len(indptr) - 1, len(indices), 32
     vals = np.random.default_rng(9).random((e, R), dtype=np.float32)
     _, sel = random_cbsr(v, k, h, seed=6)
     grad = np.random.default_rng(10).random((R, v, h), dtype=np.float32)
