@@ -62,6 +62,8 @@ LOCAL_WAVES_PER_CU = int(os.environ.get("MAXK_LOCAL_WAVES_PER_CU", 16))
 # LOCAL backward: gradient-row bytes per source band (one launch each); about 32 MB keeps a
 # band's G rows resident in the Infinity Cache (tools/exp_local_window.py)
 LOCAL_BAND_BYTES = int(os.environ.get("MAXK_LOCAL_BAND_BYTES", 32 << 20))
+# AUTO backward: timed calls per candidate (the minimum decides)
+AUTOTUNE_REPS = int(os.environ.get("MAXK_AUTOTUNE_REPS", 3))
 # panel schedule: at least this many panels (waves) per graph when the default
 # 2048-cost panels would give fewer
 MIN_PANELS = int(os.environ.get("MAXK_MIN_PANELS", 16384))
@@ -297,9 +299,9 @@ class MaxKGraph:
 
     def autotune_backward(self, grad, sel, out, values=None) -> int:
         """MAXK_BWD_AUTO: the fastest algorithm for this graph and k, measured once
-        (each candidate run twice, the second timed with HIP events on the
-        current stream) and cached.  Candidates: STAGED, ATOMIC, and LOCAL when
-        its plan exists.  During stream capture, or before any measurement,
+        (each candidate run once, then timed AUTOTUNE_REPS times with HIP events on
+        the current stream, the minimum kept) and cached.  Candidates: STAGED,
+        ATOMIC, and LOCAL when its plan exists.  During stream capture, or before any measurement,
         STAGED is used (allocation-free once its workspace exists)."""
         k = sel.shape[1]
         key = (k, grad.shape[1])
@@ -313,12 +315,14 @@ class MaxKGraph:
         best, best_ms = None, float("inf")
         for a in cands:
             sspmm_backward(self, grad, sel, out, values, a)
-            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-            e0.record()
-            sspmm_backward(self, grad, sel, out, values, a)
-            e1.record()
-            e1.synchronize()
-            ms = e0.elapsed_time(e1)
+            ms = float("inf")
+            for _ in range(AUTOTUNE_REPS):   # min of a few: one timing flipped close calls
+                e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                e0.record()
+                sspmm_backward(self, grad, sel, out, values, a)
+                e1.record()
+                e1.synchronize()
+                ms = min(ms, e0.elapsed_time(e1))
             if ms < best_ms:
                 best, best_ms = a, ms
         self._bwd_choice[key] = best
