@@ -213,6 +213,7 @@ int maxk_spgemm_forward_multi(const int32_t *sched, int64_t num_panels, const in
 #define MAXK_BWD_ATOMIC 1      /* push + global float atomics (reference's scheme) */
 #define MAXK_BWD_STAGED 2      /* push to per-edge staging rows + CSC segmented sum */
 #define MAXK_BWD_LOCAL 3       /* destination-owned LDS accumulation (maxk_sspmm_backward_local) */
+#define MAXK_BWD_TILE 4        /* gradient rows staged once per CU (maxk_sspmm_backward_tile) */
 size_t maxk_backward_workspace_bytes(int algo, int64_t num_edges, int dim_k,
                                      int64_t csc_num_panels);
 int maxk_sspmm_backward(int algo, const int32_t *sched, int64_t num_panels,
@@ -261,6 +262,28 @@ int maxk_sspmm_backward_local_rel8(const int32_t *seg_edge_off, int num_segments
                                    const float *grad_interleaved, const uint8_t *cbsr_sel,
                                    int num_rows, int dim_origin, int dim_k, float *dxs,
                                    void *stream);
+
+/* ---------------------------------------------------------------------------
+ * Backward SSpMM, TILE algorithm (dim_k = 32, dim_origin = 256): every
+ * gradient row is read once per CU into an LDS ring instead of being
+ * gathered per edge; destinations' dXs live in registers.  One workgroup per
+ * (destination group of <= 2048 columns, source-row range): grid =
+ * num_groups * splits, workgroup b = group b / splits, range b % splits.
+ * Inputs from the plan (spgemm_new_amd/tile.py; format in csrc/maxk_spgemm.hip
+ * above bwd_tile_kernel), one stream per (workgroup, wave) w = b * 16 + wave:
+ * headers int32[.., 4] from header_start[w] (16-B aligned), records
+ * int32[.., 4] from record_start[w] (16-B aligned, padded by 2 KB);
+ * num_chunks int32[num_groups * splits]; zero_row: 1 KB of zeros (16-B
+ * aligned).  part: fp32[(splits - 1) * num_cols * 32] scratch (NULL when
+ * splits == 1).  Writes every element of dxs; same result as the other
+ * algorithms up to fp32 summation order (deterministic).
+ * ------------------------------------------------------------------------- */
+int maxk_sspmm_backward_tile(const void *headers, const int64_t *header_start,
+                             const void *records, const int64_t *record_start,
+                             const int32_t *num_chunks, int num_groups, int splits,
+                             int group_size, const float *grad, const float *zero_row,
+                             const uint8_t *cbsr_sel, int num_rows, int num_cols, int dim_origin,
+                             int dim_k, float *dxs, float *part, void *stream);
 
 /* ---------------------------------------------------------------------------
  * CBSR producer (MaxK top-k) and dense-gradient scatter.

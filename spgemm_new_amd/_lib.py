@@ -27,6 +27,7 @@ MAXK_BWD_AUTO = 0
 MAXK_BWD_ATOMIC = 1
 MAXK_BWD_STAGED = 2
 MAXK_BWD_LOCAL = 3
+MAXK_BWD_TILE = 4
 MAXK_TOPK_ORDER_COLUMN = 0
 MAXK_TOPK_ORDER_VALUE = 1
 MAXK_TOPK_ORDER_LANE = 2
@@ -58,6 +59,8 @@ SIGNATURES = {
     "maxk_grad_interleave": (_I, [_P, _I, _I, _I, _P, _P]),
     "maxk_sspmm_backward_local_rel8": (_I, [_P, _I, _P, _I, _I, _P, _P, _P, _P, _I, _I, _I, _P,
                                             _P]),
+    "maxk_sspmm_backward_tile": (_I, [_P, _P, _P, _P, _P, _I, _I, _I, _P, _P, _P, _I, _I, _I, _I,
+                                      _P, _P, _P]),
     "maxk_cbsr_packed_row_bytes": (_S, [_I]),
     "maxk_cbsr_pack": (_I, [_P, _P, _I, _I, _P, _P]),
     "maxk_spgemm_forward_packed": (_I, [_P, _L, _P, _P, _P, _P, _I, _I, _I, _P, _P, _S, _P]),

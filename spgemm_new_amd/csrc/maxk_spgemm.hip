@@ -1746,6 +1746,347 @@ __global__ __launch_bounds__(kBlock) void bwd_local_rel8_kernel(
     for (int i = lane; i < nent; i += kWave) dst[i] = srow[i] < dim ? acc[i] : 0.f;
 }
 
+// ---------------------------------------------------------------------------
+// Backward SSpMM, TILE algorithm (k = 32, h = 256; maxk_sspmm_backward_tile).
+// LOCAL pays one 64-lane dword gather (~14 scattered 64-B sectors of a 1 KB
+// G row) per two edges.  TILE instead reads every G row ONCE per CU: a
+// workgroup (16 waves, the whole CU) owns up to 2048 destinations, keeps
+// their dXs in VGPRs (64 slot registers per wave, v64..v127; lanes 0-31 one
+// destination's 32 entries, lanes 32-63 another's) and their selectors as
+// packed bytes (v48..v63), and sweeps the distinct source rows that have
+// edges into its destinations through a 3-deep LDS ring of 47-row chunks
+// (LDS-DMA, one 1 KB row per wave-instruction; row 47 of each buffer is a
+// zero row for padding records).  Per edge: a selector byte picked by
+// register index, one ds_read_b32 of the staged row, one v_fma into the
+// slot register picked by index (s_set_gpr_idx: the slot is wave-uniform).
+// Source rows are split into `splits` ranges (one workgroup per destination
+// group and range) so 256 CUs are busy; range 0 writes dxs, the others write
+// partial rows that tile_combine_kernel adds.
+//
+// The plan (ops.py MaxKGraph.tile_plan) is one record stream per
+// (workgroup, wave): a 4-slot prologue {tot(0), tot(1), rows of chunks 0 and
+// 1}, then per chunk c a 3-slot header {n0 | n1 << 16, tot(c+2), rows of
+// chunk c+2 for this wave's three DMA pieces (-1 = zero row)} and n0 (n1)
+// records of destinations in lane half 0 (1), each a multiple of 4 (padding:
+// slot 0, zero row, value 0).  tot = header + records of a chunk.  Record =
+// {slot | (buffer * 48 + row) << 24, value}.
+constexpr int kTileWaves = 16;
+constexpr int kTileRows = 47;  // gradient rows per chunk; row 47 of a buffer is zero
+constexpr int kTileBufRows = 48;
+static_assert(kTileRows + 1 == kTileBufRows, "chunk rows + zero row = buffer rows");
+constexpr int kTileHdr = 3;
+constexpr int kTilePro = 4;
+
+typedef float tile_acc_t __attribute__((ext_vector_type(32)));
+typedef unsigned tile_sel_t __attribute__((ext_vector_type(16)));
+typedef int tile_hdr_t __attribute__((ext_vector_type(4)));
+
+__device__ __forceinline__ void tile_glds(const float *g, uint32_t lds_byte)
+{
+    uint32_t keep;
+    asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\t"
+                 "global_load_lds_dwordx4 %1, off\n\ts_mov_b32 m0, %0"
+                 : "=&s"(keep)
+                 : "v"(g), "s"(lds_byte)
+                 : "memory");
+}
+
+
+// Record i of a half-list: 4 dwords {slot, value bits, selector word |
+// (bit offset of the selector byte) << 8, LDS byte address of the staged
+// gradient row}.  One asm loop per half-list: exec narrowed to the half,
+// records read 4 at a time into SGPRs (s_load, the next group in flight while
+// the current one runs), selector words and slot registers picked by
+// s_set_gpr_idx.  The compiler sees neither a divergent branch nor an indexed
+// register, so the pinned slot (v64..v127) and selector (v48..v63) registers
+// stay in place; s64..s99 are the loop's.
+__device__ __forceinline__ void tile_half(const uint32_t *rb, uint32_t &ro, uint32_t groups,
+                                          uint64_t half_mask, tile_sel_t &selv, tile_acc_t &acc0,
+                                          tile_acc_t &acc1)
+{
+    uint32_t t0, t1, t2, t3, n = groups;
+    uint64_t ex;
+    asm volatile(
+        "s_cmp_eq_u32 %[n], 0\n\t"
+        "s_cbranch_scc1 .Ltile_done%=\n\t"
+        "s_mov_b64 %[ex], exec\n\t"
+        "s_mov_b64 exec, %[hm]\n\t"
+        "s_load_dwordx16 s[64:79], %[rb], %[ro]\n\t"
+        "s_add_u32 %[ro], %[ro], 64\n\t"
+        ".Ltile_a%=:\n\t"
+        "s_waitcnt lgkmcnt(0)\n\t"
+        "s_sub_u32 %[n], %[n], 1\n\t"
+        "s_cmp_eq_u32 %[n], 0\n\t"
+        "s_cbranch_scc1 .Ltile_a_last%=\n\t"
+        "s_load_dwordx16 s[80:95], %[rb], %[ro]\n\t"
+        "s_add_u32 %[ro], %[ro], 64\n\t"
+        "s_lshr_b32 s96, s66, 8\n\t"
+        "s_lshr_b32 s97, s70, 8\n\t"
+        "s_lshr_b32 s98, s74, 8\n\t"
+        "s_lshr_b32 s99, s78, 8\n\t"
+        "s_set_gpr_idx_on s66, gpr_idx(SRC0)\n\t"
+        "v_bfe_u32 %[t0], v48, s96, 8\n\t"
+        "s_set_gpr_idx_idx s70\n\t"
+        "v_bfe_u32 %[t1], v48, s97, 8\n\t"
+        "s_set_gpr_idx_idx s74\n\t"
+        "v_bfe_u32 %[t2], v48, s98, 8\n\t"
+        "s_set_gpr_idx_idx s78\n\t"
+        "v_bfe_u32 %[t3], v48, s99, 8\n\t"
+        "s_set_gpr_idx_off\n\t"
+        "v_lshl_add_u32 %[t0], %[t0], 2, s67\n\t"
+        "v_lshl_add_u32 %[t1], %[t1], 2, s71\n\t"
+        "v_lshl_add_u32 %[t2], %[t2], 2, s75\n\t"
+        "v_lshl_add_u32 %[t3], %[t3], 2, s79\n\t"
+        "ds_read_b32 %[t0], %[t0]\n\t"
+        "ds_read_b32 %[t1], %[t1]\n\t"
+        "ds_read_b32 %[t2], %[t2]\n\t"
+        "ds_read_b32 %[t3], %[t3]\n\t"
+        "s_waitcnt lgkmcnt(0)\n\t"
+        "s_set_gpr_idx_on s64, gpr_idx(SRC2,DST)\n\t"
+        "v_fma_f32 v64, %[t0], s65, v64\n\t"
+        "s_set_gpr_idx_idx s68\n\t"
+        "v_fma_f32 v64, %[t1], s69, v64\n\t"
+        "s_set_gpr_idx_idx s72\n\t"
+        "v_fma_f32 v64, %[t2], s73, v64\n\t"
+        "s_set_gpr_idx_idx s76\n\t"
+        "v_fma_f32 v64, %[t3], s77, v64\n\t"
+        "s_set_gpr_idx_off\n\t"
+        "s_waitcnt lgkmcnt(0)\n\t"
+        "s_sub_u32 %[n], %[n], 1\n\t"
+        "s_cmp_eq_u32 %[n], 0\n\t"
+        "s_cbranch_scc1 .Ltile_b_last%=\n\t"
+        "s_load_dwordx16 s[64:79], %[rb], %[ro]\n\t"
+        "s_add_u32 %[ro], %[ro], 64\n\t"
+        "s_lshr_b32 s96, s82, 8\n\t"
+        "s_lshr_b32 s97, s86, 8\n\t"
+        "s_lshr_b32 s98, s90, 8\n\t"
+        "s_lshr_b32 s99, s94, 8\n\t"
+        "s_set_gpr_idx_on s82, gpr_idx(SRC0)\n\t"
+        "v_bfe_u32 %[t0], v48, s96, 8\n\t"
+        "s_set_gpr_idx_idx s86\n\t"
+        "v_bfe_u32 %[t1], v48, s97, 8\n\t"
+        "s_set_gpr_idx_idx s90\n\t"
+        "v_bfe_u32 %[t2], v48, s98, 8\n\t"
+        "s_set_gpr_idx_idx s94\n\t"
+        "v_bfe_u32 %[t3], v48, s99, 8\n\t"
+        "s_set_gpr_idx_off\n\t"
+        "v_lshl_add_u32 %[t0], %[t0], 2, s83\n\t"
+        "v_lshl_add_u32 %[t1], %[t1], 2, s87\n\t"
+        "v_lshl_add_u32 %[t2], %[t2], 2, s91\n\t"
+        "v_lshl_add_u32 %[t3], %[t3], 2, s95\n\t"
+        "ds_read_b32 %[t0], %[t0]\n\t"
+        "ds_read_b32 %[t1], %[t1]\n\t"
+        "ds_read_b32 %[t2], %[t2]\n\t"
+        "ds_read_b32 %[t3], %[t3]\n\t"
+        "s_waitcnt lgkmcnt(0)\n\t"
+        "s_set_gpr_idx_on s80, gpr_idx(SRC2,DST)\n\t"
+        "v_fma_f32 v64, %[t0], s81, v64\n\t"
+        "s_set_gpr_idx_idx s84\n\t"
+        "v_fma_f32 v64, %[t1], s85, v64\n\t"
+        "s_set_gpr_idx_idx s88\n\t"
+        "v_fma_f32 v64, %[t2], s89, v64\n\t"
+        "s_set_gpr_idx_idx s92\n\t"
+        "v_fma_f32 v64, %[t3], s93, v64\n\t"
+        "s_set_gpr_idx_off\n\t"
+        "s_branch .Ltile_a%=\n\t"
+        ".Ltile_a_last%=:\n\t"
+        "s_lshr_b32 s96, s66, 8\n\t"
+        "s_lshr_b32 s97, s70, 8\n\t"
+        "s_lshr_b32 s98, s74, 8\n\t"
+        "s_lshr_b32 s99, s78, 8\n\t"
+        "s_set_gpr_idx_on s66, gpr_idx(SRC0)\n\t"
+        "v_bfe_u32 %[t0], v48, s96, 8\n\t"
+        "s_set_gpr_idx_idx s70\n\t"
+        "v_bfe_u32 %[t1], v48, s97, 8\n\t"
+        "s_set_gpr_idx_idx s74\n\t"
+        "v_bfe_u32 %[t2], v48, s98, 8\n\t"
+        "s_set_gpr_idx_idx s78\n\t"
+        "v_bfe_u32 %[t3], v48, s99, 8\n\t"
+        "s_set_gpr_idx_off\n\t"
+        "v_lshl_add_u32 %[t0], %[t0], 2, s67\n\t"
+        "v_lshl_add_u32 %[t1], %[t1], 2, s71\n\t"
+        "v_lshl_add_u32 %[t2], %[t2], 2, s75\n\t"
+        "v_lshl_add_u32 %[t3], %[t3], 2, s79\n\t"
+        "ds_read_b32 %[t0], %[t0]\n\t"
+        "ds_read_b32 %[t1], %[t1]\n\t"
+        "ds_read_b32 %[t2], %[t2]\n\t"
+        "ds_read_b32 %[t3], %[t3]\n\t"
+        "s_waitcnt lgkmcnt(0)\n\t"
+        "s_set_gpr_idx_on s64, gpr_idx(SRC2,DST)\n\t"
+        "v_fma_f32 v64, %[t0], s65, v64\n\t"
+        "s_set_gpr_idx_idx s68\n\t"
+        "v_fma_f32 v64, %[t1], s69, v64\n\t"
+        "s_set_gpr_idx_idx s72\n\t"
+        "v_fma_f32 v64, %[t2], s73, v64\n\t"
+        "s_set_gpr_idx_idx s76\n\t"
+        "v_fma_f32 v64, %[t3], s77, v64\n\t"
+        "s_set_gpr_idx_off\n\t"
+        "s_branch .Ltile_end%=\n\t"
+        ".Ltile_b_last%=:\n\t"
+        "s_lshr_b32 s96, s82, 8\n\t"
+        "s_lshr_b32 s97, s86, 8\n\t"
+        "s_lshr_b32 s98, s90, 8\n\t"
+        "s_lshr_b32 s99, s94, 8\n\t"
+        "s_set_gpr_idx_on s82, gpr_idx(SRC0)\n\t"
+        "v_bfe_u32 %[t0], v48, s96, 8\n\t"
+        "s_set_gpr_idx_idx s86\n\t"
+        "v_bfe_u32 %[t1], v48, s97, 8\n\t"
+        "s_set_gpr_idx_idx s90\n\t"
+        "v_bfe_u32 %[t2], v48, s98, 8\n\t"
+        "s_set_gpr_idx_idx s94\n\t"
+        "v_bfe_u32 %[t3], v48, s99, 8\n\t"
+        "s_set_gpr_idx_off\n\t"
+        "v_lshl_add_u32 %[t0], %[t0], 2, s83\n\t"
+        "v_lshl_add_u32 %[t1], %[t1], 2, s87\n\t"
+        "v_lshl_add_u32 %[t2], %[t2], 2, s91\n\t"
+        "v_lshl_add_u32 %[t3], %[t3], 2, s95\n\t"
+        "ds_read_b32 %[t0], %[t0]\n\t"
+        "ds_read_b32 %[t1], %[t1]\n\t"
+        "ds_read_b32 %[t2], %[t2]\n\t"
+        "ds_read_b32 %[t3], %[t3]\n\t"
+        "s_waitcnt lgkmcnt(0)\n\t"
+        "s_set_gpr_idx_on s80, gpr_idx(SRC2,DST)\n\t"
+        "v_fma_f32 v64, %[t0], s81, v64\n\t"
+        "s_set_gpr_idx_idx s84\n\t"
+        "v_fma_f32 v64, %[t1], s85, v64\n\t"
+        "s_set_gpr_idx_idx s88\n\t"
+        "v_fma_f32 v64, %[t2], s89, v64\n\t"
+        "s_set_gpr_idx_idx s92\n\t"
+        "v_fma_f32 v64, %[t3], s93, v64\n\t"
+        "s_set_gpr_idx_off\n\t"
+        ".Ltile_end%=:\n\t"
+        "s_mov_b64 exec, %[ex]\n\t"
+        ".Ltile_done%=:\n\t"
+        : [t0] "=&v"(t0), [t1] "=&v"(t1), [t2] "=&v"(t2), [t3] "=&v"(t3), [ex] "=&s"(ex),
+          [ro] "+s"(ro), [n] "+s"(n), "+{v[48:63]}"(selv), "+{v[64:95]}"(acc0),
+          "+{v[96:127]}"(acc1)
+        : [rb] "s"(rb), [hm] "s"(half_mask)
+        : "memory", "scc", "s64", "s65", "s66", "s67", "s68", "s69", "s70", "s71", "s72", "s73", "s74", "s75", "s76", "s77", "s78", "s79", "s80", "s81", "s82", "s83", "s84", "s85", "s86", "s87", "s88", "s89", "s90", "s91", "s92", "s93", "s94", "s95", "s96", "s97", "s98", "s99");
+}
+
+__device__ __forceinline__ tile_hdr_t tile_load_hdr(const tile_hdr_t *p)
+{
+    tile_hdr_t h;
+    asm volatile("global_load_dwordx4 %0, %1, off" : "=v"(h) : "v"(p) : "memory");
+    return h;
+}
+
+// pulls a line range into L2; the destination register stays live (the
+// caller keeps `d` in every later wait) so nothing else lands in it while the
+// load is in flight
+__device__ __forceinline__ void tile_prefetch(const uint32_t *p, uint32_t &d)
+{
+    asm volatile("global_load_dword %0, %1, off" : "+v"(d) : "v"(p) : "memory");
+}
+
+__global__ __launch_bounds__(kTileWaves * kWave) void bwd_tile_kernel(
+    const tile_hdr_t *__restrict__ hdrs, const int64_t *__restrict__ hdr_start,
+    const uint32_t *__restrict__ recs, const int64_t *__restrict__ rec_start,
+    const int32_t *__restrict__ num_chunks, const float *__restrict__ grad,
+    const float *__restrict__ zero_row, const uint8_t *__restrict__ sel, int num_cols,
+    int group_size, int splits, float *__restrict__ dxs, float *__restrict__ part)
+{
+    __shared__ __attribute__((aligned(16))) float tb[3 * kTileBufRows * kMaxDim];
+    const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int lane = lane_id(), half = lane >> 5, ent = lane & 31;
+    const int split = blockIdx.x % splits, grp = blockIdx.x / splits;
+    const int d0 = grp * group_size;
+    const int nd = min(group_size, num_cols - d0);
+    // selectors of the group's destinations, staged through LDS (tb is free
+    // until the first DMA); slot s = 4t + b of this wave holds destination
+    // (2s + half) * 16 + wv, byte b of selector word t
+    {
+        uint8_t *sb = reinterpret_cast<uint8_t *>(tb);
+        for (int i = threadIdx.x; i < 128 * kTileWaves * 2; i += kTileWaves * kWave) {
+            const int j = i >> 1;
+            uint4 v = {0u, 0u, 0u, 0u};
+            if (j < nd) v = *reinterpret_cast<const uint4 *>(sel + (size_t)(d0 + j) * 32 + (i & 1) * 16);
+            *reinterpret_cast<uint4 *>(sb + (size_t)i * 16) = v;
+        }
+        __syncthreads();
+    }
+    tile_sel_t selv;
+#pragma unroll
+    for (int t = 0; t < 16; ++t) {
+        const uint8_t *sb = reinterpret_cast<const uint8_t *>(tb);
+        uint32_t word = 0;
+#pragma unroll
+        for (int b = 0; b < 4; ++b)
+            word |= (uint32_t)sb[((2 * (4 * t + b) + half) * kTileWaves + wv) * 32 + ent] << (8 * b);
+        selv[t] = word;
+        asm volatile("" ::: "memory");  // four LDS reads in flight at a time
+    }
+    __syncthreads();
+    tile_acc_t acc0 = 0.f, acc1 = 0.f;
+    const uint32_t tb_base = (uint32_t)reinterpret_cast<uintptr_t>(tb);
+    const int bw = blockIdx.x * kTileWaves + wv;
+    const tile_hdr_t *hs = hdrs + hdr_start[bw];
+    const uint32_t *rb = recs + 4 * rec_start[bw];
+    uint32_t ro = 0;  // byte offset of the next record group in this wave's stream
+    const int nch = num_chunks[blockIdx.x];
+    auto dma = [&](int c, int r0, int r1, int r2) {
+        const uint32_t buf = tb_base + (uint32_t)(c % 3) * kTileBufRows * 1024u;
+        const int rows[3] = {r0, r1, r2};
+#pragma unroll
+        for (int i = 0; i < 3; ++i) {
+            const int r = __builtin_amdgcn_readfirstlane(rows[i]);
+            const float *src = r >= 0 ? grad + (size_t)r * kMaxDim : zero_row;
+            tile_glds(src + lane * 4,
+                      __builtin_amdgcn_readfirstlane(buf + (uint32_t)(wv * 3 + i) * 1024u));
+        }
+    };
+    // records about 1 KB ahead pulled into L2 for the s_loads (one load per chunk)
+    uint32_t pf = 0;
+    auto prefetch = [&]() { tile_prefetch(rb + (ro >> 2) + 256 + lane * 4, pf); };
+    // header e(i) = {n0 | n1 << 16 of chunk i-2, the wave's DMA rows of chunk i};
+    // queue: H(0); per "iteration" i = -2, -1, 0, ...: DMA(i+2), H(i+3), prefetch
+    const tile_hdr_t e0 = hs[0], e1 = hs[1];
+    tile_hdr_t h0 = tile_load_hdr(hs + 2);
+    dma(0, e0.y, e0.z, e0.w);
+    tile_hdr_t h1 = tile_load_hdr(hs + 3);
+    prefetch();
+    dma(1, e1.y, e1.z, e1.w);
+    tile_hdr_t h2 = tile_load_hdr(hs + 4);
+    prefetch();
+    auto step = [&](int c, tile_hdr_t &h) {
+        // this wave's DMA of chunk c and header of chunk c landed; after the
+        // barrier everyone's have, and chunk c-1's buffer is free
+        asm volatile("s_waitcnt vmcnt(7)\n\ts_barrier" : "+v"(h), "+v"(pf)::"memory");
+        const uint32_t cnt = (uint32_t)__builtin_amdgcn_readfirstlane(h.x);
+        dma(c + 2, __builtin_amdgcn_readfirstlane(h.y), __builtin_amdgcn_readfirstlane(h.z),
+            __builtin_amdgcn_readfirstlane(h.w));
+        h = tile_load_hdr(hs + c + 5);
+        prefetch();
+        tile_half(rb, ro, (cnt & 0xffffu) >> 2, 0x00000000ffffffffull, selv, acc0, acc1);
+        tile_half(rb, ro, cnt >> 18, 0xffffffff00000000ull, selv, acc0, acc1);
+    };
+    for (int c = 0; c < nch; c += 3) {
+        step(c, h0);
+        if (c + 1 < nch) step(c + 1, h1);
+        if (c + 2 < nch) step(c + 2, h2);
+    }
+    asm volatile("s_waitcnt vmcnt(0)" : "+v"(pf), "+v"(h0), "+v"(h1), "+v"(h2)::"memory");
+    float *out = split == 0 ? dxs : part + (size_t)(split - 1) * num_cols * 32;
+#pragma unroll
+    for (int s = 0; s < 64; ++s) {
+        const int j = (2 * s + half) * kTileWaves + wv;
+        if (j < nd) out[(size_t)(d0 + j) * 32 + ent] = s < 32 ? acc0[s] : acc1[s - 32];
+    }
+}
+
+// dxs += sum of the partial rows of source ranges 1 .. splits-1
+__global__ __launch_bounds__(kBlock) void tile_combine_kernel(float *__restrict__ dxs,
+                                                              const float *__restrict__ part,
+                                                              int nparts, int64_t n4)
+{
+    for (int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x; i < n4;
+         i += (int64_t)gridDim.x * kBlock) {
+        f4 a = reinterpret_cast<f4 *>(dxs)[i];
+        for (int p = 0; p < nparts; ++p) a += reinterpret_cast<const f4 *>(part)[(int64_t)p * n4 + i];
+        reinterpret_cast<f4 *>(dxs)[i] = a;
+    }
+}
+
 template <int K>
 __global__ __launch_bounds__(kBlock) void cbsr_pack_kernel(const float *__restrict__ data,
                                                            const uint8_t *__restrict__ sel,
@@ -2517,6 +2858,39 @@ int maxk_sspmm_backward_local_rel8(const int32_t *seg_edge_off, int num_segments
         if (rc) return rc;
     }
     return MAXK_OK;
+}
+
+int maxk_sspmm_backward_tile(const void *headers, const int64_t *header_start,
+                             const void *records, const int64_t *record_start,
+                             const int32_t *num_chunks, int num_groups, int splits,
+                             int group_size, const float *grad, const float *zero_row,
+                             const uint8_t *cbsr_sel, int num_rows, int num_cols, int dim_origin,
+                             int dim_k, float *dxs, float *part, void *stream)
+{
+    if (dim_k != 32 || dim_origin != kMaxDim) return MAXK_E_DIM;
+    if (!headers || !header_start || !records || !record_start || !num_chunks || !grad ||
+        !zero_row || !cbsr_sel || !dxs || num_groups < 1 || splits < 1 || group_size < 1 ||
+        group_size > 128 * kTileWaves || num_rows < 1 || num_cols < 1 ||
+        (int64_t)num_groups * group_size < num_cols || (splits > 1 && !part))
+        return MAXK_E_ARG;
+    if ((reinterpret_cast<uintptr_t>(headers) | reinterpret_cast<uintptr_t>(records) |
+         reinterpret_cast<uintptr_t>(grad) | reinterpret_cast<uintptr_t>(zero_row) |
+         reinterpret_cast<uintptr_t>(dxs) | reinterpret_cast<uintptr_t>(part) |
+         reinterpret_cast<uintptr_t>(cbsr_sel)) & 15)
+        return MAXK_E_ARG;
+    hipStream_t st = as_stream(stream);
+    hipLaunchKernelGGL(bwd_tile_kernel, dim3((unsigned)(num_groups * splits)),
+                       dim3(kTileWaves * kWave), 0, st,
+                       reinterpret_cast<const tile_hdr_t *>(headers), header_start,
+                       reinterpret_cast<const uint32_t *>(records), record_start, num_chunks, grad,
+                       zero_row, cbsr_sel, num_cols, group_size, splits, dxs, part);
+    int rc = launch_status();
+    if (rc || splits == 1) return rc;
+    const int64_t n4 = (int64_t)num_cols * 8;
+    const int64_t blocks = ceil_div(n4, kBlock);
+    hipLaunchKernelGGL(tile_combine_kernel, dim3((unsigned)(blocks < 4096 ? blocks : 4096)),
+                       dim3(kBlock), 0, st, dxs, part, splits - 1, n4);
+    return launch_status();
 }
 
 int maxk_segment_rows_add(const float *src, int width, const int64_t *order,

@@ -1,0 +1,124 @@
+"""TILE backward: the plan format (CPU, replayed by spgemm_new_amd.tile.emulate
+against the float64 oracle) and the kernel (GPU, against the oracle and the
+other backward algorithms)."""
+import numpy as np
+import pytest
+import torch
+
+from spgemm_new_amd import tile
+
+TOL = 1e-4  # fp32 summation order vs the float64 oracle (north_star tolerance)
+
+
+def _graph(V, C, avg_deg, seed, hub_rows=0):
+    rng = np.random.default_rng(seed)
+    deg = rng.poisson(avg_deg, V).astype(np.int64)
+    if hub_rows:
+        deg[:hub_rows] = min(C, avg_deg * 20)
+    indptr = np.zeros(V + 1, np.int64)
+    indptr[1:] = np.cumsum(deg)
+    idx = np.concatenate([np.sort(rng.choice(C, size=d, replace=False)) for d in deg]) \
+        if deg.sum() else np.zeros(0, np.int64)
+    vals = rng.uniform(0, 1, idx.size).astype(np.float32)
+    return indptr.astype(np.int32), idx.astype(np.int32), vals
+
+
+def _inputs(V, C, seed, k=32, h=256):
+    rng = np.random.default_rng(seed + 1)
+    grad = rng.uniform(-1, 1, (V, h)).astype(np.float32)
+    sel = np.stack([np.sort(rng.choice(h, k, replace=False)) for _ in range(C)]).astype(np.uint8)
+    return grad, sel
+
+
+@pytest.mark.parametrize("V,C,deg,shape,hubs", [
+    (300, 300, 12, None, 0),           # one group, splits up to 8, several chunks
+    (800, 800, 6, None, 12),           # hub rows: chunks cut short where records pile up
+    (500, 2600, 9, None, 0),           # two groups (> 2048 columns)
+    (700, 900, 20, (3, 300, 2), 0),    # forced: 3 groups of 300, 2 source ranges
+    (200, 64, 4, (1, 64, 1), 0),       # few destinations, one range
+])
+def test_plan_emulated_matches_oracle(oracle, V, C, deg, shape, hubs):
+    indptr, idx, vals = _graph(V, C, deg, seed=V + C, hub_rows=hubs)
+    grad, sel = _inputs(V, C, seed=V)
+    plan = tile.build(torch.from_numpy(indptr), torch.from_numpy(idx), torch.from_numpy(vals),
+                      V, C, cus=16, shape=shape)
+    assert plan is not None
+    got = tile.emulate(plan, torch.from_numpy(grad), torch.from_numpy(sel)).numpy()
+    ref = oracle.np_backward(indptr, idx, vals, grad, sel)
+    assert oracle.parity_error(got, ref) < TOL
+
+
+def test_plan_invariants():
+    V, C = 400, 1000
+    indptr, idx, vals = _graph(V, C, 15, seed=3)
+    plan = tile.build(torch.from_numpy(indptr), torch.from_numpy(idx), torch.from_numpy(vals),
+                      V, C, cus=8)
+    G, GS, NS = plan["num_groups"], plan["group_size"], plan["splits"]
+    assert G * GS >= C and GS <= tile.MAX_GROUP
+    hdrs, recs = plan["headers"], plan["records"]
+    hs, rs = plan["header_start"].tolist(), plan["record_start"].tolist()
+    nch = plan["num_chunks"].tolist()
+    n_real = 0
+    for b in range(G * NS):
+        for wv in range(tile.WAVES):
+            ro = rs[b * tile.WAVES + wv]
+            for c in range(nch[b] + 2):
+                e = hdrs[hs[b * tile.WAVES + wv] + c]
+                assert all(int(r) == -1 or 0 <= int(r) < V for r in e[1:])
+                if c >= 2:
+                    n0, n1 = int(e[0]) & 0xFFFF, int(e[0]) >> 16
+                    assert n0 % 4 == 0 and n1 % 4 == 0
+                    seg = recs[ro: ro + n0 + n1]
+                    real = seg[:, 1] != 0
+                    n_real += int(real.sum())
+                    # real records read rows of the chunk's own buffer
+                    rowf = seg[real][:, 3] // 1024
+                    assert bool(((rowf // tile.BUF_ROWS) == (c - 2) % 3).all())
+                    ro += n0 + n1
+    assert n_real == int((torch.from_numpy(vals) != 0).sum())
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("V,deg", [(3000, 40), (9000, 120)])
+def test_tile_backward_gpu_matches_oracle(dev, oracle, V, deg):
+    import spgemm_new_amd as S
+    from spgemm_new_amd import _lib
+    indptr, idx, vals = _graph(V, V, deg, seed=V)
+    grad, sel = _inputs(V, V, seed=V)
+    g = S.MaxKGraph(torch.from_numpy(indptr).to(dev), torch.from_numpy(idx).to(dev),
+                    torch.from_numpy(vals).to(dev))
+    assert g.tile_plan() is not None
+    G = torch.from_numpy(grad).to(dev)
+    sl = torch.from_numpy(sel).to(dev)
+    got = g.backward(G, sl, algo=_lib.MAXK_BWD_TILE)
+    torch.cuda.synchronize()
+    assert g.last_bwd_algo == "tile"
+    ref = oracle.np_backward(indptr, idx, vals, grad, sel)
+    assert oracle.parity_error(got.cpu().numpy(), ref) < TOL
+    # deterministic, and equal (to fp32 order) to the other algorithms
+    again = g.backward(G, sl, algo=_lib.MAXK_BWD_TILE)
+    assert torch.equal(got, again)
+    loc = g.backward(G, sl, algo=_lib.MAXK_BWD_LOCAL)
+    assert (got - loc).abs().max().item() <= 1e-4 * max(1.0, loc.abs().max().item())
+
+
+@pytest.mark.gpu
+def test_tile_backward_gpu_groups_and_zero_rows(dev, oracle):
+    """Several destination groups (> 2048 columns), columns without in-edges,
+    rows without out-edges, and G holding inf/NaN only in rows with no edges."""
+    import spgemm_new_amd as S
+    from spgemm_new_amd import _lib
+    V = 5000
+    indptr, idx, vals = _graph(V, V, 25, seed=7)
+    deg = np.diff(indptr)
+    grad, sel = _inputs(V, V, seed=7)
+    empty_rows = np.nonzero(deg == 0)[0]
+    if empty_rows.size:
+        grad[empty_rows[0], :] = np.inf
+    g = S.MaxKGraph(torch.from_numpy(indptr).to(dev), torch.from_numpy(idx).to(dev),
+                    torch.from_numpy(vals).to(dev))
+    got = g.backward(torch.from_numpy(grad).to(dev), torch.from_numpy(sel).to(dev),
+                     algo=_lib.MAXK_BWD_TILE).cpu().numpy()
+    ref = oracle.np_backward(indptr, idx, vals, grad, sel)
+    assert np.isfinite(got).all()
+    assert oracle.parity_error(got, ref) < TOL
