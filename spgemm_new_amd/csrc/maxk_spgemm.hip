@@ -1780,6 +1780,7 @@ constexpr int kTilePro = 4;
 typedef float tile_acc_t __attribute__((ext_vector_type(32)));
 typedef unsigned tile_sel_t __attribute__((ext_vector_type(16)));
 typedef int tile_hdr_t __attribute__((ext_vector_type(4)));
+typedef uint32_t tile_g16_t __attribute__((ext_vector_type(16)));
 
 __device__ __forceinline__ void tile_glds(const float *g, uint32_t lds_byte)
 {
@@ -1792,34 +1793,53 @@ __device__ __forceinline__ void tile_glds(const float *g, uint32_t lds_byte)
 }
 
 
-// Record i of a half-list: 4 dwords {slot, value bits, selector word |
-// (bit offset of the selector byte) << 8, LDS byte address of the staged
-// gradient row}.  One asm loop per half-list: exec narrowed to the half,
-// records read 4 at a time into SGPRs (s_load, the next group in flight while
-// the current one runs), selector words and slot registers picked by
-// s_set_gpr_idx.  The compiler sees neither a divergent branch nor an indexed
-// register, so the pinned slot (v64..v127) and selector (v48..v63) registers
-// stay in place; s64..s99 are the loop's.
-__device__ __forceinline__ void tile_half(const uint32_t *rb, uint32_t &ro, uint32_t groups,
-                                          uint64_t half_mask, tile_sel_t &selv, tile_acc_t &acc0,
-                                          tile_acc_t &acc1)
+// Record = 4 dwords {slot, value bits, selector word | (bit offset of the
+// selector byte) << 8, LDS byte address of the staged gradient row}.  One asm
+// loop per chunk: records 4 at a time in SGPRs (the first group loaded by the
+// caller before the chunk's barrier, each next group by s_load while the
+// current one runs), exec on lanes 0-31 for the n0 half-0 groups then on
+// lanes 32-63, selector words and slot registers picked by s_set_gpr_idx.
+// The compiler sees neither a divergent branch nor an indexed register, so
+// the pinned slot (v64..v127) and selector (v48..v63) registers stay in
+// place; s64..s99 are the loop's.
+__device__ __forceinline__ void tile_chunk(const uint32_t *rb, uint32_t cursor, uint32_t groups,
+                                           uint32_t groups0, const tile_g16_t &a,
+                                           tile_sel_t &selv, tile_acc_t &acc0, tile_acc_t &acc1)
 {
-    uint32_t t0, t1, t2, t3, n = groups;
+    uint32_t t0, t1, t2, t3, n = groups, gi, ro = cursor;
     uint64_t ex;
+    const uint64_t lo = 0x00000000ffffffffull, hi = 0xffffffff00000000ull;
     asm volatile(
         "s_cmp_eq_u32 %[n], 0\n\t"
         "s_cbranch_scc1 .Ltile_done%=\n\t"
         "s_mov_b64 %[ex], exec\n\t"
-        "s_mov_b64 exec, %[hm]\n\t"
-        "s_load_dwordx16 s[64:79], %[rb], %[ro]\n\t"
-        "s_add_u32 %[ro], %[ro], 64\n\t"
-        ".Ltile_a%=:\n\t"
+        "s_mov_b32 %[gi], 0\n\t"
         "s_waitcnt lgkmcnt(0)\n\t"
+        "s_mov_b32 s64, %[a0]\n\t"
+        "s_mov_b32 s65, %[a1]\n\t"
+        "s_mov_b32 s66, %[a2]\n\t"
+        "s_mov_b32 s67, %[a3]\n\t"
+        "s_mov_b32 s68, %[a4]\n\t"
+        "s_mov_b32 s69, %[a5]\n\t"
+        "s_mov_b32 s70, %[a6]\n\t"
+        "s_mov_b32 s71, %[a7]\n\t"
+        "s_mov_b32 s72, %[a8]\n\t"
+        "s_mov_b32 s73, %[a9]\n\t"
+        "s_mov_b32 s74, %[a10]\n\t"
+        "s_mov_b32 s75, %[a11]\n\t"
+        "s_mov_b32 s76, %[a12]\n\t"
+        "s_mov_b32 s77, %[a13]\n\t"
+        "s_mov_b32 s78, %[a14]\n\t"
+        "s_mov_b32 s79, %[a15]\n\t"
+        ".Ltile_a%=:\n\t"
         "s_sub_u32 %[n], %[n], 1\n\t"
         "s_cmp_eq_u32 %[n], 0\n\t"
         "s_cbranch_scc1 .Ltile_a_last%=\n\t"
         "s_load_dwordx16 s[80:95], %[rb], %[ro]\n\t"
         "s_add_u32 %[ro], %[ro], 64\n\t"
+        "s_cmp_lt_u32 %[gi], %[n0]\n\t"
+        "s_cselect_b64 exec, %[lo], %[hi]\n\t"
+        "s_add_u32 %[gi], %[gi], 1\n\t"
         "s_lshr_b32 s96, s66, 8\n\t"
         "s_lshr_b32 s97, s70, 8\n\t"
         "s_lshr_b32 s98, s74, 8\n\t"
@@ -1851,12 +1871,14 @@ __device__ __forceinline__ void tile_half(const uint32_t *rb, uint32_t &ro, uint
         "s_set_gpr_idx_idx s76\n\t"
         "v_fma_f32 v64, %[t3], s77, v64\n\t"
         "s_set_gpr_idx_off\n\t"
-        "s_waitcnt lgkmcnt(0)\n\t"
         "s_sub_u32 %[n], %[n], 1\n\t"
         "s_cmp_eq_u32 %[n], 0\n\t"
         "s_cbranch_scc1 .Ltile_b_last%=\n\t"
         "s_load_dwordx16 s[64:79], %[rb], %[ro]\n\t"
         "s_add_u32 %[ro], %[ro], 64\n\t"
+        "s_cmp_lt_u32 %[gi], %[n0]\n\t"
+        "s_cselect_b64 exec, %[lo], %[hi]\n\t"
+        "s_add_u32 %[gi], %[gi], 1\n\t"
         "s_lshr_b32 s96, s82, 8\n\t"
         "s_lshr_b32 s97, s86, 8\n\t"
         "s_lshr_b32 s98, s90, 8\n\t"
@@ -1888,8 +1910,12 @@ __device__ __forceinline__ void tile_half(const uint32_t *rb, uint32_t &ro, uint
         "s_set_gpr_idx_idx s92\n\t"
         "v_fma_f32 v64, %[t3], s93, v64\n\t"
         "s_set_gpr_idx_off\n\t"
+        "s_waitcnt lgkmcnt(0)\n\t"
         "s_branch .Ltile_a%=\n\t"
         ".Ltile_a_last%=:\n\t"
+        "s_cmp_lt_u32 %[gi], %[n0]\n\t"
+        "s_cselect_b64 exec, %[lo], %[hi]\n\t"
+        "s_add_u32 %[gi], %[gi], 1\n\t"
         "s_lshr_b32 s96, s66, 8\n\t"
         "s_lshr_b32 s97, s70, 8\n\t"
         "s_lshr_b32 s98, s74, 8\n\t"
@@ -1923,6 +1949,10 @@ __device__ __forceinline__ void tile_half(const uint32_t *rb, uint32_t &ro, uint
         "s_set_gpr_idx_off\n\t"
         "s_branch .Ltile_end%=\n\t"
         ".Ltile_b_last%=:\n\t"
+        "s_waitcnt lgkmcnt(0)\n\t"
+        "s_cmp_lt_u32 %[gi], %[n0]\n\t"
+        "s_cselect_b64 exec, %[lo], %[hi]\n\t"
+        "s_add_u32 %[gi], %[gi], 1\n\t"
         "s_lshr_b32 s96, s82, 8\n\t"
         "s_lshr_b32 s97, s86, 8\n\t"
         "s_lshr_b32 s98, s90, 8\n\t"
@@ -1958,9 +1988,13 @@ __device__ __forceinline__ void tile_half(const uint32_t *rb, uint32_t &ro, uint
         "s_mov_b64 exec, %[ex]\n\t"
         ".Ltile_done%=:\n\t"
         : [t0] "=&v"(t0), [t1] "=&v"(t1), [t2] "=&v"(t2), [t3] "=&v"(t3), [ex] "=&s"(ex),
-          [ro] "+s"(ro), [n] "+s"(n), "+{v[48:63]}"(selv), "+{v[64:95]}"(acc0),
+          [gi] "=&s"(gi), [ro] "+s"(ro), [n] "+s"(n), "+{v[48:63]}"(selv), "+{v[64:95]}"(acc0),
           "+{v[96:127]}"(acc1)
-        : [rb] "s"(rb), [hm] "s"(half_mask)
+        : [rb] "s"(rb), [n0] "s"(groups0), [lo] "s"(lo), [hi] "s"(hi), [a0] "s"(a[0]),
+          [a1] "s"(a[1]), [a2] "s"(a[2]), [a3] "s"(a[3]), [a4] "s"(a[4]), [a5] "s"(a[5]),
+          [a6] "s"(a[6]), [a7] "s"(a[7]), [a8] "s"(a[8]), [a9] "s"(a[9]), [a10] "s"(a[10]),
+          [a11] "s"(a[11]), [a12] "s"(a[12]), [a13] "s"(a[13]), [a14] "s"(a[14]),
+          [a15] "s"(a[15])
         : "memory", "scc", "s64", "s65", "s66", "s67", "s68", "s69", "s70", "s71", "s72", "s73", "s74", "s75", "s76", "s77", "s78", "s79", "s80", "s81", "s82", "s83", "s84", "s85", "s86", "s87", "s88", "s89", "s90", "s91", "s92", "s93", "s94", "s95", "s96", "s97", "s98", "s99");
 }
 
@@ -2049,6 +2083,9 @@ __global__ __launch_bounds__(kTileWaves * kWave) void bwd_tile_kernel(
     tile_hdr_t h2 = tile_load_hdr(hs + 4);
     prefetch();
     auto step = [&](int c, tile_hdr_t &h) {
+        // the chunk's first record group, in flight across the barrier
+        tile_g16_t a;
+        asm volatile("s_load_dwordx16 %0, %1, %2" : "=s"(a) : "s"(rb), "s"(ro) : "memory");
         // this wave's DMA of chunk c and header of chunk c landed; after the
         // barrier everyone's have, and chunk c-1's buffer is free
         asm volatile("s_waitcnt vmcnt(7)\n\ts_barrier" : "+v"(h), "+v"(pf)::"memory");
@@ -2057,8 +2094,9 @@ __global__ __launch_bounds__(kTileWaves * kWave) void bwd_tile_kernel(
             __builtin_amdgcn_readfirstlane(h.w));
         h = tile_load_hdr(hs + c + 5);
         prefetch();
-        tile_half(rb, ro, (cnt & 0xffffu) >> 2, 0x00000000ffffffffull, selv, acc0, acc1);
-        tile_half(rb, ro, cnt >> 18, 0xffffffff00000000ull, selv, acc0, acc1);
+        const uint32_t g0n = (cnt & 0xffffu) >> 2, gn = g0n + (cnt >> 18);
+        tile_chunk(rb, ro + 64, gn, g0n, a, selv, acc0, acc1);
+        ro += 64 * gn;
     };
     for (int c = 0; c < nch; c += 3) {
         step(c, h0);
