@@ -38,7 +38,7 @@ def parse():
     p.add_argument("--k", type=int, default=32)
     p.add_argument("--h", type=int, default=256)
     p.add_argument("--seed", type=int, default=123)
-    p.add_argument("--bwd-algo", default="auto", choices=["auto", "atomic", "staged", "local"])
+    p.add_argument("--bwd-algo", default="auto", choices=["auto", "atomic", "staged", "local", "tile"])
     p.add_argument("--panel-cost", type=int, default=None)
     p.add_argument("--row-cost", type=int, default=None)
     p.add_argument("--no-cpu-baseline", action="store_true")
@@ -144,6 +144,8 @@ def pmc_traffic(key, call, algo=None, bands=1):
         parts = [k.get("fwd_panel_kernel"), k.get("carry_fixup_owner_kernel", fix)]
     elif algo == "local":
         parts = [None if "bwd_local_kernel" not in k else k["bwd_local_kernel"] * bands]
+    elif algo == "tile":
+        parts = [k.get("bwd_tile_kernel"), k.get("tile_combine_kernel", 0.0)]
     elif algo == "staged":
         parts = [k.get("bwd_panel_kernel"), k.get("bwd_segsum_kernel"), fix]
     else:
@@ -365,7 +367,8 @@ def main():
     log(f"[bench] graph {args.graph} V={V} E={E} built in {time.time() - t0:.1f}s")
 
     algo = {"auto": _lib.MAXK_BWD_AUTO, "atomic": _lib.MAXK_BWD_ATOMIC,
-            "staged": _lib.MAXK_BWD_STAGED, "local": _lib.MAXK_BWD_LOCAL}[args.bwd_algo]
+            "staged": _lib.MAXK_BWD_STAGED, "local": _lib.MAXK_BWD_LOCAL,
+            "tile": _lib.MAXK_BWD_TILE}[args.bwd_algo]
     kw = {}
     if args.panel_cost:
         kw["panel_cost"] = args.panel_cost

@@ -1806,14 +1806,15 @@ __device__ __forceinline__ void tile_chunk(const uint32_t *rb, uint32_t cursor, 
                                            uint32_t groups0, const tile_g16_t &a,
                                            tile_sel_t &selv, tile_acc_t &acc0, tile_acc_t &acc1)
 {
-    uint32_t t0, t1, t2, t3, n = groups, gi, ro = cursor;
+    uint32_t t0, t1, t2, t3, n = 0u - groups, m = 0u - groups0, ro = cursor;
     uint64_t ex;
     const uint64_t lo = 0x00000000ffffffffull, hi = 0xffffffff00000000ull;
     asm volatile(
         "s_cmp_eq_u32 %[n], 0\n\t"
         "s_cbranch_scc1 .Ltile_done%=\n\t"
         "s_mov_b64 %[ex], exec\n\t"
-        "s_mov_b32 %[gi], 0\n\t"
+        "s_cmp_eq_u32 %[m], 0\n\t"
+        "s_cselect_b64 exec, %[hi], %[lo]\n\t"
         "s_waitcnt lgkmcnt(0)\n\t"
         "s_mov_b32 s64, %[a0]\n\t"
         "s_mov_b32 s65, %[a1]\n\t"
@@ -1832,14 +1833,10 @@ __device__ __forceinline__ void tile_chunk(const uint32_t *rb, uint32_t cursor, 
         "s_mov_b32 s78, %[a14]\n\t"
         "s_mov_b32 s79, %[a15]\n\t"
         ".Ltile_a%=:\n\t"
-        "s_sub_u32 %[n], %[n], 1\n\t"
-        "s_cmp_eq_u32 %[n], 0\n\t"
+        "s_add_u32 %[n], %[n], 1\n\t"
         "s_cbranch_scc1 .Ltile_a_last%=\n\t"
         "s_load_dwordx16 s[80:95], %[rb], %[ro]\n\t"
         "s_add_u32 %[ro], %[ro], 64\n\t"
-        "s_cmp_lt_u32 %[gi], %[n0]\n\t"
-        "s_cselect_b64 exec, %[lo], %[hi]\n\t"
-        "s_add_u32 %[gi], %[gi], 1\n\t"
         "s_lshr_b32 s96, s66, 8\n\t"
         "s_lshr_b32 s97, s70, 8\n\t"
         "s_lshr_b32 s98, s74, 8\n\t"
@@ -1871,14 +1868,12 @@ __device__ __forceinline__ void tile_chunk(const uint32_t *rb, uint32_t cursor, 
         "s_set_gpr_idx_idx s76\n\t"
         "v_fma_f32 v64, %[t3], s77, v64\n\t"
         "s_set_gpr_idx_off\n\t"
-        "s_sub_u32 %[n], %[n], 1\n\t"
-        "s_cmp_eq_u32 %[n], 0\n\t"
+        "s_add_u32 %[m], %[m], 1\n\t"
+        "s_cselect_b64 exec, %[hi], exec\n\t"
+        "s_add_u32 %[n], %[n], 1\n\t"
         "s_cbranch_scc1 .Ltile_b_last%=\n\t"
         "s_load_dwordx16 s[64:79], %[rb], %[ro]\n\t"
         "s_add_u32 %[ro], %[ro], 64\n\t"
-        "s_cmp_lt_u32 %[gi], %[n0]\n\t"
-        "s_cselect_b64 exec, %[lo], %[hi]\n\t"
-        "s_add_u32 %[gi], %[gi], 1\n\t"
         "s_lshr_b32 s96, s82, 8\n\t"
         "s_lshr_b32 s97, s86, 8\n\t"
         "s_lshr_b32 s98, s90, 8\n\t"
@@ -1910,12 +1905,11 @@ __device__ __forceinline__ void tile_chunk(const uint32_t *rb, uint32_t cursor, 
         "s_set_gpr_idx_idx s92\n\t"
         "v_fma_f32 v64, %[t3], s93, v64\n\t"
         "s_set_gpr_idx_off\n\t"
+        "s_add_u32 %[m], %[m], 1\n\t"
+        "s_cselect_b64 exec, %[hi], exec\n\t"
         "s_waitcnt lgkmcnt(0)\n\t"
         "s_branch .Ltile_a%=\n\t"
         ".Ltile_a_last%=:\n\t"
-        "s_cmp_lt_u32 %[gi], %[n0]\n\t"
-        "s_cselect_b64 exec, %[lo], %[hi]\n\t"
-        "s_add_u32 %[gi], %[gi], 1\n\t"
         "s_lshr_b32 s96, s66, 8\n\t"
         "s_lshr_b32 s97, s70, 8\n\t"
         "s_lshr_b32 s98, s74, 8\n\t"
@@ -1950,9 +1944,6 @@ __device__ __forceinline__ void tile_chunk(const uint32_t *rb, uint32_t cursor, 
         "s_branch .Ltile_end%=\n\t"
         ".Ltile_b_last%=:\n\t"
         "s_waitcnt lgkmcnt(0)\n\t"
-        "s_cmp_lt_u32 %[gi], %[n0]\n\t"
-        "s_cselect_b64 exec, %[lo], %[hi]\n\t"
-        "s_add_u32 %[gi], %[gi], 1\n\t"
         "s_lshr_b32 s96, s82, 8\n\t"
         "s_lshr_b32 s97, s86, 8\n\t"
         "s_lshr_b32 s98, s90, 8\n\t"
@@ -1988,9 +1979,9 @@ __device__ __forceinline__ void tile_chunk(const uint32_t *rb, uint32_t cursor, 
         "s_mov_b64 exec, %[ex]\n\t"
         ".Ltile_done%=:\n\t"
         : [t0] "=&v"(t0), [t1] "=&v"(t1), [t2] "=&v"(t2), [t3] "=&v"(t3), [ex] "=&s"(ex),
-          [gi] "=&s"(gi), [ro] "+s"(ro), [n] "+s"(n), "+{v[48:63]}"(selv), "+{v[64:95]}"(acc0),
+          [m] "+s"(m), [ro] "+s"(ro), [n] "+s"(n), "+{v[48:63]}"(selv), "+{v[64:95]}"(acc0),
           "+{v[96:127]}"(acc1)
-        : [rb] "s"(rb), [n0] "s"(groups0), [lo] "s"(lo), [hi] "s"(hi), [a0] "s"(a[0]),
+        : [rb] "s"(rb), [lo] "s"(lo), [hi] "s"(hi), [a0] "s"(a[0]),
           [a1] "s"(a[1]), [a2] "s"(a[2]), [a3] "s"(a[3]), [a4] "s"(a[4]), [a5] "s"(a[5]),
           [a6] "s"(a[6]), [a7] "s"(a[7]), [a8] "s"(a[8]), [a9] "s"(a[9]), [a10] "s"(a[10]),
           [a11] "s"(a[11]), [a12] "s"(a[12]), [a13] "s"(a[13]), [a14] "s"(a[14]),
