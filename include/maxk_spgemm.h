@@ -272,7 +272,7 @@ int maxk_sspmm_backward_local_rel8(const int32_t *seg_edge_off, int num_segments
  * Inputs from the plan (spgemm_new_amd/tile.py; format in csrc/maxk_spgemm.hip
  * above bwd_tile_kernel), one stream per (workgroup, wave) w = b * 16 + wave:
  * headers int32[.., 4] from header_start[w] (16-B aligned), records
- * int32[.., 4] from record_start[w] (16-B aligned, padded by 2 KB);
+ * int32[.., 2] from record_start[w] (16-B aligned, padded by 4 KB);
  * num_chunks int32[num_groups * splits]; zero_row: 1 KB of zeros (16-B
  * aligned).  part: fp32[(splits - 1) * num_cols * 32] scratch (NULL when
  * splits == 1).  Writes every element of dxs; same result as the other

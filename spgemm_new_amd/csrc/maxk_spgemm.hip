@@ -1793,67 +1793,129 @@ __device__ __forceinline__ void tile_glds(const float *g, uint32_t lds_byte)
 }
 
 
-// Record = 4 dwords {slot, value bits, selector word | (bit offset of the
-// selector byte) << 8, LDS byte address of the staged gradient row}.  One asm
-// loop per chunk: records 4 at a time in SGPRs (the first group loaded by the
-// caller before the chunk's barrier, each next group by s_load while the
-// current one runs), exec on lanes 0-31 for the n0 half-0 groups then on
-// lanes 32-63, selector words and slot registers picked by s_set_gpr_idx.
-// The compiler sees neither a divergent branch nor an indexed register, so
-// the pinned slot (v64..v127) and selector (v48..v63) registers stay in
-// place; s64..s99 are the loop's.
-__device__ __forceinline__ void tile_chunk(const uint32_t *rb, uint32_t cursor, uint32_t groups,
-                                           uint32_t groups0, const tile_g16_t &a,
-                                           tile_sel_t &selv, tile_acc_t &acc0, tile_acc_t &acc1)
+// Record = int32x2 {w = slot | row field << 24, value bits}; the slot
+// register index reads w[7:0], the selector word is w >> 2, the selector
+// byte's bit offset (w << 3) & 24, the staged row's LDS address w >> 14.
+// Four records per step, all in one asm block: exec narrowed to the lane
+// half (lanes 0-31 while half-0 groups remain, counted by m < 0), selector
+// byte = v_bfe_u32 of the selector register picked by s_set_gpr_idx (SRC0),
+// one ds_read_b32, v_fma_f32 into the slot register picked by s_set_gpr_idx
+// (SRC2 | DST).  The compiler sees neither a divergent branch nor an
+// indexed register, so the pinned slot (v64..v127) and selector (v48..v63)
+// registers stay in place.  n = -(groups left), m = -(half-0 groups left):
+// s_add_u32 sets SCC when a count reaches 0.
+__device__ __forceinline__ void tile_group_pre(const uint32_t (&g)[8], uint32_t &n, uint32_t &m,
+                                               tile_sel_t &selv, tile_acc_t &acc0,
+                                               tile_acc_t &acc1)
 {
-    uint32_t t0, t1, t2, t3, n = 0u - groups, m = 0u - groups0, ro = cursor;
+    uint32_t t0, t1, t2, t3;
+    uint64_t ex;
+    const uint64_t lo = 0x00000000ffffffffull, hi = 0xffffffff00000000ull;
+    asm volatile(
+        "s_cmp_eq_u32 %[n], 0\n\t"
+        "s_cbranch_scc1 .Ltile_skip%=\n\t"
+        "s_mov_b64 %[ex], exec\n\t"
+        "s_cmp_lt_i32 %[m], 0\n\t"
+        "s_cselect_b64 exec, %[lo], %[hi]\n\t"
+        "s_waitcnt lgkmcnt(0)\n\t"
+        "s_lshr_b32 s80, %[g0], 2\n\t"
+        "s_lshl_b32 s81, %[g0], 3\n\t"
+        "s_lshr_b32 s82, %[g0], 14\n\t"
+        "s_lshr_b32 s83, %[g2], 2\n\t"
+        "s_lshl_b32 s84, %[g2], 3\n\t"
+        "s_lshr_b32 s85, %[g2], 14\n\t"
+        "s_lshr_b32 s86, %[g4], 2\n\t"
+        "s_lshl_b32 s87, %[g4], 3\n\t"
+        "s_lshr_b32 s88, %[g4], 14\n\t"
+        "s_lshr_b32 s89, %[g6], 2\n\t"
+        "s_lshl_b32 s90, %[g6], 3\n\t"
+        "s_lshr_b32 s91, %[g6], 14\n\t"
+        "s_set_gpr_idx_on s80, gpr_idx(SRC0)\n\t"
+        "v_bfe_u32 %[t0], v48, s81, 8\n\t"
+        "s_set_gpr_idx_idx s83\n\t"
+        "v_bfe_u32 %[t1], v48, s84, 8\n\t"
+        "s_set_gpr_idx_idx s86\n\t"
+        "v_bfe_u32 %[t2], v48, s87, 8\n\t"
+        "s_set_gpr_idx_idx s89\n\t"
+        "v_bfe_u32 %[t3], v48, s90, 8\n\t"
+        "s_set_gpr_idx_off\n\t"
+        "v_lshl_add_u32 %[t0], %[t0], 2, s82\n\t"
+        "v_lshl_add_u32 %[t1], %[t1], 2, s85\n\t"
+        "v_lshl_add_u32 %[t2], %[t2], 2, s88\n\t"
+        "v_lshl_add_u32 %[t3], %[t3], 2, s91\n\t"
+        "ds_read_b32 %[t0], %[t0]\n\t"
+        "ds_read_b32 %[t1], %[t1]\n\t"
+        "ds_read_b32 %[t2], %[t2]\n\t"
+        "ds_read_b32 %[t3], %[t3]\n\t"
+        "s_waitcnt lgkmcnt(0)\n\t"
+        "s_set_gpr_idx_on %[g0], gpr_idx(SRC2,DST)\n\t"
+        "v_fma_f32 v64, %[t0], %[g1], v64\n\t"
+        "s_set_gpr_idx_idx %[g2]\n\t"
+        "v_fma_f32 v64, %[t1], %[g3], v64\n\t"
+        "s_set_gpr_idx_idx %[g4]\n\t"
+        "v_fma_f32 v64, %[t2], %[g5], v64\n\t"
+        "s_set_gpr_idx_idx %[g6]\n\t"
+        "v_fma_f32 v64, %[t3], %[g7], v64\n\t"
+        "s_set_gpr_idx_off\n\t"
+        "s_add_u32 %[m], %[m], 1\n\t"
+        "s_add_u32 %[n], %[n], 1\n\t"
+        "s_mov_b64 exec, %[ex]\n\t"
+        ".Ltile_skip%=:\n\t"
+        : [t0] "=&v"(t0), [t1] "=&v"(t1), [t2] "=&v"(t2), [t3] "=&v"(t3), [ex] "=&s"(ex),
+          [m] "+s"(m), [n] "+s"(n), "+{v[48:63]}"(selv), "+{v[64:95]}"(acc0), "+{v[96:127]}"(acc1)
+        : [lo] "s"(lo), [hi] "s"(hi), [g0] "s"(g[0]), [g1] "s"(g[1]), [g2] "s"(g[2]),
+          [g3] "s"(g[3]), [g4] "s"(g[4]), [g5] "s"(g[5]), [g6] "s"(g[6]), [g7] "s"(g[7])
+        : "memory", "scc", "s80", "s81", "s82", "s83", "s84", "s85", "s86", "s87", "s88", "s89", "s90", "s91");
+}
+
+// the groups after the four loaded before the barrier: s_load, the next group
+// in flight while the current one runs; s64..s91 are the loop's
+__device__ __forceinline__ void tile_group_loop(const uint32_t *rb, uint32_t ro, uint32_t &n,
+                                                uint32_t &m, tile_sel_t &selv, tile_acc_t &acc0,
+                                                tile_acc_t &acc1)
+{
+    uint32_t t0, t1, t2, t3;
     uint64_t ex;
     const uint64_t lo = 0x00000000ffffffffull, hi = 0xffffffff00000000ull;
     asm volatile(
         "s_cmp_eq_u32 %[n], 0\n\t"
         "s_cbranch_scc1 .Ltile_done%=\n\t"
         "s_mov_b64 %[ex], exec\n\t"
-        "s_cmp_eq_u32 %[m], 0\n\t"
-        "s_cselect_b64 exec, %[hi], %[lo]\n\t"
+        "s_cmp_lt_i32 %[m], 0\n\t"
+        "s_cselect_b64 exec, %[lo], %[hi]\n\t"
+        "s_load_dwordx8 s[64:71], %[rb], %[ro]\n\t"
+        "s_add_u32 %[ro], %[ro], 32\n\t"
         "s_waitcnt lgkmcnt(0)\n\t"
-        "s_mov_b32 s64, %[a0]\n\t"
-        "s_mov_b32 s65, %[a1]\n\t"
-        "s_mov_b32 s66, %[a2]\n\t"
-        "s_mov_b32 s67, %[a3]\n\t"
-        "s_mov_b32 s68, %[a4]\n\t"
-        "s_mov_b32 s69, %[a5]\n\t"
-        "s_mov_b32 s70, %[a6]\n\t"
-        "s_mov_b32 s71, %[a7]\n\t"
-        "s_mov_b32 s72, %[a8]\n\t"
-        "s_mov_b32 s73, %[a9]\n\t"
-        "s_mov_b32 s74, %[a10]\n\t"
-        "s_mov_b32 s75, %[a11]\n\t"
-        "s_mov_b32 s76, %[a12]\n\t"
-        "s_mov_b32 s77, %[a13]\n\t"
-        "s_mov_b32 s78, %[a14]\n\t"
-        "s_mov_b32 s79, %[a15]\n\t"
         ".Ltile_a%=:\n\t"
         "s_add_u32 %[n], %[n], 1\n\t"
         "s_cbranch_scc1 .Ltile_a_last%=\n\t"
-        "s_load_dwordx16 s[80:95], %[rb], %[ro]\n\t"
-        "s_add_u32 %[ro], %[ro], 64\n\t"
-        "s_lshr_b32 s96, s66, 8\n\t"
-        "s_lshr_b32 s97, s70, 8\n\t"
-        "s_lshr_b32 s98, s74, 8\n\t"
-        "s_lshr_b32 s99, s78, 8\n\t"
-        "s_set_gpr_idx_on s66, gpr_idx(SRC0)\n\t"
-        "v_bfe_u32 %[t0], v48, s96, 8\n\t"
-        "s_set_gpr_idx_idx s70\n\t"
-        "v_bfe_u32 %[t1], v48, s97, 8\n\t"
-        "s_set_gpr_idx_idx s74\n\t"
-        "v_bfe_u32 %[t2], v48, s98, 8\n\t"
-        "s_set_gpr_idx_idx s78\n\t"
-        "v_bfe_u32 %[t3], v48, s99, 8\n\t"
+        "s_load_dwordx8 s[72:79], %[rb], %[ro]\n\t"
+        "s_add_u32 %[ro], %[ro], 32\n\t"
+        "s_lshr_b32 s80, s64, 2\n\t"
+        "s_lshl_b32 s81, s64, 3\n\t"
+        "s_lshr_b32 s82, s64, 14\n\t"
+        "s_lshr_b32 s83, s66, 2\n\t"
+        "s_lshl_b32 s84, s66, 3\n\t"
+        "s_lshr_b32 s85, s66, 14\n\t"
+        "s_lshr_b32 s86, s68, 2\n\t"
+        "s_lshl_b32 s87, s68, 3\n\t"
+        "s_lshr_b32 s88, s68, 14\n\t"
+        "s_lshr_b32 s89, s70, 2\n\t"
+        "s_lshl_b32 s90, s70, 3\n\t"
+        "s_lshr_b32 s91, s70, 14\n\t"
+        "s_set_gpr_idx_on s80, gpr_idx(SRC0)\n\t"
+        "v_bfe_u32 %[t0], v48, s81, 8\n\t"
+        "s_set_gpr_idx_idx s83\n\t"
+        "v_bfe_u32 %[t1], v48, s84, 8\n\t"
+        "s_set_gpr_idx_idx s86\n\t"
+        "v_bfe_u32 %[t2], v48, s87, 8\n\t"
+        "s_set_gpr_idx_idx s89\n\t"
+        "v_bfe_u32 %[t3], v48, s90, 8\n\t"
         "s_set_gpr_idx_off\n\t"
-        "v_lshl_add_u32 %[t0], %[t0], 2, s67\n\t"
-        "v_lshl_add_u32 %[t1], %[t1], 2, s71\n\t"
-        "v_lshl_add_u32 %[t2], %[t2], 2, s75\n\t"
-        "v_lshl_add_u32 %[t3], %[t3], 2, s79\n\t"
+        "v_lshl_add_u32 %[t0], %[t0], 2, s82\n\t"
+        "v_lshl_add_u32 %[t1], %[t1], 2, s85\n\t"
+        "v_lshl_add_u32 %[t2], %[t2], 2, s88\n\t"
+        "v_lshl_add_u32 %[t3], %[t3], 2, s91\n\t"
         "ds_read_b32 %[t0], %[t0]\n\t"
         "ds_read_b32 %[t1], %[t1]\n\t"
         "ds_read_b32 %[t2], %[t2]\n\t"
@@ -1861,72 +1923,88 @@ __device__ __forceinline__ void tile_chunk(const uint32_t *rb, uint32_t cursor, 
         "s_waitcnt lgkmcnt(0)\n\t"
         "s_set_gpr_idx_on s64, gpr_idx(SRC2,DST)\n\t"
         "v_fma_f32 v64, %[t0], s65, v64\n\t"
+        "s_set_gpr_idx_idx s66\n\t"
+        "v_fma_f32 v64, %[t1], s67, v64\n\t"
         "s_set_gpr_idx_idx s68\n\t"
-        "v_fma_f32 v64, %[t1], s69, v64\n\t"
-        "s_set_gpr_idx_idx s72\n\t"
-        "v_fma_f32 v64, %[t2], s73, v64\n\t"
-        "s_set_gpr_idx_idx s76\n\t"
-        "v_fma_f32 v64, %[t3], s77, v64\n\t"
+        "v_fma_f32 v64, %[t2], s69, v64\n\t"
+        "s_set_gpr_idx_idx s70\n\t"
+        "v_fma_f32 v64, %[t3], s71, v64\n\t"
         "s_set_gpr_idx_off\n\t"
         "s_add_u32 %[m], %[m], 1\n\t"
         "s_cselect_b64 exec, %[hi], exec\n\t"
         "s_add_u32 %[n], %[n], 1\n\t"
         "s_cbranch_scc1 .Ltile_b_last%=\n\t"
-        "s_load_dwordx16 s[64:79], %[rb], %[ro]\n\t"
-        "s_add_u32 %[ro], %[ro], 64\n\t"
-        "s_lshr_b32 s96, s82, 8\n\t"
-        "s_lshr_b32 s97, s86, 8\n\t"
-        "s_lshr_b32 s98, s90, 8\n\t"
-        "s_lshr_b32 s99, s94, 8\n\t"
-        "s_set_gpr_idx_on s82, gpr_idx(SRC0)\n\t"
-        "v_bfe_u32 %[t0], v48, s96, 8\n\t"
+        "s_load_dwordx8 s[64:71], %[rb], %[ro]\n\t"
+        "s_add_u32 %[ro], %[ro], 32\n\t"
+        "s_lshr_b32 s80, s72, 2\n\t"
+        "s_lshl_b32 s81, s72, 3\n\t"
+        "s_lshr_b32 s82, s72, 14\n\t"
+        "s_lshr_b32 s83, s74, 2\n\t"
+        "s_lshl_b32 s84, s74, 3\n\t"
+        "s_lshr_b32 s85, s74, 14\n\t"
+        "s_lshr_b32 s86, s76, 2\n\t"
+        "s_lshl_b32 s87, s76, 3\n\t"
+        "s_lshr_b32 s88, s76, 14\n\t"
+        "s_lshr_b32 s89, s78, 2\n\t"
+        "s_lshl_b32 s90, s78, 3\n\t"
+        "s_lshr_b32 s91, s78, 14\n\t"
+        "s_set_gpr_idx_on s80, gpr_idx(SRC0)\n\t"
+        "v_bfe_u32 %[t0], v48, s81, 8\n\t"
+        "s_set_gpr_idx_idx s83\n\t"
+        "v_bfe_u32 %[t1], v48, s84, 8\n\t"
         "s_set_gpr_idx_idx s86\n\t"
-        "v_bfe_u32 %[t1], v48, s97, 8\n\t"
-        "s_set_gpr_idx_idx s90\n\t"
-        "v_bfe_u32 %[t2], v48, s98, 8\n\t"
-        "s_set_gpr_idx_idx s94\n\t"
-        "v_bfe_u32 %[t3], v48, s99, 8\n\t"
+        "v_bfe_u32 %[t2], v48, s87, 8\n\t"
+        "s_set_gpr_idx_idx s89\n\t"
+        "v_bfe_u32 %[t3], v48, s90, 8\n\t"
         "s_set_gpr_idx_off\n\t"
-        "v_lshl_add_u32 %[t0], %[t0], 2, s83\n\t"
-        "v_lshl_add_u32 %[t1], %[t1], 2, s87\n\t"
-        "v_lshl_add_u32 %[t2], %[t2], 2, s91\n\t"
-        "v_lshl_add_u32 %[t3], %[t3], 2, s95\n\t"
+        "v_lshl_add_u32 %[t0], %[t0], 2, s82\n\t"
+        "v_lshl_add_u32 %[t1], %[t1], 2, s85\n\t"
+        "v_lshl_add_u32 %[t2], %[t2], 2, s88\n\t"
+        "v_lshl_add_u32 %[t3], %[t3], 2, s91\n\t"
         "ds_read_b32 %[t0], %[t0]\n\t"
         "ds_read_b32 %[t1], %[t1]\n\t"
         "ds_read_b32 %[t2], %[t2]\n\t"
         "ds_read_b32 %[t3], %[t3]\n\t"
         "s_waitcnt lgkmcnt(0)\n\t"
-        "s_set_gpr_idx_on s80, gpr_idx(SRC2,DST)\n\t"
-        "v_fma_f32 v64, %[t0], s81, v64\n\t"
-        "s_set_gpr_idx_idx s84\n\t"
-        "v_fma_f32 v64, %[t1], s85, v64\n\t"
-        "s_set_gpr_idx_idx s88\n\t"
-        "v_fma_f32 v64, %[t2], s89, v64\n\t"
-        "s_set_gpr_idx_idx s92\n\t"
-        "v_fma_f32 v64, %[t3], s93, v64\n\t"
+        "s_set_gpr_idx_on s72, gpr_idx(SRC2,DST)\n\t"
+        "v_fma_f32 v64, %[t0], s73, v64\n\t"
+        "s_set_gpr_idx_idx s74\n\t"
+        "v_fma_f32 v64, %[t1], s75, v64\n\t"
+        "s_set_gpr_idx_idx s76\n\t"
+        "v_fma_f32 v64, %[t2], s77, v64\n\t"
+        "s_set_gpr_idx_idx s78\n\t"
+        "v_fma_f32 v64, %[t3], s79, v64\n\t"
         "s_set_gpr_idx_off\n\t"
         "s_add_u32 %[m], %[m], 1\n\t"
         "s_cselect_b64 exec, %[hi], exec\n\t"
         "s_waitcnt lgkmcnt(0)\n\t"
         "s_branch .Ltile_a%=\n\t"
         ".Ltile_a_last%=:\n\t"
-        "s_lshr_b32 s96, s66, 8\n\t"
-        "s_lshr_b32 s97, s70, 8\n\t"
-        "s_lshr_b32 s98, s74, 8\n\t"
-        "s_lshr_b32 s99, s78, 8\n\t"
-        "s_set_gpr_idx_on s66, gpr_idx(SRC0)\n\t"
-        "v_bfe_u32 %[t0], v48, s96, 8\n\t"
-        "s_set_gpr_idx_idx s70\n\t"
-        "v_bfe_u32 %[t1], v48, s97, 8\n\t"
-        "s_set_gpr_idx_idx s74\n\t"
-        "v_bfe_u32 %[t2], v48, s98, 8\n\t"
-        "s_set_gpr_idx_idx s78\n\t"
-        "v_bfe_u32 %[t3], v48, s99, 8\n\t"
+        "s_lshr_b32 s80, s64, 2\n\t"
+        "s_lshl_b32 s81, s64, 3\n\t"
+        "s_lshr_b32 s82, s64, 14\n\t"
+        "s_lshr_b32 s83, s66, 2\n\t"
+        "s_lshl_b32 s84, s66, 3\n\t"
+        "s_lshr_b32 s85, s66, 14\n\t"
+        "s_lshr_b32 s86, s68, 2\n\t"
+        "s_lshl_b32 s87, s68, 3\n\t"
+        "s_lshr_b32 s88, s68, 14\n\t"
+        "s_lshr_b32 s89, s70, 2\n\t"
+        "s_lshl_b32 s90, s70, 3\n\t"
+        "s_lshr_b32 s91, s70, 14\n\t"
+        "s_set_gpr_idx_on s80, gpr_idx(SRC0)\n\t"
+        "v_bfe_u32 %[t0], v48, s81, 8\n\t"
+        "s_set_gpr_idx_idx s83\n\t"
+        "v_bfe_u32 %[t1], v48, s84, 8\n\t"
+        "s_set_gpr_idx_idx s86\n\t"
+        "v_bfe_u32 %[t2], v48, s87, 8\n\t"
+        "s_set_gpr_idx_idx s89\n\t"
+        "v_bfe_u32 %[t3], v48, s90, 8\n\t"
         "s_set_gpr_idx_off\n\t"
-        "v_lshl_add_u32 %[t0], %[t0], 2, s67\n\t"
-        "v_lshl_add_u32 %[t1], %[t1], 2, s71\n\t"
-        "v_lshl_add_u32 %[t2], %[t2], 2, s75\n\t"
-        "v_lshl_add_u32 %[t3], %[t3], 2, s79\n\t"
+        "v_lshl_add_u32 %[t0], %[t0], 2, s82\n\t"
+        "v_lshl_add_u32 %[t1], %[t1], 2, s85\n\t"
+        "v_lshl_add_u32 %[t2], %[t2], 2, s88\n\t"
+        "v_lshl_add_u32 %[t3], %[t3], 2, s91\n\t"
         "ds_read_b32 %[t0], %[t0]\n\t"
         "ds_read_b32 %[t1], %[t1]\n\t"
         "ds_read_b32 %[t2], %[t2]\n\t"
@@ -1934,59 +2012,63 @@ __device__ __forceinline__ void tile_chunk(const uint32_t *rb, uint32_t cursor, 
         "s_waitcnt lgkmcnt(0)\n\t"
         "s_set_gpr_idx_on s64, gpr_idx(SRC2,DST)\n\t"
         "v_fma_f32 v64, %[t0], s65, v64\n\t"
+        "s_set_gpr_idx_idx s66\n\t"
+        "v_fma_f32 v64, %[t1], s67, v64\n\t"
         "s_set_gpr_idx_idx s68\n\t"
-        "v_fma_f32 v64, %[t1], s69, v64\n\t"
-        "s_set_gpr_idx_idx s72\n\t"
-        "v_fma_f32 v64, %[t2], s73, v64\n\t"
-        "s_set_gpr_idx_idx s76\n\t"
-        "v_fma_f32 v64, %[t3], s77, v64\n\t"
+        "v_fma_f32 v64, %[t2], s69, v64\n\t"
+        "s_set_gpr_idx_idx s70\n\t"
+        "v_fma_f32 v64, %[t3], s71, v64\n\t"
         "s_set_gpr_idx_off\n\t"
         "s_branch .Ltile_end%=\n\t"
         ".Ltile_b_last%=:\n\t"
         "s_waitcnt lgkmcnt(0)\n\t"
-        "s_lshr_b32 s96, s82, 8\n\t"
-        "s_lshr_b32 s97, s86, 8\n\t"
-        "s_lshr_b32 s98, s90, 8\n\t"
-        "s_lshr_b32 s99, s94, 8\n\t"
-        "s_set_gpr_idx_on s82, gpr_idx(SRC0)\n\t"
-        "v_bfe_u32 %[t0], v48, s96, 8\n\t"
+        "s_lshr_b32 s80, s72, 2\n\t"
+        "s_lshl_b32 s81, s72, 3\n\t"
+        "s_lshr_b32 s82, s72, 14\n\t"
+        "s_lshr_b32 s83, s74, 2\n\t"
+        "s_lshl_b32 s84, s74, 3\n\t"
+        "s_lshr_b32 s85, s74, 14\n\t"
+        "s_lshr_b32 s86, s76, 2\n\t"
+        "s_lshl_b32 s87, s76, 3\n\t"
+        "s_lshr_b32 s88, s76, 14\n\t"
+        "s_lshr_b32 s89, s78, 2\n\t"
+        "s_lshl_b32 s90, s78, 3\n\t"
+        "s_lshr_b32 s91, s78, 14\n\t"
+        "s_set_gpr_idx_on s80, gpr_idx(SRC0)\n\t"
+        "v_bfe_u32 %[t0], v48, s81, 8\n\t"
+        "s_set_gpr_idx_idx s83\n\t"
+        "v_bfe_u32 %[t1], v48, s84, 8\n\t"
         "s_set_gpr_idx_idx s86\n\t"
-        "v_bfe_u32 %[t1], v48, s97, 8\n\t"
-        "s_set_gpr_idx_idx s90\n\t"
-        "v_bfe_u32 %[t2], v48, s98, 8\n\t"
-        "s_set_gpr_idx_idx s94\n\t"
-        "v_bfe_u32 %[t3], v48, s99, 8\n\t"
+        "v_bfe_u32 %[t2], v48, s87, 8\n\t"
+        "s_set_gpr_idx_idx s89\n\t"
+        "v_bfe_u32 %[t3], v48, s90, 8\n\t"
         "s_set_gpr_idx_off\n\t"
-        "v_lshl_add_u32 %[t0], %[t0], 2, s83\n\t"
-        "v_lshl_add_u32 %[t1], %[t1], 2, s87\n\t"
-        "v_lshl_add_u32 %[t2], %[t2], 2, s91\n\t"
-        "v_lshl_add_u32 %[t3], %[t3], 2, s95\n\t"
+        "v_lshl_add_u32 %[t0], %[t0], 2, s82\n\t"
+        "v_lshl_add_u32 %[t1], %[t1], 2, s85\n\t"
+        "v_lshl_add_u32 %[t2], %[t2], 2, s88\n\t"
+        "v_lshl_add_u32 %[t3], %[t3], 2, s91\n\t"
         "ds_read_b32 %[t0], %[t0]\n\t"
         "ds_read_b32 %[t1], %[t1]\n\t"
         "ds_read_b32 %[t2], %[t2]\n\t"
         "ds_read_b32 %[t3], %[t3]\n\t"
         "s_waitcnt lgkmcnt(0)\n\t"
-        "s_set_gpr_idx_on s80, gpr_idx(SRC2,DST)\n\t"
-        "v_fma_f32 v64, %[t0], s81, v64\n\t"
-        "s_set_gpr_idx_idx s84\n\t"
-        "v_fma_f32 v64, %[t1], s85, v64\n\t"
-        "s_set_gpr_idx_idx s88\n\t"
-        "v_fma_f32 v64, %[t2], s89, v64\n\t"
-        "s_set_gpr_idx_idx s92\n\t"
-        "v_fma_f32 v64, %[t3], s93, v64\n\t"
+        "s_set_gpr_idx_on s72, gpr_idx(SRC2,DST)\n\t"
+        "v_fma_f32 v64, %[t0], s73, v64\n\t"
+        "s_set_gpr_idx_idx s74\n\t"
+        "v_fma_f32 v64, %[t1], s75, v64\n\t"
+        "s_set_gpr_idx_idx s76\n\t"
+        "v_fma_f32 v64, %[t2], s77, v64\n\t"
+        "s_set_gpr_idx_idx s78\n\t"
+        "v_fma_f32 v64, %[t3], s79, v64\n\t"
         "s_set_gpr_idx_off\n\t"
         ".Ltile_end%=:\n\t"
         "s_mov_b64 exec, %[ex]\n\t"
         ".Ltile_done%=:\n\t"
         : [t0] "=&v"(t0), [t1] "=&v"(t1), [t2] "=&v"(t2), [t3] "=&v"(t3), [ex] "=&s"(ex),
-          [m] "+s"(m), [ro] "+s"(ro), [n] "+s"(n), "+{v[48:63]}"(selv), "+{v[64:95]}"(acc0),
+          [ro] "+s"(ro), [m] "+s"(m), [n] "+s"(n), "+{v[48:63]}"(selv), "+{v[64:95]}"(acc0),
           "+{v[96:127]}"(acc1)
-        : [rb] "s"(rb), [lo] "s"(lo), [hi] "s"(hi), [a0] "s"(a[0]),
-          [a1] "s"(a[1]), [a2] "s"(a[2]), [a3] "s"(a[3]), [a4] "s"(a[4]), [a5] "s"(a[5]),
-          [a6] "s"(a[6]), [a7] "s"(a[7]), [a8] "s"(a[8]), [a9] "s"(a[9]), [a10] "s"(a[10]),
-          [a11] "s"(a[11]), [a12] "s"(a[12]), [a13] "s"(a[13]), [a14] "s"(a[14]),
-          [a15] "s"(a[15])
-        : "memory", "scc", "s64", "s65", "s66", "s67", "s68", "s69", "s70", "s71", "s72", "s73", "s74", "s75", "s76", "s77", "s78", "s79", "s80", "s81", "s82", "s83", "s84", "s85", "s86", "s87", "s88", "s89", "s90", "s91", "s92", "s93", "s94", "s95", "s96", "s97", "s98", "s99");
+        : [rb] "s"(rb), [lo] "s"(lo), [hi] "s"(hi)
+        : "memory", "scc", "s64", "s65", "s66", "s67", "s68", "s69", "s70", "s71", "s72", "s73", "s74", "s75", "s76", "s77", "s78", "s79", "s80", "s81", "s82", "s83", "s84", "s85", "s86", "s87", "s88", "s89", "s90", "s91");
 }
 
 __device__ __forceinline__ tile_hdr_t tile_load_hdr(const tile_hdr_t *p)
@@ -2046,7 +2128,7 @@ __global__ __launch_bounds__(kTileWaves * kWave) void bwd_tile_kernel(
     const uint32_t tb_base = (uint32_t)reinterpret_cast<uintptr_t>(tb);
     const int bw = blockIdx.x * kTileWaves + wv;
     const tile_hdr_t *hs = hdrs + hdr_start[bw];
-    const uint32_t *rb = recs + 4 * rec_start[bw];
+    const uint32_t *rb = recs + 2 * rec_start[bw];
     uint32_t ro = 0;  // byte offset of the next record group in this wave's stream
     const int nch = num_chunks[blockIdx.x];
     auto dma = [&](int c, int r0, int r1, int r2) {
@@ -2062,7 +2144,7 @@ __global__ __launch_bounds__(kTileWaves * kWave) void bwd_tile_kernel(
     };
     // records about 1 KB ahead pulled into L2 for the s_loads (one load per chunk)
     uint32_t pf = 0;
-    auto prefetch = [&]() { tile_prefetch(rb + (ro >> 2) + 256 + lane * 4, pf); };
+    auto prefetch = [&]() { tile_prefetch(rb + (ro >> 2) + 128 + lane * 4, pf); };
     // header e(i) = {n0 | n1 << 16 of chunk i-2, the wave's DMA rows of chunk i};
     // queue: H(0); per "iteration" i = -2, -1, 0, ...: DMA(i+2), H(i+3), prefetch
     const tile_hdr_t e0 = hs[0], e1 = hs[1];
@@ -2075,8 +2157,9 @@ __global__ __launch_bounds__(kTileWaves * kWave) void bwd_tile_kernel(
     prefetch();
     auto step = [&](int c, tile_hdr_t &h) {
         // the chunk's first record group, in flight across the barrier
-        tile_g16_t a;
-        asm volatile("s_load_dwordx16 %0, %1, %2" : "=s"(a) : "s"(rb), "s"(ro) : "memory");
+        tile_g16_t pa, pb;
+        asm volatile("s_load_dwordx16 %0, %2, %3\n\ts_load_dwordx16 %1, %2, %4"
+                     : "=&s"(pa), "=&s"(pb) : "s"(rb), "s"(ro), "s"(ro + 64) : "memory");
         // this wave's DMA of chunk c and header of chunk c landed; after the
         // barrier everyone's have, and chunk c-1's buffer is free
         asm volatile("s_waitcnt vmcnt(7)\n\ts_barrier" : "+v"(h), "+v"(pf)::"memory");
@@ -2086,8 +2169,17 @@ __global__ __launch_bounds__(kTileWaves * kWave) void bwd_tile_kernel(
         h = tile_load_hdr(hs + c + 5);
         prefetch();
         const uint32_t g0n = (cnt & 0xffffu) >> 2, gn = g0n + (cnt >> 18);
-        tile_chunk(rb, ro + 64, gn, g0n, a, selv, acc0, acc1);
-        ro += 64 * gn;
+        uint32_t n = 0u - gn, m = 0u - g0n;
+        const uint32_t ga[8] = {pa[0], pa[1], pa[2], pa[3], pa[4], pa[5], pa[6], pa[7]};
+        const uint32_t gb[8] = {pa[8], pa[9], pa[10], pa[11], pa[12], pa[13], pa[14], pa[15]};
+        const uint32_t gc[8] = {pb[0], pb[1], pb[2], pb[3], pb[4], pb[5], pb[6], pb[7]};
+        const uint32_t gd[8] = {pb[8], pb[9], pb[10], pb[11], pb[12], pb[13], pb[14], pb[15]};
+        tile_group_pre(ga, n, m, selv, acc0, acc1);
+        tile_group_pre(gb, n, m, selv, acc0, acc1);
+        tile_group_pre(gc, n, m, selv, acc0, acc1);
+        tile_group_pre(gd, n, m, selv, acc0, acc1);
+        tile_group_loop(rb, ro + 128, n, m, selv, acc0, acc1);
+        ro += 32 * gn;
     };
     for (int c = 0; c < nch; c += 3) {
         step(c, h0);

@@ -19,8 +19,10 @@ module builds, once per graph, the streams the kernel walks:
   pieces (rows 3w .. 3w+2 of the chunk; -1 = the zero row);
 * and a record stream: per chunk n0 records of half-0 destinations, then n1 of
   half-1 ones (each count a multiple of 4; padding record = slot 0, value 0,
-  the zero row); record = int32x4 {slot, value bits, (slot >> 2) | ((slot & 3)
-  * 8) << 8, LDS byte address ((c % 3) * 48 + row in chunk) * 1024}.
+  the zero row); record = int32x2 {slot | ((c % 3) * 48 + row in chunk) << 24,
+  value bits}: the slot register index reads bits 7:0, the selector word is
+  w >> 2, its byte offset (w << 3) & 24 and the LDS byte address of the row
+  w >> 14.
 
 The plan is built with torch sorts on the graph's device (no host loop);
 ``emulate`` replays it on the CPU (test infrastructure: it checks the format
@@ -97,9 +99,9 @@ def build(indptr: torch.Tensor, indices: torch.Tensor, values: torch.Tensor, num
     rlen = nrec.sum(-1).flatten()                                         # [NWG*16]
     rstart = torch.cumsum(rlen, 0) - rlen
     seg_off = rstart.view(NWG, WAVES, 1) + torch.cumsum(nrec, -1) - nrec  # first record of (wg,w,c)
-    total = int(rlen.sum()) + 256                                          # + 4 KB over-read pad
-    recs = torch.zeros(total, 4, dtype=torch.int32, device=dev)
-    recs[:, 3] = (BUF_ROWS - 1) * 1024                                    # padding: zero row
+    total = int(rlen.sum()) + 512                                          # + 4 KB over-read pad
+    recs = torch.zeros(total, 2, dtype=torch.int32, device=dev)
+    recs[:, 0] = (BUF_ROWS - 1) << 24                                     # padding: slot 0, zero row
     order = torch.argsort(seg, stable=True)
     sseg = seg[order]
     first = torch.searchsorted(sseg, sseg)
@@ -110,10 +112,9 @@ def build(indptr: torch.Tensor, indices: torch.Tensor, values: torch.Tensor, num
     pos = seg_off.flatten()[base_seg] + h * pad.view(-1, 2)[base_seg, 0] + rank
     del sseg, rank, base_seg, h
     so = slot[order]
-    recs[pos, 0] = so.to(torch.int32)
+    w0 = so | (((c % 3) * BUF_ROWS + rin)[order] << 24)
+    recs[pos, 0] = torch.where(w0 >= (1 << 31), w0 - (1 << 32), w0).to(torch.int32)
     recs[pos, 1] = values[order].contiguous().view(torch.int32)
-    recs[pos, 2] = ((so >> 2) | ((so & 3) * 8) << 8).to(torch.int32)
-    recs[pos, 3] = ((((c % 3) * BUF_ROWS + rin)[order]) * 1024).to(torch.int32)
     del order, pos, so, seg, slot, rin, c
     # header stream: e(0), e(1), then e(c + 2) per chunk
     wv = torch.arange(WAVES, **i64)
@@ -182,10 +183,12 @@ def emulate(plan, grad: torch.Tensor, sel: torch.Tensor) -> torch.Tensor:
                 cols = torch.where(j < nd, sel[(d0 + j).clamp(max=C - 1), ent], 0)   # [slot, lane]
                 for t in range(n0 + n1):
                     r = recs[ro[wv] + t]
-                    s, d2, addr = int(r[0]), int(r[2]), int(r[3])
+                    w0 = int(r[0]) & 0xFFFFFFFF
                     val = r[1:2].view(torch.float32).item()
-                    word, off = d2 & 0xFF, (d2 >> 8) & 31
-                    assert word == s >> 2 and off == (s & 3) * 8
+                    # the kernel's decode: slot = w0 & 63 (register index reads bits 7:0),
+                    # selector word = w0 >> 2, byte offset = (w0 << 3) & 24, row = w0 >> 14
+                    s, addr = w0 & 63, w0 >> 14
+                    assert (w0 >> 6) & 0x3FFFF == 0
                     lanes = slice(0, 32) if t < n0 else slice(32, 64)
                     acc[wv, s, lanes] += val * lds[addr // 4 + cols[s, lanes]]
                 ro[wv] += n0 + n1

@@ -72,7 +72,7 @@ def test_plan_invariants():
                     real = seg[:, 1] != 0
                     n_real += int(real.sum())
                     # real records read rows of the chunk's own buffer
-                    rowf = seg[real][:, 3] // 1024
+                    rowf = (seg[real][:, 0].long() & 0xFFFFFFFF) >> 24
                     assert bool(((rowf // tile.BUF_ROWS) == (c - 2) % 3).all())
                     ro += n0 + n1
     assert n_real == int((torch.from_numpy(vals) != 0).sum())
