@@ -42,8 +42,11 @@ def choose_shape(num_cols: int, cus: int = 256) -> tuple[int, int, int]:
     """(num_groups, group_size, splits): groups of <= 2048 destinations, and
     source ranges so that num_groups * splits fills about one workgroup per CU."""
     groups = -(-num_cols // MAX_GROUP)
-    size = -(-num_cols // groups)
     splits = max(1, min(8, cus // groups))
+    # as many groups as the CUs left over allow: smaller groups, same sweep
+    groups = max(groups, min(cus // splits, num_cols))
+    size = -(-num_cols // groups)
+    groups = -(-num_cols // size)
     return groups, size, splits
 
 
