@@ -1804,20 +1804,24 @@ __device__ __forceinline__ void tile_glds(const float *g, uint32_t lds_byte)
 // indexed register, so the pinned slot (v64..v127) and selector (v48..v63)
 // registers stay in place.  n = -(groups left), m = -(half-0 groups left):
 // s_add_u32 sets SCC when a count reaches 0.
-__device__ __forceinline__ void tile_group_pre(const uint32_t (&g)[8], uint32_t &n, uint32_t &m,
-                                               tile_sel_t &selv, tile_acc_t &acc0,
-                                               tile_acc_t &acc1)
+// Two of the groups loaded before the chunk's barrier, software-pipelined:
+// the second group's selector bytes and LDS reads are issued before the
+// first group's FMAs (no SMEM is in flight here, so lgkmcnt(4) waits for
+// exactly the first group's reads).  m < -g on entry: group g is a half-0
+// group.  The counts saturate: m keeps counting past 0 harmlessly.
+__device__ __forceinline__ void tile_groups2(const uint32_t (&g)[16], uint32_t &n, uint32_t &m,
+                                             tile_sel_t &selv, tile_acc_t &acc0, tile_acc_t &acc1)
 {
-    uint32_t t0, t1, t2, t3;
+    uint32_t t0, t1, t2, t3, t4, t5, t6, t7;
     uint64_t ex;
     const uint64_t lo = 0x00000000ffffffffull, hi = 0xffffffff00000000ull;
     asm volatile(
         "s_cmp_eq_u32 %[n], 0\n\t"
-        "s_cbranch_scc1 .Ltile_skip%=\n\t"
+        "s_cbranch_scc1 .Ltp_done%=\n\t"
         "s_mov_b64 %[ex], exec\n\t"
+        "s_waitcnt lgkmcnt(0)\n\t"
         "s_cmp_lt_i32 %[m], 0\n\t"
         "s_cselect_b64 exec, %[lo], %[hi]\n\t"
-        "s_waitcnt lgkmcnt(0)\n\t"
         "s_lshr_b32 s80, %[g0], 2\n\t"
         "s_lshl_b32 s81, %[g0], 3\n\t"
         "s_lshr_b32 s82, %[g0], 14\n\t"
@@ -1847,7 +1851,42 @@ __device__ __forceinline__ void tile_group_pre(const uint32_t (&g)[8], uint32_t 
         "ds_read_b32 %[t1], %[t1]\n\t"
         "ds_read_b32 %[t2], %[t2]\n\t"
         "ds_read_b32 %[t3], %[t3]\n\t"
-        "s_waitcnt lgkmcnt(0)\n\t"
+        "s_cmp_eq_u32 %[n], -1\n\t"
+        "s_cbranch_scc1 .Ltp_one%=\n\t"
+        "s_cmp_lt_i32 %[m], -1\n\t"
+        "s_cselect_b64 exec, %[lo], %[hi]\n\t"
+        "s_lshr_b32 s80, %[g8], 2\n\t"
+        "s_lshl_b32 s81, %[g8], 3\n\t"
+        "s_lshr_b32 s82, %[g8], 14\n\t"
+        "s_lshr_b32 s83, %[g10], 2\n\t"
+        "s_lshl_b32 s84, %[g10], 3\n\t"
+        "s_lshr_b32 s85, %[g10], 14\n\t"
+        "s_lshr_b32 s86, %[g12], 2\n\t"
+        "s_lshl_b32 s87, %[g12], 3\n\t"
+        "s_lshr_b32 s88, %[g12], 14\n\t"
+        "s_lshr_b32 s89, %[g14], 2\n\t"
+        "s_lshl_b32 s90, %[g14], 3\n\t"
+        "s_lshr_b32 s91, %[g14], 14\n\t"
+        "s_set_gpr_idx_on s80, gpr_idx(SRC0)\n\t"
+        "v_bfe_u32 %[t4], v48, s81, 8\n\t"
+        "s_set_gpr_idx_idx s83\n\t"
+        "v_bfe_u32 %[t5], v48, s84, 8\n\t"
+        "s_set_gpr_idx_idx s86\n\t"
+        "v_bfe_u32 %[t6], v48, s87, 8\n\t"
+        "s_set_gpr_idx_idx s89\n\t"
+        "v_bfe_u32 %[t7], v48, s90, 8\n\t"
+        "s_set_gpr_idx_off\n\t"
+        "v_lshl_add_u32 %[t4], %[t4], 2, s82\n\t"
+        "v_lshl_add_u32 %[t5], %[t5], 2, s85\n\t"
+        "v_lshl_add_u32 %[t6], %[t6], 2, s88\n\t"
+        "v_lshl_add_u32 %[t7], %[t7], 2, s91\n\t"
+        "ds_read_b32 %[t4], %[t4]\n\t"
+        "ds_read_b32 %[t5], %[t5]\n\t"
+        "ds_read_b32 %[t6], %[t6]\n\t"
+        "ds_read_b32 %[t7], %[t7]\n\t"
+        "s_waitcnt lgkmcnt(4)\n\t"
+        "s_cmp_lt_i32 %[m], 0\n\t"
+        "s_cselect_b64 exec, %[lo], %[hi]\n\t"
         "s_set_gpr_idx_on %[g0], gpr_idx(SRC2,DST)\n\t"
         "v_fma_f32 v64, %[t0], %[g1], v64\n\t"
         "s_set_gpr_idx_idx %[g2]\n\t"
@@ -1857,15 +1896,49 @@ __device__ __forceinline__ void tile_group_pre(const uint32_t (&g)[8], uint32_t 
         "s_set_gpr_idx_idx %[g6]\n\t"
         "v_fma_f32 v64, %[t3], %[g7], v64\n\t"
         "s_set_gpr_idx_off\n\t"
-        "s_add_u32 %[m], %[m], 1\n\t"
+        "s_waitcnt lgkmcnt(0)\n\t"
+        "s_cmp_lt_i32 %[m], -1\n\t"
+        "s_cselect_b64 exec, %[lo], %[hi]\n\t"
+        "s_set_gpr_idx_on %[g8], gpr_idx(SRC2,DST)\n\t"
+        "v_fma_f32 v64, %[t4], %[g9], v64\n\t"
+        "s_set_gpr_idx_idx %[g10]\n\t"
+        "v_fma_f32 v64, %[t5], %[g11], v64\n\t"
+        "s_set_gpr_idx_idx %[g12]\n\t"
+        "v_fma_f32 v64, %[t6], %[g13], v64\n\t"
+        "s_set_gpr_idx_idx %[g14]\n\t"
+        "v_fma_f32 v64, %[t7], %[g15], v64\n\t"
+        "s_set_gpr_idx_off\n\t"
+        "s_add_u32 %[n], %[n], 2\n\t"
+        "s_add_u32 %[m], %[m], 2\n\t"
+        "s_branch .Ltp_end%=\n\t"
+        ".Ltp_one%=:\n\t"
+        "s_waitcnt lgkmcnt(0)\n\t"
+        "s_cmp_lt_i32 %[m], 0\n\t"
+        "s_cselect_b64 exec, %[lo], %[hi]\n\t"
+        "s_set_gpr_idx_on %[g0], gpr_idx(SRC2,DST)\n\t"
+        "v_fma_f32 v64, %[t0], %[g1], v64\n\t"
+        "s_set_gpr_idx_idx %[g2]\n\t"
+        "v_fma_f32 v64, %[t1], %[g3], v64\n\t"
+        "s_set_gpr_idx_idx %[g4]\n\t"
+        "v_fma_f32 v64, %[t2], %[g5], v64\n\t"
+        "s_set_gpr_idx_idx %[g6]\n\t"
+        "v_fma_f32 v64, %[t3], %[g7], v64\n\t"
+        "s_set_gpr_idx_off\n\t"
         "s_add_u32 %[n], %[n], 1\n\t"
+        "s_add_u32 %[m], %[m], 1\n\t"
+        ".Ltp_end%=:\n\t"
         "s_mov_b64 exec, %[ex]\n\t"
-        ".Ltile_skip%=:\n\t"
-        : [t0] "=&v"(t0), [t1] "=&v"(t1), [t2] "=&v"(t2), [t3] "=&v"(t3), [ex] "=&s"(ex),
-          [m] "+s"(m), [n] "+s"(n), "+{v[48:63]}"(selv), "+{v[64:95]}"(acc0), "+{v[96:127]}"(acc1)
-        : [lo] "s"(lo), [hi] "s"(hi), [g0] "s"(g[0]), [g1] "s"(g[1]), [g2] "s"(g[2]),
-          [g3] "s"(g[3]), [g4] "s"(g[4]), [g5] "s"(g[5]), [g6] "s"(g[6]), [g7] "s"(g[7])
-        : "memory", "scc", "s80", "s81", "s82", "s83", "s84", "s85", "s86", "s87", "s88", "s89", "s90", "s91");
+        ".Ltp_done%=:\n\t"
+        : [t0] "=&v"(t0), [t1] "=&v"(t1), [t2] "=&v"(t2), [t3] "=&v"(t3), [t4] "=&v"(t4),
+          [t5] "=&v"(t5), [t6] "=&v"(t6), [t7] "=&v"(t7), [ex] "=&s"(ex), [n] "+s"(n),
+          [m] "+s"(m), "+{v[48:63]}"(selv), "+{v[64:95]}"(acc0), "+{v[96:127]}"(acc1)
+        : [lo] "s"(lo), [hi] "s"(hi),
+          [g0] "s"(g[0]), [g1] "s"(g[1]), [g2] "s"(g[2]), [g3] "s"(g[3]),
+          [g4] "s"(g[4]), [g5] "s"(g[5]), [g6] "s"(g[6]), [g7] "s"(g[7]),
+          [g8] "s"(g[8]), [g9] "s"(g[9]), [g10] "s"(g[10]), [g11] "s"(g[11]),
+          [g12] "s"(g[12]), [g13] "s"(g[13]), [g14] "s"(g[14]), [g15] "s"(g[15])
+        : "memory", "scc", "s80", "s81", "s82", "s83", "s84", "s85", "s86", "s87", "s88", "s89",
+          "s90", "s91");
 }
 
 // the groups after the four loaded before the barrier: s_load, the next group
@@ -2170,14 +2243,14 @@ __global__ __launch_bounds__(kTileWaves * kWave) void bwd_tile_kernel(
         prefetch();
         const uint32_t g0n = (cnt & 0xffffu) >> 2, gn = g0n + (cnt >> 18);
         uint32_t n = 0u - gn, m = 0u - g0n;
-        const uint32_t ga[8] = {pa[0], pa[1], pa[2], pa[3], pa[4], pa[5], pa[6], pa[7]};
-        const uint32_t gb[8] = {pa[8], pa[9], pa[10], pa[11], pa[12], pa[13], pa[14], pa[15]};
-        const uint32_t gc[8] = {pb[0], pb[1], pb[2], pb[3], pb[4], pb[5], pb[6], pb[7]};
-        const uint32_t gd[8] = {pb[8], pb[9], pb[10], pb[11], pb[12], pb[13], pb[14], pb[15]};
-        tile_group_pre(ga, n, m, selv, acc0, acc1);
-        tile_group_pre(gb, n, m, selv, acc0, acc1);
-        tile_group_pre(gc, n, m, selv, acc0, acc1);
-        tile_group_pre(gd, n, m, selv, acc0, acc1);
+        uint32_t ga[16], gb[16];
+#pragma unroll
+        for (int i = 0; i < 16; ++i) {
+            ga[i] = pa[i];
+            gb[i] = pb[i];
+        }
+        tile_groups2(ga, n, m, selv, acc0, acc1);
+        tile_groups2(gb, n, m, selv, acc0, acc1);
         tile_group_loop(rb, ro + 128, n, m, selv, acc0, acc1);
         ro += 32 * gn;
     };
