@@ -1763,13 +1763,15 @@ __global__ __launch_bounds__(kBlock) void bwd_local_rel8_kernel(
 // group and range) so 256 CUs are busy; range 0 writes dxs, the others write
 // partial rows that tile_combine_kernel adds.
 //
-// The plan (ops.py MaxKGraph.tile_plan) is one record stream per
-// (workgroup, wave): a 4-slot prologue {tot(0), tot(1), rows of chunks 0 and
-// 1}, then per chunk c a 3-slot header {n0 | n1 << 16, tot(c+2), rows of
-// chunk c+2 for this wave's three DMA pieces (-1 = zero row)} and n0 (n1)
-// records of destinations in lane half 0 (1), each a multiple of 4 (padding:
-// slot 0, zero row, value 0).  tot = header + records of a chunk.  Record =
-// {slot | (buffer * 48 + row) << 24, value}.
+// The plan (spgemm_new_amd/tile.py, MaxKGraph.tile_plan) holds per
+// (workgroup, wave) a header stream of int32x4: e(0), e(1) = {0, the rows of
+// the wave's three DMA pieces of chunks 0 and 1}, then e(c+2) = {n0 | n1 <<
+// 16 of chunk c, rows of chunk c+2} (-1 = the zero row); and a record
+// stream: per chunk n0 records of destinations in lane half 0, then n1 of
+// half 1, each a multiple of 4 (padding: slot 0, zero row, value 0).
+// Record = int32x2 {slot | (buffer * 48 + row) << 24, value bits}.
+// Per chunk: the first 4 record groups are s_loaded before the barrier and
+// run software-pipelined in pairs; further groups run in an s_load loop.
 constexpr int kTileWaves = 16;
 constexpr int kTileRows = 47;  // gradient rows per chunk; row 47 of a buffer is zero
 constexpr int kTileBufRows = 48;
