@@ -79,14 +79,16 @@ def test_plan_invariants():
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("V,deg", [(3000, 40), (9000, 120)])
-def test_tile_backward_gpu_matches_oracle(dev, oracle, V, deg):
+@pytest.mark.parametrize("V,C,deg", [(3000, 3000, 40), (9000, 9000, 120), (3000, 5000, 60),
+                                     (4000, 1500, 30)])
+def test_tile_backward_gpu_matches_oracle(dev, oracle, V, C, deg):
+    """Square and rectangular (a multi-GPU rank's block with halo columns)."""
     import spgemm_new_amd as S
     from spgemm_new_amd import _lib
-    indptr, idx, vals = _graph(V, V, deg, seed=V)
-    grad, sel = _inputs(V, V, seed=V)
+    indptr, idx, vals = _graph(V, C, deg, seed=V + C)
+    grad, sel = _inputs(V, C, seed=V)
     g = S.MaxKGraph(torch.from_numpy(indptr).to(dev), torch.from_numpy(idx).to(dev),
-                    torch.from_numpy(vals).to(dev))
+                    torch.from_numpy(vals).to(dev), num_cols=C)
     assert g.tile_plan() is not None
     G = torch.from_numpy(grad).to(dev)
     sl = torch.from_numpy(sel).to(dev)
