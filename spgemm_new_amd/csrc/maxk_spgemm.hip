@@ -2219,7 +2219,16 @@ __global__ __launch_bounds__(kTileWaves * kWave) void bwd_tile_kernel(
     };
     // records about 1 KB ahead pulled into L2 for the s_loads (one load per chunk)
     uint32_t pf = 0;
-    auto prefetch = [&]() { tile_prefetch(rb + (ro >> 2) + 128 + lane * 4, pf); };
+#ifndef TILE_PF_AHEAD
+#define TILE_PF_AHEAD 128  // dwords: the window starts 512 B past the chunk's records
+#endif
+#ifndef TILE_NO_PREFETCH
+    auto prefetch = [&]() { tile_prefetch(rb + (ro >> 2) + TILE_PF_AHEAD + lane * 4, pf); };
+#define TILE_VMCNT "7"
+#else
+    auto prefetch = [&]() {};
+#define TILE_VMCNT "5"
+#endif
     // header e(i) = {n0 | n1 << 16 of chunk i-2, the wave's DMA rows of chunk i};
     // queue: H(0); per "iteration" i = -2, -1, 0, ...: DMA(i+2), H(i+3), prefetch
     const tile_hdr_t e0 = hs[0], e1 = hs[1];
@@ -2237,7 +2246,7 @@ __global__ __launch_bounds__(kTileWaves * kWave) void bwd_tile_kernel(
                      : "=&s"(pa), "=&s"(pb) : "s"(rb), "s"(ro), "s"(ro + 64) : "memory");
         // this wave's DMA of chunk c and header of chunk c landed; after the
         // barrier everyone's have, and chunk c-1's buffer is free
-        asm volatile("s_waitcnt vmcnt(7)\n\ts_barrier" : "+v"(h), "+v"(pf)::"memory");
+        asm volatile("s_waitcnt vmcnt(" TILE_VMCNT ")\n\ts_barrier" : "+v"(h), "+v"(pf)::"memory");
         const uint32_t cnt = (uint32_t)__builtin_amdgcn_readfirstlane(h.x);
         dma(c + 2, __builtin_amdgcn_readfirstlane(h.y), __builtin_amdgcn_readfirstlane(h.z),
             __builtin_amdgcn_readfirstlane(h.w));
