@@ -1812,11 +1812,11 @@ __device__ __forceinline__ void tile_glds(const float *g, uint32_t lds_byte)
 // exactly the first group's reads).  m < -g on entry: group g is a half-0
 // group.  The counts saturate: m keeps counting past 0 harmlessly.
 __device__ __forceinline__ void tile_groups2(const uint32_t (&g)[16], uint32_t &n, uint32_t &m,
-                                             tile_sel_t &selv, tile_acc_t &acc0, tile_acc_t &acc1)
+                                             uint64_t lo, uint64_t hi, tile_sel_t &selv,
+                                             tile_acc_t &acc0, tile_acc_t &acc1)
 {
     uint32_t t0, t1, t2, t3, t4, t5, t6, t7;
     uint64_t ex;
-    const uint64_t lo = 0x00000000ffffffffull, hi = 0xffffffff00000000ull;
     asm volatile(
         "s_cmp_eq_u32 %[n], 0\n\t"
         "s_cbranch_scc1 .Ltp_done%=\n\t"
@@ -1946,12 +1946,12 @@ __device__ __forceinline__ void tile_groups2(const uint32_t (&g)[16], uint32_t &
 // the groups after the four loaded before the barrier: s_load, the next group
 // in flight while the current one runs; s64..s91 are the loop's
 __device__ __forceinline__ void tile_group_loop(const uint32_t *rb, uint32_t ro, uint32_t &n,
-                                                uint32_t &m, tile_sel_t &selv, tile_acc_t &acc0,
+                                                uint32_t &m, uint64_t lo, uint64_t hi,
+                                                tile_sel_t &selv, tile_acc_t &acc0,
                                                 tile_acc_t &acc1)
 {
     uint32_t t0, t1, t2, t3;
     uint64_t ex;
-    const uint64_t lo = 0x00000000ffffffffull, hi = 0xffffffff00000000ull;
     asm volatile(
         "s_cmp_eq_u32 %[n], 0\n\t"
         "s_cbranch_scc1 .Ltile_done%=\n\t"
@@ -2161,6 +2161,10 @@ __device__ __forceinline__ void tile_prefetch(const uint32_t *p, uint32_t &d)
     asm volatile("global_load_dword %0, %1, off" : "+v"(d) : "v"(p) : "memory");
 }
 
+// K = 32: slot register s holds destinations (2s + half) * 16 + wave, lanes
+// 0-31 / 32-63 their 32 entries; K = 64: destination s * 16 + wave, one entry
+// per lane, the records all in "half 0" with exec on every lane.
+template <int K>
 __global__ __launch_bounds__(kTileWaves * kWave) void bwd_tile_kernel(
     const tile_hdr_t *__restrict__ hdrs, const int64_t *__restrict__ hdr_start,
     const uint32_t *__restrict__ recs, const int64_t *__restrict__ rec_start,
@@ -2170,7 +2174,10 @@ __global__ __launch_bounds__(kTileWaves * kWave) void bwd_tile_kernel(
 {
     __shared__ __attribute__((aligned(16))) float tb[3 * kTileBufRows * kMaxDim];
     const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    const int lane = lane_id(), half = lane >> 5, ent = lane & 31;
+    const int lane = lane_id(), half = K == 32 ? lane >> 5 : 0, ent = lane & (K - 1);
+    const uint64_t lo = K == 32 ? 0x00000000ffffffffull : ~0ull;
+    const uint64_t hi = K == 32 ? 0xffffffff00000000ull : ~0ull;
+    auto dest_of = [&](int slot) { return (K == 32 ? 2 * slot + half : slot) * kTileWaves + wv; };
     const int split = blockIdx.x % splits, grp = blockIdx.x / splits;
     const int d0 = grp * group_size;
     const int nd = min(group_size, num_cols - d0);
@@ -2179,10 +2186,11 @@ __global__ __launch_bounds__(kTileWaves * kWave) void bwd_tile_kernel(
     // (2s + half) * 16 + wv, byte b of selector word t
     {
         uint8_t *sb = reinterpret_cast<uint8_t *>(tb);
-        for (int i = threadIdx.x; i < 128 * kTileWaves * 2; i += kTileWaves * kWave) {
-            const int j = i >> 1;
+        constexpr int U = K / 16;  // 16-B units per selector row; 4096 units either way
+        for (int i = threadIdx.x; i < 64 * kTileWaves * 4; i += kTileWaves * kWave) {
+            const int j = i / U;
             uint4 v = {0u, 0u, 0u, 0u};
-            if (j < nd) v = *reinterpret_cast<const uint4 *>(sel + (size_t)(d0 + j) * 32 + (i & 1) * 16);
+            if (j < nd) v = *reinterpret_cast<const uint4 *>(sel + (size_t)(d0 + j) * K + (i % U) * 16);
             *reinterpret_cast<uint4 *>(sb + (size_t)i * 16) = v;
         }
         __syncthreads();
@@ -2194,7 +2202,7 @@ __global__ __launch_bounds__(kTileWaves * kWave) void bwd_tile_kernel(
         uint32_t word = 0;
 #pragma unroll
         for (int b = 0; b < 4; ++b)
-            word |= (uint32_t)sb[((2 * (4 * t + b) + half) * kTileWaves + wv) * 32 + ent] << (8 * b);
+            word |= (uint32_t)sb[dest_of(4 * t + b) * K + ent] << (8 * b);
         selv[t] = word;
         asm volatile("" ::: "memory");  // four LDS reads in flight at a time
     }
@@ -2260,9 +2268,9 @@ __global__ __launch_bounds__(kTileWaves * kWave) void bwd_tile_kernel(
             ga[i] = pa[i];
             gb[i] = pb[i];
         }
-        tile_groups2(ga, n, m, selv, acc0, acc1);
-        tile_groups2(gb, n, m, selv, acc0, acc1);
-        tile_group_loop(rb, ro + 128, n, m, selv, acc0, acc1);
+        tile_groups2(ga, n, m, lo, hi, selv, acc0, acc1);
+        tile_groups2(gb, n, m, lo, hi, selv, acc0, acc1);
+        tile_group_loop(rb, ro + 128, n, m, lo, hi, selv, acc0, acc1);
         ro += 32 * gn;
     };
     for (int c = 0; c < nch; c += 3) {
@@ -2271,11 +2279,11 @@ __global__ __launch_bounds__(kTileWaves * kWave) void bwd_tile_kernel(
         if (c + 2 < nch) step(c + 2, h2);
     }
     asm volatile("s_waitcnt vmcnt(0)" : "+v"(pf), "+v"(h0), "+v"(h1), "+v"(h2)::"memory");
-    float *out = split == 0 ? dxs : part + (size_t)(split - 1) * num_cols * 32;
+    float *out = split == 0 ? dxs : part + (size_t)(split - 1) * num_cols * K;
 #pragma unroll
     for (int s = 0; s < 64; ++s) {
-        const int j = (2 * s + half) * kTileWaves + wv;
-        if (j < nd) out[(size_t)(d0 + j) * 32 + ent] = s < 32 ? acc0[s] : acc1[s - 32];
+        const int j = dest_of(s);
+        if (j < nd) out[(size_t)(d0 + j) * K + ent] = s < 32 ? acc0[s] : acc1[s - 32];
     }
 }
 
@@ -3072,10 +3080,10 @@ int maxk_sspmm_backward_tile(const void *headers, const int64_t *header_start,
                              const uint8_t *cbsr_sel, int num_rows, int num_cols, int dim_origin,
                              int dim_k, float *dxs, float *part, void *stream)
 {
-    if (dim_k != 32 || dim_origin != kMaxDim) return MAXK_E_DIM;
+    if ((dim_k != 32 && dim_k != 64) || dim_origin != kMaxDim) return MAXK_E_DIM;
     if (!headers || !header_start || !records || !record_start || !num_chunks || !grad ||
         !zero_row || !cbsr_sel || !dxs || num_groups < 1 || splits < 1 || group_size < 1 ||
-        group_size > 128 * kTileWaves || num_rows < 1 || num_cols < 1 ||
+        group_size > (dim_k == 32 ? 128 : 64) * kTileWaves || num_rows < 1 || num_cols < 1 ||
         (int64_t)num_groups * group_size < num_cols || (splits > 1 && !part))
         return MAXK_E_ARG;
     if ((reinterpret_cast<uintptr_t>(headers) | reinterpret_cast<uintptr_t>(records) |
@@ -3084,14 +3092,15 @@ int maxk_sspmm_backward_tile(const void *headers, const int64_t *header_start,
          reinterpret_cast<uintptr_t>(cbsr_sel)) & 15)
         return MAXK_E_ARG;
     hipStream_t st = as_stream(stream);
-    hipLaunchKernelGGL(bwd_tile_kernel, dim3((unsigned)(num_groups * splits)),
+    hipLaunchKernelGGL(dim_k == 32 ? bwd_tile_kernel<32> : bwd_tile_kernel<64>,
+                       dim3((unsigned)(num_groups * splits)),
                        dim3(kTileWaves * kWave), 0, st,
                        reinterpret_cast<const tile_hdr_t *>(headers), header_start,
                        reinterpret_cast<const uint32_t *>(records), record_start, num_chunks, grad,
                        zero_row, cbsr_sel, num_cols, group_size, splits, dxs, part);
     int rc = launch_status();
     if (rc || splits == 1) return rc;
-    const int64_t n4 = (int64_t)num_cols * 8;
+    const int64_t n4 = (int64_t)num_cols * dim_k / 4;
     const int64_t blocks = ceil_div(n4, kBlock);
     hipLaunchKernelGGL(tile_combine_kernel, dim3((unsigned)(blocks < 4096 ? blocks : 4096)),
                        dim3(kBlock), 0, st, dxs, part, splits - 1, n4);

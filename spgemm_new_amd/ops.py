@@ -72,7 +72,7 @@ TILE_AUTO = os.environ.get("MAXK_TILE", "1") != "0"
 
 
 def tile_shape_ok(dim_k: int, dim_origin: int) -> bool:
-    return dim_k == 32 and dim_origin == 256
+    return dim_k in (32, 64) and dim_origin == 256
 # forward at k in {4, 8, 16}: pack CBSR into one record per node (MAXK_FWD_PACKED=0 disables)
 FWD_PACKED = os.environ.get("MAXK_FWD_PACKED", "1") != "0"
 # fused multi-relation forward: reorder CBSR entries against LDS store conflicts
@@ -181,7 +181,7 @@ class MaxKGraph:
         self.csc_panel_cost = csc_panel_cost or panel_cost
         self._csc = None
         self._local = {}
-        self._tile = None
+        self._tile = {}
         self._ws = {}
         self._bwd_choice = {}
         self.last_bwd_algo = None
@@ -293,25 +293,25 @@ class MaxKGraph:
             hit = cache[key] = (ev, values)
         return hit[0]
 
-    def tile_plan(self):
-        """Plan of the TILE backward (k = 32, h = 256; spgemm_new_amd/tile.py), or
-        None when the graph's segments overflow (then the other algorithms
-        serve it).  Built once with torch sorts on the device."""
-        if self._tile is None:
+    def tile_plan(self, dim_k: int = 32):
+        """Plan of the TILE backward (k = 32 or 64, h = 256; spgemm_new_amd/tile.py),
+        or None when the shape does not suit it (then the other algorithms serve
+        it).  Built once per k with torch sorts on the device."""
+        if dim_k not in self._tile:
             from . import tile
             plan = None
             if self.num_edges > 0 and self.device.type == "cuda":
                 cus = torch.cuda.get_device_properties(self.device).multi_processor_count
                 plan = tile.build(self.indptr, self.indices[: self.num_edges],
                                   self.values[: self.num_edges], self.num_rows, self.num_cols,
-                                  cus=cus)
+                                  cus=cus, k=dim_k)
             if plan is not None:
                 plan["values_key"] = _tensor_key(self.values)
                 G, NS = plan["num_groups"], plan["splits"]
-                plan["part"] = torch.empty(max(1, (NS - 1) * self.num_cols * 32),
+                plan["part"] = torch.empty(max(1, (NS - 1) * self.num_cols * dim_k),
                                            dtype=torch.float32, device=self.device)
-            self._tile = plan if plan is not None else False
-        return self._tile or None
+            self._tile[dim_k] = plan
+        return self._tile[dim_k]
 
     def local_fits(self, dim_k: int) -> bool:
         """True when the LOCAL plan's waves are all co-resident (one sweep of G)."""
@@ -340,7 +340,7 @@ class MaxKGraph:
         if self.local_plan(k) is not None:
             cands.append(_lib.MAXK_BWD_LOCAL)
         if TILE_AUTO and tile_shape_ok(k, grad.shape[1]) and values is self.values and \
-                self.tile_plan() is not None:
+                self.tile_plan(k) is not None:
             cands.append(_lib.MAXK_BWD_TILE)
         best, best_ms = None, float("inf")
         for a in cands:
@@ -686,10 +686,9 @@ def sspmm_backward(g: MaxKGraph, grad, sel, out=None, values=None, algo: int = _
         algo = _lib.MAXK_BWD_ATOMIC  # nothing to stage: the call just zeroes dXs
     L = _lib.load()
     if algo == _lib.MAXK_BWD_TILE:
-        plan = g.tile_plan() if tile_shape_ok(k, dim_origin) else None
+        plan = g.tile_plan(k) if tile_shape_ok(k, dim_origin) else None
         if plan is None:
-            raise RuntimeError("TILE backward unsupported for this shape (k = 32, h = 256, "
-                               "bounded in-edges per source chunk)")
+            raise RuntimeError("TILE backward unsupported for this shape (k = 32 or 64, h = 256)")
         if values is not g.values:
             raise RuntimeError("TILE backward: the plan holds the graph's own edge values")
         g.last_bwd_algo = "tile"

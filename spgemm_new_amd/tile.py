@@ -35,13 +35,17 @@ import torch
 WAVES = 16
 CHUNK_ROWS = 47
 BUF_ROWS = 48
-MAX_GROUP = 128 * WAVES
+MAX_GROUP = 128 * WAVES     # k = 32: two destinations per slot register
 
 
-def choose_shape(num_cols: int, cus: int = 256) -> tuple[int, int, int]:
+def max_group(k: int) -> int:
+    return (128 if k == 32 else 64) * WAVES
+
+
+def choose_shape(num_cols: int, cus: int = 256, k: int = 32) -> tuple[int, int, int]:
     """(num_groups, group_size, splits): groups of <= 2048 destinations, and
     source ranges so that num_groups * splits fills about one workgroup per CU."""
-    groups = -(-num_cols // MAX_GROUP)
+    groups = -(-num_cols // max_group(k))
     splits = max(1, min(8, cus // groups))
     # as many groups as the CUs left over allow: smaller groups, same sweep
     groups = max(groups, min(cus // splits, num_cols))
@@ -51,7 +55,7 @@ def choose_shape(num_cols: int, cus: int = 256) -> tuple[int, int, int]:
 
 
 def build(indptr: torch.Tensor, indices: torch.Tensor, values: torch.Tensor, num_rows: int,
-          num_cols: int, cus: int = 256, shape: tuple[int, int, int] | None = None):
+          num_cols: int, cus: int = 256, shape: tuple[int, int, int] | None = None, k: int = 32):
     """The TILE plan as a dict, or None when a chunk would overflow a wave's
     64-slot segment (many edges of few source rows into one wave's
     destinations; the other algorithms serve such graphs)."""
@@ -59,7 +63,11 @@ def build(indptr: torch.Tensor, indices: torch.Tensor, values: torch.Tensor, num
     E = indices.numel()
     if E == 0 or num_rows < 1 or num_cols < 1:
         return None
-    G, GS, NS = shape or choose_shape(num_cols, cus)
+    if k not in (32, 64):
+        return None
+    G, GS, NS = shape or choose_shape(num_cols, cus, k)
+    if GS > max_group(k):
+        return None
     NWG = G * NS
     V = num_rows
     i64 = dict(dtype=torch.int64, device=dev)
@@ -70,7 +78,10 @@ def build(indptr: torch.Tensor, indices: torch.Tensor, values: torch.Tensor, num
     j = d - grp * GS
     w = j % WAVES
     q = j // WAVES
-    slot, half = q >> 1, q & 1
+    if k == 32:
+        slot, half = q >> 1, q & 1
+    else:                                  # k = 64: one destination per slot register
+        slot, half = q, torch.zeros_like(q)
     bounds = (torch.arange(NS + 1, **i64) * V) // NS
     split = torch.bucketize(rows, bounds[1:NS], right=True)
     wg = grp * NS + split
@@ -148,6 +159,7 @@ def build(indptr: torch.Tensor, indices: torch.Tensor, values: torch.Tensor, num
     return {"headers": hdrs, "header_start": hstart.contiguous(), "records": recs,
             "record_start": rstart.contiguous(), "num_chunks": nch.to(torch.int32).contiguous(),
             "num_groups": G, "group_size": GS, "splits": NS, "num_rows": V, "num_cols": num_cols,
+            "k": k,
             "zero_row": torch.zeros(256, dtype=torch.float32, device=dev)}
 
 
@@ -162,9 +174,13 @@ def emulate(plan, grad: torch.Tensor, sel: torch.Tensor) -> torch.Tensor:
     G, GS, NS, C = plan["num_groups"], plan["group_size"], plan["splits"], plan["num_cols"]
     grad = grad.cpu().float()
     sel = sel.cpu().long()
-    out = torch.zeros(NS, C, 32)
-    jj = (2 * torch.arange(64)[:, None] + torch.arange(64)[None, :] // 32) * WAVES  # [slot, lane]
-    ent = torch.arange(64)[None, :] % 32
+    K = plan.get("k", 32)
+    out = torch.zeros(NS, C, K)
+    if K == 32:
+        jj = (2 * torch.arange(64)[:, None] + torch.arange(64)[None, :] // 32) * WAVES  # [slot, lane]
+    else:
+        jj = torch.arange(64)[:, None].expand(64, 64) * WAVES
+    ent = torch.arange(64)[None, :] % K
     lds = torch.zeros(3 * BUF_ROWS * 256)
     for b in range(G * NS):
         sp, g = b % NS, b // NS
@@ -192,7 +208,8 @@ def emulate(plan, grad: torch.Tensor, sel: torch.Tensor) -> torch.Tensor:
                     # selector word = w0 >> 2, byte offset = (w0 << 3) & 24, row = w0 >> 14
                     s, addr = w0 & 63, w0 >> 14
                     assert (w0 >> 6) & 0x3FFFF == 0
-                    lanes = slice(0, 32) if t < n0 else slice(32, 64)
+                    lanes = (slice(0, 64) if K == 64 else
+                             slice(0, 32) if t < n0 else slice(32, 64))
                     acc[wv, s, lanes] += val * lds[addr // 4 + cols[s, lanes]]
                 ro[wv] += n0 + n1
         for wv in range(WAVES):

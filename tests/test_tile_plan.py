@@ -30,6 +30,7 @@ def _inputs(V, C, seed, k=32, h=256):
     return grad, sel
 
 
+@pytest.mark.parametrize("k", [32, 64])
 @pytest.mark.parametrize("V,C,deg,shape,hubs", [
     (300, 300, 12, None, 0),           # one group, splits up to 8, several chunks
     (800, 800, 6, None, 12),           # hub rows: chunks cut short where records pile up
@@ -37,11 +38,11 @@ def _inputs(V, C, seed, k=32, h=256):
     (700, 900, 20, (3, 300, 2), 0),    # forced: 3 groups of 300, 2 source ranges
     (200, 64, 4, (1, 64, 1), 0),       # few destinations, one range
 ])
-def test_plan_emulated_matches_oracle(oracle, V, C, deg, shape, hubs):
+def test_plan_emulated_matches_oracle(oracle, V, C, deg, shape, hubs, k):
     indptr, idx, vals = _graph(V, C, deg, seed=V + C, hub_rows=hubs)
-    grad, sel = _inputs(V, C, seed=V)
+    grad, sel = _inputs(V, C, seed=V, k=k)
     plan = tile.build(torch.from_numpy(indptr), torch.from_numpy(idx), torch.from_numpy(vals),
-                      V, C, cus=16, shape=shape)
+                      V, C, cus=16, shape=shape, k=k)
     assert plan is not None
     got = tile.emulate(plan, torch.from_numpy(grad), torch.from_numpy(sel)).numpy()
     ref = oracle.np_backward(indptr, idx, vals, grad, sel)
@@ -79,17 +80,18 @@ def test_plan_invariants():
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("V,C,deg", [(3000, 3000, 40), (9000, 9000, 120), (3000, 5000, 60),
-                                     (4000, 1500, 30)])
-def test_tile_backward_gpu_matches_oracle(dev, oracle, V, C, deg):
-    """Square and rectangular (a multi-GPU rank's block with halo columns)."""
+@pytest.mark.parametrize("V,C,deg,k", [(3000, 3000, 40, 32), (9000, 9000, 120, 32),
+                                       (3000, 5000, 60, 32), (4000, 1500, 30, 32),
+                                       (3000, 3000, 40, 64), (5000, 2500, 50, 64)])
+def test_tile_backward_gpu_matches_oracle(dev, oracle, V, C, deg, k):
+    """Square and rectangular (a multi-GPU rank's block with halo columns), k = 32 and 64."""
     import spgemm_new_amd as S
     from spgemm_new_amd import _lib
     indptr, idx, vals = _graph(V, C, deg, seed=V + C)
-    grad, sel = _inputs(V, C, seed=V)
+    grad, sel = _inputs(V, C, seed=V, k=k)
     g = S.MaxKGraph(torch.from_numpy(indptr).to(dev), torch.from_numpy(idx).to(dev),
                     torch.from_numpy(vals).to(dev), num_cols=C)
-    assert g.tile_plan() is not None
+    assert g.tile_plan(k) is not None
     G = torch.from_numpy(grad).to(dev)
     sl = torch.from_numpy(sel).to(dev)
     got = g.backward(G, sl, algo=_lib.MAXK_BWD_TILE)

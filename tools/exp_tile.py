@@ -29,6 +29,7 @@ def ev(fn, reps):
 
 graph = sys.argv[1] if len(sys.argv) > 1 else "reddit"
 reps = int(sys.argv[2]) if len(sys.argv) > 2 else 10
+K = int(sys.argv[3]) if len(sys.argv) > 3 else 32
 dev = torch.device("cuda:0")
 V, E = CONFIGS[graph]
 indptr, indices = synthetic_csr_gpu(V, E, device=dev)
@@ -37,10 +38,10 @@ gen.manual_seed(1)
 values = torch.rand(E, generator=gen, device=dev)
 X = torch.rand((V, 256), generator=gen, device=dev)
 G = torch.rand((V, 256), generator=gen, device=dev)
-data, sel = S.topk_cbsr(X, 32)
+data, sel = S.topk_cbsr(X, K)
 g = S.MaxKGraph(indptr, indices, values)
 t0 = time.time()
-plan = g.tile_plan()
+plan = g.tile_plan(K)
 torch.cuda.synchronize()
 print(f"{graph}: plan {time.time() - t0:.2f} s", flush=True)
 if plan is None:
@@ -50,8 +51,8 @@ print(f"  groups {plan['num_groups']} x {plan['group_size']}, splits {plan['spli
       f"chunks/WG max {int(plan['num_chunks'].max())} mean "
       f"{plan['num_chunks'].float().mean().item():.0f}, records {plan['records'].shape[0] / 1e6:.1f} M "
       f"({plan['records'].shape[0] / E:.2f} per edge)", flush=True)
-dx_t = torch.empty((V, 32), device=dev)
-dx_l = torch.empty((V, 32), device=dev)
+dx_t = torch.empty((V, K), device=dev)
+dx_l = torch.empty((V, K), device=dev)
 g.backward(G, sel, out=dx_t, algo=_lib.MAXK_BWD_TILE)
 g.backward(G, sel, out=dx_l, algo=_lib.MAXK_BWD_LOCAL)
 torch.cuda.synchronize()
