@@ -14,7 +14,7 @@ ok_or_fail() {  # continue only on 0 / 1
     fi
 }
 if [ -z "$SKIP_TESTS" ]; then
-    timeout -k 10 900 python -m pytest tests -m gpu -x -q -p no:cacheprovider "$@" \
+    timeout -k 10 900 python -u -m pytest tests -m gpu -x -q -p no:cacheprovider --timeout 300 --timeout-method thread "$@" \
         > gpurun_out/pytest_gpu.log 2>&1
     ok_or_fail $? pytest_gpu
     tail -5 gpurun_out/pytest_gpu.log
