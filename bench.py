@@ -42,7 +42,7 @@ def parse():
     p.add_argument("--panel-cost", type=int, default=None)
     p.add_argument("--row-cost", type=int, default=None)
     p.add_argument("--no-cpu-baseline", action="store_true")
-    p.add_argument("--cpu-seconds", type=float, default=12.0)
+    p.add_argument("--cpu-seconds", type=float, default=15.0)
     p.add_argument("--partitioned", action="store_true",
                    help="use the multi-GPU (row partition + halo exchange) path even at N=1")
     p.add_argument("--verbose", action="store_true")
@@ -74,13 +74,28 @@ def log(*a):
     print(*a, file=sys.stderr, flush=True)
 
 
+def cpu_threads():
+    """Host threads for the CPU baseline: every core this process may run on
+    (sched_getaffinity), capped by OMP_NUM_THREADS when the launcher sets it
+    (the GPU box sets it to its per-GPU CPU share)."""
+    visible = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else \
+        (os.cpu_count() or 1)
+    cap = os.environ.get("OMP_NUM_THREADS")
+    threads = min(visible, int(cap)) if cap and cap.isdigit() and int(cap) > 0 else visible
+    return threads, visible, cap
+
+
 def cpu_baseline(indptr, indices, values, x_masked, grad, mask, k, h, budget_s):
     """The reference's CPU aggregation path (utils/models.py:281-287:
-    torch.sparse.mm(adj, x)), forward and backward (A^T G * mask), on a bounded
-    row sample of the same graph, timed on the host cores."""
+    torch.sparse.mm(adj, x) and its mean form torch.sparse.mm(adj, x) /
+    (adj.sum(1) + 1e-6)), forward and backward (A^T G * mask), on a bounded
+    row sample of the same graph, timed on the host cores.  `value` is the
+    sum form's fwd + bwd rate on the sample (same byte formula as the GPU
+    line); the full-graph time is the sample's time scaled by E / e_sample."""
     import numpy as np
-    threads = min(16, os.cpu_count() or 1)
+    threads, visible, cap = cpu_threads()
     torch.set_num_threads(threads)
+    log(f"[bench] CPU baseline on {threads} threads ({visible} visible, OMP_NUM_THREADS={cap})")
     ip = indptr.cpu().numpy().astype(np.int64)
     V = len(ip) - 1
     E = int(ip[-1])
@@ -92,32 +107,44 @@ def cpu_baseline(indptr, indices, values, x_masked, grad, mask, k, h, budget_s):
         xm = x_masked
         g = grad[:rows]
         t0 = time.perf_counter()
-        y = torch.sparse.mm(a, xm)                                   # forward
+        y = torch.sparse.mm(a, xm)                                   # forward, sum form
         t1 = time.perf_counter()
         dx = torch.sparse.mm(a.to_sparse_coo().t().coalesce(), g) * mask   # backward
         t2 = time.perf_counter()
-        del y, dx
-        return e, t1 - t0, t2 - t1
+        # mean form (utils/models.py:287): / (row sums + 1e-6); the reference adds
+        # the scalar to the sparse sum, which torch 2.10 rejects -- the same math on
+        # the dense row sums
+        ym = torch.sparse.mm(a, xm) / (torch.sparse.sum(a.to_sparse_coo(), 1).to_dense()
+                                       .unsqueeze(1) + 1e-6)
+        t3 = time.perf_counter()
+        del y, dx, ym
+        return e, t1 - t0, t2 - t1, t3 - t2
 
     rows = max(1, min(V, V // 200))
-    e, tf, tb = run(rows)
+    e, tf, tb, _ = run(rows)
     per_edge = (tf + tb) / max(e, 1)
-    target_e = min(E, int(budget_s / 2 / max(per_edge, 1e-12)))
+    target_e = min(E, int(budget_s / 3 / max(per_edge, 1e-12)))
     rows = int(np.searchsorted(ip, target_e))
     rows = max(1, min(V, rows))
     run(rows)  # warm-up
     res = [run(rows) for _ in range(3)]
     e = res[0][0]
-    tf = sorted(r[1] for r in res)[1]
-    tb = sorted(r[2] for r in res)[1]
+    tf, tb, tm = (sorted(r[i] for r in res)[1] for i in (1, 2, 3))
     nbytes = 2 * (8 * e + 5 * k * e + 4 * h * rows)
+    scale = E / max(e, 1)
     return {
         "value": round(nbytes / (tf + tb) / 1e9, 3), "unit": "GB/s", "cores": threads,
-        "kind": "reference",
+        "cores_visible": visible, "kind": "reference",
         "ms_per_step_sample": round((tf + tb) * 1e3, 2),
-        "sample": (f"rows [0,{rows}) of the same graph ({e} edges, {e / E:.1%} of E): "
-                   "torch.sparse.mm(A,X*mask) + torch.sparse.mm(A^T,G)*mask on CPU fp32, "
-                   "median of 3 after 1 warm-up (reference CPU path utils/models.py:281-287)"),
+        "fwd_ms_sample": round(tf * 1e3, 2), "bwd_ms_sample": round(tb * 1e3, 2),
+        "mean_form_fwd_ms_sample": round(tm * 1e3, 2),
+        "mean_form_GBs": round((nbytes / 2) / tm / 1e9, 3),
+        "ms_per_step_full_graph_extrapolated": round((tf + tb) * scale * 1e3, 1),
+        "sample": (f"rows [0,{rows}) of the same graph ({e} edges, {e / E:.1%} of E; full-graph "
+                   f"time extrapolated x{scale:.2f} by edges): torch.sparse.mm(A,X*mask) + "
+                   "torch.sparse.mm(A^T,G)*mask on CPU fp32 (sum form = value), plus the mean "
+                   "form /(rowsum+1e-6), median of 3 after 1 warm-up (reference CPU path "
+                   f"utils/models.py:281-287), {threads} threads"),
         "cpu_model": _cpu_model(),
     }
 
@@ -510,6 +537,18 @@ def main():
         if traffic is not None:
             rf["traffic_per_launch"] = traffic // rf["launches_per_call"]
         result["config"]["bwd_algo"] = g.last_bwd_algo
+        # untimed parity check of the timed outputs: dx of the timed algorithm vs
+        # STAGED (an independent algorithm), and the exact adjoint identity
+        # <A.X^, G> = <X^_s, dXs> (fp64 sums) for the timed y and dx
+        torch.cuda.synchronize()
+        dx_ref = g.backward(G, sel, algo=_lib.MAXK_BWD_STAGED)
+        lhs = float((y.double() * G.double()).sum())
+        rhs = float((data.double() * dx.double()).sum())
+        result["bwd_check"] = {
+            "vs": "staged",
+            "max_rel_diff": float(((dx - dx_ref).abs() / dx_ref.abs().clamp_min(1)).max()),
+            "adjoint_rel_err": abs(lhs - rhs) / max(abs(lhs), 1e-30)}
+        del dx_ref
         result["fwd_ms"] = round(fms, 4)
         result["bwd_ms"] = round(bms, 4)
         result["fwd_GBs"] = round(b_call / fms / 1e6, 1)

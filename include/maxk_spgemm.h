@@ -264,17 +264,17 @@ int maxk_sspmm_backward_local_rel8(const int32_t *seg_edge_off, int num_segments
                                    void *stream);
 
 /* ---------------------------------------------------------------------------
- * Backward SSpMM, TILE algorithm (dim_k = 32, dim_origin = 256): every
+ * Backward SSpMM, TILE algorithm (dim_k = 32 or 64, dim_origin = 256): every
  * gradient row is read once per CU into an LDS ring instead of being
  * gathered per edge; destinations' dXs live in registers.  One workgroup per
- * (destination group of <= 2048 columns, source-row range): grid =
+ * (destination group of <= 2048 (k = 64: 1024) columns, source-row range): grid =
  * num_groups * splits, workgroup b = group b / splits, range b % splits.
- * Inputs from the plan (spgemm_new_amd/tile.py; format in csrc/maxk_spgemm.hip
+ * Inputs from the plan (maxk_tile_plan_build below; format in csrc/maxk_spgemm.hip
  * above bwd_tile_kernel), one stream per (workgroup, wave) w = b * 16 + wave:
  * headers int32[.., 4] from header_start[w] (16-B aligned), records
  * int32[.., 2] from record_start[w] (16-B aligned, padded by 4 KB);
  * num_chunks int32[num_groups * splits]; zero_row: 1 KB of zeros (16-B
- * aligned).  part: fp32[(splits - 1) * num_cols * 32] scratch (NULL when
+ * aligned).  part: fp32[(splits - 1) * num_cols * dim_k] scratch (NULL when
  * splits == 1).  Writes every element of dxs; same result as the other
  * algorithms up to fp32 summation order (deterministic).
  * ------------------------------------------------------------------------- */
@@ -284,6 +284,34 @@ int maxk_sspmm_backward_tile(const void *headers, const int64_t *header_start,
                              int group_size, const float *grad, const float *zero_row,
                              const uint8_t *cbsr_sel, int num_rows, int num_cols, int dim_origin,
                              int dim_k, float *dxs, float *part, void *stream);
+
+/* TILE plan, built on the device (spgemm_new_amd/csrc/maxk_plan.hip; no
+ * reference counterpart: the reference backward reuses the forward's .warp4
+ * chunks, kernels/spmm_maxk_backward.cu:117-139).  CSR with indptr[0] == 0.
+ *  maxk_tile_plan_shape: (num_groups, group_size, splits) for num_cus CUs --
+ *    groups of <= 2048 (k = 32) / 1024 (k = 64) destinations and source
+ *    ranges so that about one workgroup runs per CU.
+ *  maxk_tile_plan_build: call once with headers == NULL (count call): writes
+ *    sizes (host int64[3]) = {header entries, records (int32x2), largest
+ *    padded per-segment record count}; the plan is usable only if sizes[2] <=
+ *    65535.  Then call with headers int32x4[sizes[0]], header_start
+ *    int64[G*S*16], records int32x2[sizes[1]], record_start int64[G*S*16],
+ *    num_chunks int32[G*S] and optionally edge_record int32[E] (the record of
+ *    each CSR edge, for maxk_tile_plan_set_values).  Both calls synchronise
+ *    the stream once.  Deterministic: records keep CSR order per segment.
+ *  maxk_tile_plan_set_values: records' values := values (after the graph's
+ *    edge values changed; the plan's structure does not depend on them). */
+int maxk_tile_plan_shape(int num_cols, int num_cus, int dim_k, int *num_groups, int *group_size,
+                         int *splits);
+size_t maxk_tile_plan_workspace_bytes(int64_t num_edges, int num_workgroups);
+int maxk_tile_plan_build(const int32_t *indptr, const int32_t *indices, const float *values,
+                         int num_rows, int num_cols, int64_t num_edges, int dim_k, int num_groups,
+                         int group_size, int splits, void *headers, int64_t header_capacity,
+                         int64_t *header_start, void *records, int64_t record_capacity,
+                         int64_t *record_start, int32_t *num_chunks, int32_t *edge_record,
+                         int64_t *sizes, void *workspace, size_t workspace_bytes, void *stream);
+int maxk_tile_plan_set_values(const int32_t *edge_record, const float *values, int64_t num_edges,
+                              void *records, void *stream);
 
 /* ---------------------------------------------------------------------------
  * CBSR producer (MaxK top-k) and dense-gradient scatter.

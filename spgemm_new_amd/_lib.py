@@ -61,6 +61,12 @@ SIGNATURES = {
                                             _P]),
     "maxk_sspmm_backward_tile": (_I, [_P, _P, _P, _P, _P, _I, _I, _I, _P, _P, _P, _I, _I, _I, _I,
                                       _P, _P, _P]),
+    "maxk_tile_plan_shape": (_I, [_I, _I, _I, ctypes.POINTER(_I), ctypes.POINTER(_I),
+                                  ctypes.POINTER(_I)]),
+    "maxk_tile_plan_workspace_bytes": (_S, [_L, _I]),
+    "maxk_tile_plan_build": (_I, [_P, _P, _P, _I, _I, _L, _I, _I, _I, _I, _P, _L, _P, _P, _L, _P,
+                                  _P, _P, ctypes.POINTER(ctypes.c_int64), _P, _S, _P]),
+    "maxk_tile_plan_set_values": (_I, [_P, _P, _L, _P, _P]),
     "maxk_cbsr_packed_row_bytes": (_S, [_I]),
     "maxk_cbsr_pack": (_I, [_P, _P, _I, _I, _P, _P]),
     "maxk_spgemm_forward_packed": (_I, [_P, _L, _P, _P, _P, _P, _I, _I, _I, _P, _P, _S, _P]),

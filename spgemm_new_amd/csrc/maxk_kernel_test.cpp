@@ -15,7 +15,8 @@
 //                   this is the library's HIP dense SpMM on the same input)
 //   maxk            forward SpGEMM (merge-path schedule, no pre-zeroing)
 //   maxk_backward   backward SSpMM, the fastest of the algorithms below
-//   maxk_backward_{atomic,staged,local}
+//   maxk_backward_{atomic,staged,local,tile}   (tile: k in {32, 64}; its plan
+//                   from maxk_tile_plan_build, as MaxKGraph.tile_plan builds it)
 // Each time is the mean of 4 runs after 4 warm-ups, each run followed by a
 // device synchronise (spmm_base.h:58-75).  --check compares the forward
 // with the dense SpMM of the densified input (main.cu:18-48's check_err) and
@@ -296,6 +297,41 @@ void test_graph(const std::string &dir, const std::string &graph, int idx, int c
             for (void *p : {(void *)L.dstart, (void *)L.woff, (void *)L.erc, (void *)L.perm,
                             (void *)L.ev, (void *)L.seg, ws})
                 HIPCHECK(hipFree(p));
+        }
+        if ((k == 32 || k == 64) && E > 0) {
+            int G = 0, GS = 0, NS = 0;
+            MAXKCHECK(maxk_tile_plan_shape(V, prop.multiProcessorCount, k, &G, &GS, &NS));
+            const size_t b = maxk_tile_plan_workspace_bytes(E, G * NS);
+            void *ws = dev_alloc<char>(b);
+            int64_t sizes[3] = {0, 0, 0};
+            MAXKCHECK(maxk_tile_plan_build(indptr, indices, val, V, V, E, k, G, GS, NS, nullptr, 0,
+                                           nullptr, nullptr, 0, nullptr, nullptr, nullptr, sizes, ws,
+                                           b, st));
+            if (sizes[2] <= 0xFFFF) {
+                const int nw = G * NS * 16;
+                void *hdrs = dev_alloc<int32_t>((size_t)sizes[0] * 4);
+                void *recs = dev_alloc<int32_t>((size_t)sizes[1] * 2);
+                int64_t *hstart = dev_alloc<int64_t>(nw), *rstart = dev_alloc<int64_t>(nw);
+                int32_t *nch = dev_alloc<int32_t>((size_t)G * NS);
+                MAXKCHECK(maxk_tile_plan_build(indptr, indices, val, V, V, E, k, G, GS, NS, hdrs,
+                                               sizes[0], hstart, recs, sizes[1], rstart, nch, nullptr,
+                                               sizes, ws, b, st));
+                std::vector<float> zeros(kDimOrigin, 0.f);
+                float *zero_row = to_device(zeros);
+                float *part = NS > 1 ? dev_alloc<float>((size_t)(NS - 1) * V * k) : nullptr;
+                const double t = time_ms([&] {
+                    MAXKCHECK(maxk_sspmm_backward_tile(hdrs, hstart, recs, rstart, nch, G, NS, GS,
+                                                       dense, zero_row, sel, V, V, kDimOrigin, k,
+                                                       dxs, part, st));
+                });
+                std::printf("%s maxk_backward_tile %g\n", out.c_str(), t);
+                compare("tile");
+                best = std::min(best, t);
+                for (void *q : {hdrs, recs, (void *)hstart, (void *)rstart, (void *)nch,
+                                (void *)zero_row, (void *)part})
+                    if (q) HIPCHECK(hipFree(q));
+            }
+            HIPCHECK(hipFree(ws));
         }
         std::printf("%s maxk_backward %g\n", out.c_str(), best);
         std::fflush(stdout);

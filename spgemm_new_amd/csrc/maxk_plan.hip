@@ -9,7 +9,12 @@
 //    in-degree, at most dmax destinations each), every range's in-edges in
 //    source-row order packed as (row | c_local << 24, value), and the
 //    permutation that produced them;
-//  * maxk_local_bands_build: the per-band first edge of every range.
+//  * maxk_local_bands_build: the per-band first edge of every range;
+//  * maxk_tile_plan_build: the TILE backward's header and record streams
+//    (destination groups x source ranges, 47-row chunks of each workgroup's
+//    distinct source rows; format above bwd_tile_kernel in maxk_spgemm.hip),
+//    and maxk_tile_plan_set_values, which rewrites the records' edge values
+//    in place when the graph's values change.
 //
 // The reference has no counterpart (its backward takes the same .warp4 chunk
 // list as the forward, kernels/spmm_maxk_backward.cu:117-139); these replace
@@ -199,6 +204,259 @@ size_t scan_temp_bytes(int64_t n)
     return bytes;
 }
 
+// ----------------------------------------------------------------- TILE
+// Plan of bwd_tile_kernel (format above it in maxk_spgemm.hip).  Edge e =
+// (row r, column d): destination group d / GS, source range split(r) (rows
+// cut at floor(s * V / NS)), workgroup wg = group * NS + range.  Within a
+// workgroup, the distinct source rows (ascending) are cut into 47-row chunks;
+// an edge's segment is (wg, wave, chunk, lane half) with wave = (d % GS) % 16.
+// Segments are numbered in record-stream order, (wg, wave)-major:
+//   seg = ((chunk_base[wg] * 16 + wave * nch[wg] + chunk) * 2 + half),
+// and within a segment the records keep CSR edge order (two stable sorts).
+constexpr int kTileWaves = 16;
+constexpr int kTileRows = 47;
+constexpr int kTileBufRows = 48;
+constexpr int kTileRecPad = 512;   // records of over-read padding after the stream
+constexpr int kTileHdrPad = 8;     // header entries of padding
+
+__device__ __forceinline__ int tile_split(int r, int V, int NS)
+{
+    int s = 0;
+    for (int i = 1; i < NS; ++i) s += ((int64_t)i * V / NS) <= r;
+    return s;
+}
+
+__global__ void tile_edge_kernel(const int32_t *__restrict__ indptr, int num_rows,
+                                 const int32_t *__restrict__ indices, int64_t num_edges, int GS,
+                                 int NS, int32_t *__restrict__ wg_key, int32_t *__restrict__ erow)
+{
+    const int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (e >= num_edges) return;
+    const int r = (int)(upper_bound(indptr, (int64_t)num_rows + 1, e) - 1);
+    erow[e] = r;
+    wg_key[e] = (indices[e] / GS) * NS + tile_split(r, num_rows, NS);
+}
+
+// flag[i] = 1 where the wg-sorted edge i starts a new (workgroup, row) pair
+__global__ void tile_flag_kernel(const int32_t *__restrict__ wgs, const int32_t *__restrict__ perm,
+                                 const int32_t *__restrict__ erow, int64_t n,
+                                 int32_t *__restrict__ flag)
+{
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    flag[i] = (i == 0 || wgs[i] != wgs[i - 1] || erow[perm[i]] != erow[perm[i - 1]]) ? 1 : 0;
+}
+
+// the distinct (workgroup, row) pairs; uidx = inclusive scan of the flags
+__global__ void tile_unique_kernel(const int32_t *__restrict__ uidx, const int32_t *__restrict__ wgs,
+                                   const int32_t *__restrict__ perm, const int32_t *__restrict__ erow,
+                                   int64_t n, int32_t *__restrict__ urow, int32_t *__restrict__ uwg)
+{
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n || (i > 0 && uidx[i] == uidx[i - 1])) return;
+    const int u = uidx[i] - 1;
+    urow[u] = erow[perm[i]];
+    uwg[u] = wgs[i];
+}
+
+// wg_start[b] = first distinct pair of workgroup b (b in [0, NWG]); nch_in[b] =
+// its chunk count (input of the chunk_base scan, nch_in[NWG] = 0)
+__global__ void tile_wg_kernel(const int32_t *__restrict__ uwg, const int32_t *__restrict__ num_unique,
+                               int NWG, int32_t *__restrict__ wg_start)
+{
+    const int b = blockIdx.x * blockDim.x + threadIdx.x;
+    if (b <= NWG) wg_start[b] = (int32_t)lower_bound(uwg, *num_unique, b);
+}
+
+__global__ void tile_nch_kernel(const int32_t *__restrict__ wg_start, int NWG,
+                                int32_t *__restrict__ nch_in, int32_t *__restrict__ num_chunks)
+{
+    const int b = blockIdx.x * blockDim.x + threadIdx.x;
+    if (b > NWG) return;
+    const int n = b < NWG ? (wg_start[b + 1] - wg_start[b] + kTileRows - 1) / kTileRows : 0;
+    nch_in[b] = n;
+    if (num_chunks && b < NWG) num_chunks[b] = n;
+}
+
+__device__ __forceinline__ void tile_edge_place(int32_t e, int32_t wg, int32_t u,
+                                                const int32_t *__restrict__ indices,
+                                                const int32_t *__restrict__ wg_start, int GS, int k,
+                                                int &wave, int &slot, int &half, int &chunk, int &rin)
+{
+    const int ri = u - wg_start[wg];
+    chunk = ri / kTileRows;
+    rin = ri - chunk * kTileRows;
+    const int j = indices[e] % GS;
+    wave = j % kTileWaves;
+    const int q = j / kTileWaves;
+    slot = k == 32 ? q >> 1 : q;
+    half = k == 32 ? q & 1 : 0;
+}
+
+__global__ void tile_seg_kernel(const int32_t *__restrict__ perm, const int32_t *__restrict__ wgs,
+                                const int32_t *__restrict__ uidx, const int32_t *__restrict__ indices,
+                                const int32_t *__restrict__ wg_start,
+                                const int32_t *__restrict__ chunk_base, int GS, int k, int64_t n,
+                                int32_t *__restrict__ seg)
+{
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const int wg = wgs[i];
+    int wave, slot, half, chunk, rin;
+    tile_edge_place(perm[i], wg, uidx[i] - 1, indices, wg_start, GS, k, wave, slot, half, chunk, rin);
+    const int nch = chunk_base[wg + 1] - chunk_base[wg];
+    seg[i] = ((chunk_base[wg] * kTileWaves + wave * nch + chunk) << 1) + half;
+}
+
+// pad[s] = record count of segment s rounded up to 4 (s < bound; pad[bound] = 0);
+// max over the segments into *max_pad (zeroed before)
+__global__ void tile_pad_kernel(const int32_t *__restrict__ segs, int64_t n, int64_t bound,
+                                int32_t *__restrict__ pad, int32_t *__restrict__ max_pad)
+{
+    const int64_t s = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    int p = 0;
+    if (s < bound) {
+        const int64_t c = lower_bound(segs, n, s + 1) - lower_bound(segs, n, s);
+        p = (int)((c + 3) & ~int64_t(3));
+        pad[s] = p;
+    } else if (s == bound) {
+        pad[s] = 0;
+    }
+    for (int o = 32; o > 0; o >>= 1) p = max(p, __shfl_xor(p, o));
+    if ((threadIdx.x & 63) == 0 && p > 0) atomicMax(max_pad, p);
+}
+
+// sizes: header entries, records (both with padding), max padded segment
+__global__ void tile_sizes_kernel(const int32_t *__restrict__ chunk_base, int NWG,
+                                  const int64_t *__restrict__ rec_off,
+                                  const int32_t *__restrict__ max_pad, int64_t *__restrict__ sizes)
+{
+    const int64_t chunks = chunk_base[NWG];
+    sizes[0] = kTileWaves * (chunks + 2 * (int64_t)NWG) + kTileHdrPad;
+    sizes[1] = rec_off[chunks * 2 * kTileWaves] + kTileRecPad;
+    sizes[2] = *max_pad;
+}
+
+__global__ void tile_starts_kernel(const int32_t *__restrict__ chunk_base,
+                                   const int64_t *__restrict__ rec_off, int NWG,
+                                   int64_t *__restrict__ header_start,
+                                   int64_t *__restrict__ record_start)
+{
+    const int t = blockIdx.x * blockDim.x + threadIdx.x;
+    if (t >= NWG * kTileWaves) return;
+    const int b = t / kTileWaves, w = t % kTileWaves;
+    const int64_t nch = chunk_base[b + 1] - chunk_base[b];
+    header_start[t] = kTileWaves * ((int64_t)chunk_base[b] + 2 * (int64_t)b) + w * (nch + 2);
+    record_start[t] = rec_off[((int64_t)chunk_base[b] * kTileWaves + w * nch) * 2];
+}
+
+// header entry t of (workgroup b, wave w), index i: counts of chunk i - 2 and
+// the source rows of the wave's three DMA pieces of chunk i (-1 = zero row)
+__global__ void tile_headers_kernel(const int32_t *__restrict__ chunk_base,
+                                    const int32_t *__restrict__ wg_start,
+                                    const int32_t *__restrict__ urow,
+                                    const int32_t *__restrict__ pad, int NWG, int64_t capacity,
+                                    int4 *__restrict__ hdrs)
+{
+    const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (t >= capacity) return;
+    int4 out = make_int4(0, 0, 0, 0);
+    const int64_t total = kTileWaves * ((int64_t)chunk_base[NWG] + 2 * (int64_t)NWG);
+    if (t < total) {
+        int lo = 0, hi = NWG;  // last b with 16 * (chunk_base[b] + 2b) <= t
+        while (hi - lo > 1) {
+            const int mid = (lo + hi) >> 1;
+            if (kTileWaves * ((int64_t)chunk_base[mid] + 2 * (int64_t)mid) <= t) lo = mid; else hi = mid;
+        }
+        const int b = lo;
+        const int64_t nch = chunk_base[b + 1] - chunk_base[b];
+        const int64_t local = t - kTileWaves * ((int64_t)chunk_base[b] + 2 * (int64_t)b);
+        const int w = (int)(local / (nch + 2));
+        const int i = (int)(local % (nch + 2));
+        if (i >= 2) {
+            const int64_t s0 = (((int64_t)chunk_base[b] * kTileWaves + w * nch + (i - 2)) << 1);
+            out.x = pad[s0] | (pad[s0 + 1] << 16);
+        }
+        const int nrows = wg_start[b + 1] - wg_start[b];
+        int rr[3];
+        for (int p = 0; p < 3; ++p) {
+            const int li = w * 3 + p;
+            const int64_t r = (int64_t)i * kTileRows + li;
+            rr[p] = (li < kTileRows && r < nrows) ? urow[wg_start[b] + r] : -1;
+        }
+        out.y = rr[0];
+        out.z = rr[1];
+        out.w = rr[2];
+    }
+    hdrs[t] = out;
+}
+
+__global__ void tile_records_init_kernel(int2 *__restrict__ recs, int64_t capacity)
+{
+    const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (t < capacity) recs[t] = make_int2((kTileBufRows - 1) << 24, 0);  // slot 0, zero row, 0
+}
+
+__global__ void tile_records_kernel(const int32_t *__restrict__ segs, const int32_t *__restrict__ perm2,
+                                    const int32_t *__restrict__ perm, const int32_t *__restrict__ wgs,
+                                    const int32_t *__restrict__ uidx,
+                                    const int32_t *__restrict__ wg_start,
+                                    const int32_t *__restrict__ indices,
+                                    const float *__restrict__ values,
+                                    const int64_t *__restrict__ rec_off, int GS, int k, int64_t n,
+                                    int64_t capacity, int2 *__restrict__ recs,
+                                    int32_t *__restrict__ edge_record)
+{
+    const int64_t j = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (j >= n) return;
+    const int32_t s = segs[j];
+    const int64_t first = lower_bound(segs, n, s);  // rank within the segment = j - first
+    const int32_t i = perm2[j];
+    const int32_t e = perm[i];
+    int wave, slot, half, chunk, rin;
+    tile_edge_place(e, wgs[i], uidx[i] - 1, indices, wg_start, GS, k, wave, slot, half, chunk, rin);
+    const int64_t pos = rec_off[s] + (j - first);
+    if (pos >= capacity) return;
+    const uint32_t w0 = (uint32_t)slot | ((uint32_t)((chunk % 3) * kTileBufRows + rin) << 24);
+    recs[pos] = make_int2((int)w0, __float_as_int(values[e]));
+    if (edge_record) edge_record[e] = (int32_t)pos;
+}
+
+__global__ void tile_set_values_kernel(const int32_t *__restrict__ edge_record,
+                                       const float *__restrict__ values, int64_t n,
+                                       int2 *__restrict__ recs)
+{
+    const int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (e < n) recs[edge_record[e]].y = __float_as_int(values[e]);
+}
+
+size_t inclusive_scan_temp_bytes(int64_t n)
+{
+    size_t bytes = 0;
+    if (rocprim::inclusive_scan(nullptr, bytes, (const int32_t *)nullptr, (int32_t *)nullptr,
+                                (size_t)n, rocprim::plus<int32_t>()) != hipSuccess)
+        return 0;
+    return bytes;
+}
+
+size_t scan64_temp_bytes(int64_t n)
+{
+    size_t bytes = 0;
+    if (rocprim::exclusive_scan(nullptr, bytes, (const int32_t *)nullptr, (int64_t *)nullptr,
+                                int64_t(0), (size_t)n, rocprim::plus<int64_t>()) != hipSuccess)
+        return 0;
+    return bytes;
+}
+
+int64_t tile_seg_bound(int64_t num_edges, int nwg)
+{
+    // segments = 32 x chunks; chunks <= sum over workgroups of ceil(rows / 47)
+    // <= E / 47 + NWG (a workgroup's distinct rows never exceed its edges)
+    return 2 * kTileWaves * (num_edges / kTileRows + nwg + 1);
+}
+
+int tile_max_group(int k) { return (k == 32 ? 128 : 64) * kTileWaves; }
+
 }  // namespace
 
 extern "C" {
@@ -324,6 +582,162 @@ int maxk_local_bands_build(const int32_t *woff, const int32_t *edge_rc, int num_
     hipLaunchKernelGGL(local_bands_kernel, dim3((unsigned)blocks_for(n)), dim3(kThreads), 0,
                        static_cast<hipStream_t>(stream), woff, edge_rc, num_waves, num_rows,
                        num_bands, seg_edge_off);
+    return launch_status();
+}
+
+int maxk_tile_plan_shape(int num_cols, int num_cus, int dim_k, int *num_groups, int *group_size,
+                         int *splits)
+{
+    if (num_cols < 1 || num_cus < 1 || (dim_k != 32 && dim_k != 64) || !num_groups ||
+        !group_size || !splits)
+        return MAXK_E_ARG;
+    int64_t groups = (num_cols + (int64_t)tile_max_group(dim_k) - 1) / tile_max_group(dim_k);
+    int64_t ns = num_cus / groups;
+    ns = ns < 1 ? 1 : ns > 8 ? 8 : ns;
+    // as many groups as the CUs left over allow: smaller groups, same sweep
+    int64_t g2 = num_cus / ns < num_cols ? num_cus / ns : num_cols;
+    if (g2 > groups) groups = g2;
+    const int64_t size = (num_cols + groups - 1) / groups;
+    *num_groups = (int)((num_cols + size - 1) / size);
+    *group_size = (int)size;
+    *splits = (int)ns;
+    return MAXK_OK;
+}
+
+size_t maxk_tile_plan_workspace_bytes(int64_t num_edges, int num_workgroups)
+{
+    if (num_edges < 1 || num_workgroups < 1) return 0;
+    const int64_t bound = tile_seg_bound(num_edges, num_workgroups);
+    const size_t ea = align_up((size_t)num_edges * 4, 256);
+    size_t t = sort_temp_bytes(num_edges, bits_for(bound + 1));
+    const size_t t2 = inclusive_scan_temp_bytes(num_edges);
+    const size_t t3 = scan64_temp_bytes(bound + 1);
+    const size_t t4 = scan_temp_bytes((int64_t)num_workgroups + 1);
+    t = t > t2 ? t : t2;
+    t = t > t3 ? t : t3;
+    t = t > t4 ? t : t4;
+    return 9 * ea + 3 * align_up(((size_t)num_workgroups + 1) * 4, 256) +
+           align_up((size_t)(bound + 1) * 4, 256) + align_up((size_t)(bound + 1) * 8, 256) + 512 +
+           align_up(t, 256) + 256;
+}
+
+int maxk_tile_plan_build(const int32_t *indptr, const int32_t *indices, const float *values,
+                         int num_rows, int num_cols, int64_t num_edges, int dim_k, int num_groups,
+                         int group_size, int splits, void *headers, int64_t header_capacity,
+                         int64_t *header_start, void *records, int64_t record_capacity,
+                         int64_t *record_start, int32_t *num_chunks, int32_t *edge_record,
+                         int64_t *sizes, void *workspace, size_t workspace_bytes, void *stream)
+{
+    if (!indptr || !indices || !values || !sizes) return MAXK_E_ARG;
+    if ((dim_k != 32 && dim_k != 64) || num_rows < 1 || num_cols < 1 || num_edges < 1 ||
+        num_edges > INT32_MAX || num_groups < 1 || splits < 1 || splits > 64 || group_size < 1 ||
+        group_size > tile_max_group(dim_k) || (int64_t)num_groups * group_size < num_cols)
+        return MAXK_E_ARG;
+    const int NWG = num_groups * splits;
+    const int64_t bound = tile_seg_bound(num_edges, NWG);
+    if (bound + 1 > INT32_MAX) return MAXK_E_ARG;
+    if (!workspace || workspace_bytes < maxk_tile_plan_workspace_bytes(num_edges, NWG))
+        return MAXK_E_WORKSPACE;
+    const bool fill = headers != nullptr;
+    if (fill && (!records || !header_start || !record_start || !num_chunks)) return MAXK_E_ARG;
+    hipStream_t st = static_cast<hipStream_t>(stream);
+    const int64_t E = num_edges;
+    char *p = static_cast<char *>(workspace);
+    int32_t *key = carve<int32_t>(p, E);    // wg keys, then flags, then segment keys
+    int32_t *wgs = carve<int32_t>(p, E);    // wg keys sorted
+    int32_t *perm = carve<int32_t>(p, E);   // CSR edge of wg-sorted slot i
+    int32_t *erow = carve<int32_t>(p, E);   // source row per CSR edge
+    int32_t *uidx = carve<int32_t>(p, E);   // 1 + distinct-pair index of wg-sorted slot i
+    int32_t *urow = carve<int32_t>(p, E);
+    int32_t *uwg = carve<int32_t>(p, E);
+    int32_t *segs = carve<int32_t>(p, E);   // segment keys sorted
+    int32_t *perm2 = carve<int32_t>(p, E);  // wg-sorted slot of segment-sorted slot j
+    int32_t *wg_start = carve<int32_t>(p, (size_t)NWG + 1);
+    int32_t *nch_in = carve<int32_t>(p, (size_t)NWG + 1);
+    int32_t *chunk_base = carve<int32_t>(p, (size_t)NWG + 1);
+    int32_t *pad = carve<int32_t>(p, (size_t)bound + 1);
+    int64_t *rec_off = carve<int64_t>(p, (size_t)bound + 1);
+    int32_t *max_pad = carve<int32_t>(p, 2);
+    int64_t *dsizes = carve<int64_t>(p, 4);
+    void *tmp = p;
+    const size_t tmp_bytes = workspace_bytes - (size_t)(p - static_cast<char *>(workspace));
+    const unsigned eb = (unsigned)blocks_for(E);
+    const unsigned wb = (unsigned)blocks_for((int64_t)NWG + 1);
+    rocprim::counting_iterator<int32_t> iota(0);
+    size_t tb;
+    hipError_t e;
+    int rc;
+
+    hipLaunchKernelGGL(tile_edge_kernel, dim3(eb), dim3(kThreads), 0, st, indptr, num_rows, indices,
+                       E, group_size, splits, key, erow);
+    if ((rc = launch_status())) return rc;
+    tb = tmp_bytes;
+    e = rocprim::radix_sort_pairs(tmp, tb, key, wgs, iota, perm, (size_t)E, 0u, bits_for(NWG), st);
+    if (e != hipSuccess) return (int)e;
+    hipLaunchKernelGGL(tile_flag_kernel, dim3(eb), dim3(kThreads), 0, st, wgs, perm, erow, E, key);
+    if ((rc = launch_status())) return rc;
+    tb = tmp_bytes;
+    e = rocprim::inclusive_scan(tmp, tb, key, uidx, (size_t)E, rocprim::plus<int32_t>(), st);
+    if (e != hipSuccess) return (int)e;
+    hipLaunchKernelGGL(tile_unique_kernel, dim3(eb), dim3(kThreads), 0, st, uidx, wgs, perm, erow, E,
+                       urow, uwg);
+    hipLaunchKernelGGL(tile_wg_kernel, dim3(wb), dim3(kThreads), 0, st, uwg, uidx + (E - 1), NWG,
+                       wg_start);
+    hipLaunchKernelGGL(tile_nch_kernel, dim3(wb), dim3(kThreads), 0, st, wg_start, NWG, nch_in,
+                       fill ? num_chunks : nullptr);
+    if ((rc = launch_status())) return rc;
+    tb = tmp_bytes;
+    e = rocprim::exclusive_scan(tmp, tb, nch_in, chunk_base, 0, (size_t)NWG + 1,
+                                rocprim::plus<int32_t>(), st);
+    if (e != hipSuccess) return (int)e;
+    hipLaunchKernelGGL(tile_seg_kernel, dim3(eb), dim3(kThreads), 0, st, perm, wgs, uidx, indices,
+                       wg_start, chunk_base, group_size, dim_k, E, key);
+    if ((rc = launch_status())) return rc;
+    tb = tmp_bytes;
+    e = rocprim::radix_sort_pairs(tmp, tb, key, segs, iota, perm2, (size_t)E, 0u,
+                                  bits_for(bound + 1), st);
+    if (e != hipSuccess) return (int)e;
+    if ((e = hipMemsetAsync(max_pad, 0, sizeof(int32_t), st)) != hipSuccess) return (int)e;
+    hipLaunchKernelGGL(tile_pad_kernel, dim3((unsigned)blocks_for(bound + 1)), dim3(kThreads), 0, st,
+                       segs, E, bound, pad, max_pad);
+    if ((rc = launch_status())) return rc;
+    tb = tmp_bytes;
+    e = rocprim::exclusive_scan(tmp, tb, pad, rec_off, int64_t(0), (size_t)bound + 1,
+                                rocprim::plus<int64_t>(), st);
+    if (e != hipSuccess) return (int)e;
+    hipLaunchKernelGGL(tile_sizes_kernel, dim3(1), dim3(1), 0, st, chunk_base, NWG, rec_off, max_pad,
+                       dsizes);
+    if ((rc = launch_status())) return rc;
+    if (fill) {
+        hipLaunchKernelGGL(tile_starts_kernel, dim3((unsigned)blocks_for((int64_t)NWG * kTileWaves)),
+                           dim3(kThreads), 0, st, chunk_base, rec_off, NWG, header_start,
+                           record_start);
+        hipLaunchKernelGGL(tile_headers_kernel, dim3((unsigned)blocks_for(header_capacity)),
+                           dim3(kThreads), 0, st, chunk_base, wg_start, urow, pad, NWG,
+                           header_capacity, static_cast<int4 *>(headers));
+        hipLaunchKernelGGL(tile_records_init_kernel, dim3((unsigned)blocks_for(record_capacity)),
+                           dim3(kThreads), 0, st, static_cast<int2 *>(records), record_capacity);
+        hipLaunchKernelGGL(tile_records_kernel, dim3(eb), dim3(kThreads), 0, st, segs, perm2, perm,
+                           wgs, uidx, wg_start, indices, values, rec_off, group_size, dim_k, E,
+                           record_capacity, static_cast<int2 *>(records), edge_record);
+        if ((rc = launch_status())) return rc;
+    }
+    e = hipMemcpyAsync(sizes, dsizes, 3 * sizeof(int64_t), hipMemcpyDeviceToHost, st);
+    if (e == hipSuccess) e = hipStreamSynchronize(st);
+    if (e != hipSuccess) return (int)e;
+    if (fill && (sizes[0] > header_capacity || sizes[1] > record_capacity)) return MAXK_E_WORKSPACE;
+    if (fill && sizes[2] > 0xFFFF) return MAXK_E_ARG;
+    return MAXK_OK;
+}
+
+int maxk_tile_plan_set_values(const int32_t *edge_record, const float *values, int64_t num_edges,
+                              void *records, void *stream)
+{
+    if (!edge_record || !values || !records || num_edges < 0) return MAXK_E_ARG;
+    if (num_edges == 0) return MAXK_OK;
+    hipLaunchKernelGGL(tile_set_values_kernel, dim3((unsigned)blocks_for(num_edges)), dim3(kThreads),
+                       0, static_cast<hipStream_t>(stream), edge_record, values, num_edges,
+                       static_cast<int2 *>(records));
     return launch_status();
 }
 

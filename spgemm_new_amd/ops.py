@@ -296,7 +296,9 @@ class MaxKGraph:
     def tile_plan(self, dim_k: int = 32):
         """Plan of the TILE backward (k = 32 or 64, h = 256; spgemm_new_amd/tile.py),
         or None when the shape does not suit it (then the other algorithms serve
-        it).  Built once per k with torch sorts on the device."""
+        it).  Built once per k on the device (maxk_tile_plan_build).  The
+        records carry the graph's edge values: when ``self.values`` has changed
+        in place since, they are rewritten first (one scatter, tile.set_values)."""
         if dim_k not in self._tile:
             from . import tile
             plan = None
@@ -311,7 +313,12 @@ class MaxKGraph:
                 plan["part"] = torch.empty(max(1, (NS - 1) * self.num_cols * dim_k),
                                            dtype=torch.float32, device=self.device)
             self._tile[dim_k] = plan
-        return self._tile[dim_k]
+        plan = self._tile[dim_k]
+        if plan is not None and plan["values_key"] != _tensor_key(self.values):
+            from . import tile
+            tile.set_values(plan, self.values[: self.num_edges])
+            plan["values_key"] = _tensor_key(self.values)
+        return plan
 
     def local_fits(self, dim_k: int) -> bool:
         """True when the LOCAL plan's waves are all co-resident (one sweep of G)."""
@@ -328,19 +335,36 @@ class MaxKGraph:
         """MAXK_BWD_AUTO: the fastest algorithm for this graph and k, measured once
         (each candidate run once, then timed AUTOTUNE_REPS times with HIP events on
         the current stream, the minimum kept) and cached.  Candidates: STAGED,
-        ATOMIC, and LOCAL when its plan exists.  During stream capture, or before any measurement,
-        STAGED is used (allocation-free once its workspace exists)."""
+        ATOMIC, LOCAL when its plan exists, TILE for k in {32, 64}, h = 256 and the
+        graph's own values.  During stream capture nothing is timed: the choice
+        already measured for the shape, else TILE if its plan exists, else STAGED.
+        With several timed candidates within noise the minimum decides, so the
+        choice (and with it the fp32 summation order) is fixed per graph and
+        shape once made; MAXK_BWD_* pins one explicitly."""
         k = sel.shape[1]
-        key = (k, grad.shape[1])
+        own = values is None or values is self.values
+        # TILE's records hold the graph's own values, so the choice is kept per
+        # (k, h, own values): a call with other values never gets TILE back
+        key = (k, grad.shape[1], own)
         if key in self._bwd_choice:
             return self._bwd_choice[key]
-        if self.num_edges == 0 or torch.cuda.is_current_stream_capturing():
+        tile_ok = TILE_AUTO and own and tile_shape_ok(k, grad.shape[1])
+        if self.num_edges == 0:
+            return _lib.MAXK_BWD_STAGED
+        if torch.cuda.is_current_stream_capturing():
+            # nothing can be timed (or planned) while a graph is captured: the
+            # choice measured for the same shape with the graph's own values,
+            # else TILE when its plan was built before the capture, else STAGED
+            hit = self._bwd_choice.get((k, grad.shape[1], True))
+            if hit is not None and (own or hit != _lib.MAXK_BWD_TILE):
+                return hit
+            if tile_ok and self._tile.get(k) is not None:
+                return _lib.MAXK_BWD_TILE
             return _lib.MAXK_BWD_STAGED
         cands = [_lib.MAXK_BWD_STAGED, _lib.MAXK_BWD_ATOMIC]
         if self.local_plan(k) is not None:
             cands.append(_lib.MAXK_BWD_LOCAL)
-        if TILE_AUTO and tile_shape_ok(k, grad.shape[1]) and values is self.values and \
-                self.tile_plan(k) is not None:
+        if tile_ok and self.tile_plan(k) is not None:
             cands.append(_lib.MAXK_BWD_TILE)
         best, best_ms = None, float("inf")
         for a in cands:

@@ -24,18 +24,22 @@ module builds, once per graph, the streams the kernel walks:
   w >> 2, its byte offset (w << 3) & 24 and the LDS byte address of the row
   w >> 14.
 
-The plan is built with torch sorts on the graph's device (no host loop);
-``emulate`` replays it on the CPU (test infrastructure: it checks the format
-against the oracle without a GPU).
+The plan is built on the graph's device by the library
+(maxk_tile_plan_build, csrc/maxk_plan.hip: two stable rocPRIM radix sorts, no
+host loop); ``emulate`` replays a plan on the CPU (test infrastructure: it
+checks the format against the oracle without a GPU).
 """
 from __future__ import annotations
 
+import ctypes
+
 import torch
+
+from . import _lib
 
 WAVES = 16
 CHUNK_ROWS = 47
 BUF_ROWS = 48
-MAX_GROUP = 128 * WAVES     # k = 32: two destinations per slot register
 
 
 def max_group(k: int) -> int:
@@ -43,124 +47,70 @@ def max_group(k: int) -> int:
 
 
 def choose_shape(num_cols: int, cus: int = 256, k: int = 32) -> tuple[int, int, int]:
-    """(num_groups, group_size, splits): groups of <= 2048 destinations, and
-    source ranges so that num_groups * splits fills about one workgroup per CU."""
-    groups = -(-num_cols // max_group(k))
-    splits = max(1, min(8, cus // groups))
-    # as many groups as the CUs left over allow: smaller groups, same sweep
-    groups = max(groups, min(cus // splits, num_cols))
-    size = -(-num_cols // groups)
-    groups = -(-num_cols // size)
-    return groups, size, splits
+    """(num_groups, group_size, splits): groups of <= max_group(k) destinations,
+    and source ranges so that num_groups * splits fills about one workgroup per
+    CU (maxk_tile_plan_shape)."""
+    L = _lib.load()
+    g, s, n = ctypes.c_int(0), ctypes.c_int(0), ctypes.c_int(0)
+    _lib.check(L.maxk_tile_plan_shape(num_cols, cus, k, ctypes.byref(g), ctypes.byref(s),
+                                      ctypes.byref(n)), "maxk_tile_plan_shape")
+    return g.value, s.value, n.value
 
 
 def build(indptr: torch.Tensor, indices: torch.Tensor, values: torch.Tensor, num_rows: int,
           num_cols: int, cus: int = 256, shape: tuple[int, int, int] | None = None, k: int = 32):
-    """The TILE plan as a dict, or None when a chunk would overflow a wave's
-    64-slot segment (many edges of few source rows into one wave's
-    destinations; the other algorithms serve such graphs)."""
+    """The TILE plan as a dict (maxk_tile_plan_build on the graph's device), or
+    None when a chunk would overflow a wave's 64-slot segment (many edges of
+    few source rows into one wave's destinations; the other algorithms serve
+    such graphs).  indptr[0] == 0 and indices / values hold exactly the graph's
+    edges.  ``edge_record`` maps each CSR edge to its record, so a change of
+    the graph's values is one maxk_tile_plan_set_values call (set_values)."""
     dev = indices.device
     E = indices.numel()
-    if E == 0 or num_rows < 1 or num_cols < 1:
-        return None
-    if k not in (32, 64):
+    if E == 0 or num_rows < 1 or num_cols < 1 or k not in (32, 64):
         return None
     G, GS, NS = shape or choose_shape(num_cols, cus, k)
     if GS > max_group(k):
         return None
+    L = _lib.load()
     NWG = G * NS
-    V = num_rows
-    i64 = dict(dtype=torch.int64, device=dev)
-    deg = (indptr[1:] - indptr[:-1]).long()
-    rows = torch.repeat_interleave(torch.arange(V, **i64), deg)
-    d = indices.long()
-    grp = d // GS
-    j = d - grp * GS
-    w = j % WAVES
-    q = j // WAVES
-    if k == 32:
-        slot, half = q >> 1, q & 1
-    else:                                  # k = 64: one destination per slot register
-        slot, half = q, torch.zeros_like(q)
-    bounds = (torch.arange(NS + 1, **i64) * V) // NS
-    split = torch.bucketize(rows, bounds[1:NS], right=True)
-    wg = grp * NS + split
-    del d, j, q, grp, split
-    # distinct source rows per workgroup, and each edge's row index in that list
-    key = wg * V + rows
-    ukey, inv = torch.unique(key, sorted=True, return_inverse=True)
-    del key
-    uwg = ukey // V
-    urow = (ukey - uwg * V).to(torch.int32)
-    wg_start = torch.searchsorted(uwg, torch.arange(NWG + 1, **i64))
-    nrows = wg_start[1:] - wg_start[:-1]
-    ri = inv - wg_start[wg]
-    del inv
-    c = ri // CHUNK_ROWS
-    rin = ri - c * CHUNK_ROWS
-    del ri
-    nch = (nrows + CHUNK_ROWS - 1) // CHUNK_ROWS
-    maxch = max(1, int(nch.max()))
-    # segments (workgroup, wave, chunk, half): record counts, padded to 4
-    seg = ((wg * WAVES + w) * maxch + c) * 2 + half
-    cnt = torch.bincount(seg, minlength=NWG * WAVES * maxch * 2).view(NWG, WAVES, maxch, 2)
-    pad = (cnt + 3) // 4 * 4
-    if int(pad.max()) > 0xFFFF:
+    ws = torch.empty(max(1, L.maxk_tile_plan_workspace_bytes(E, NWG)), dtype=torch.uint8,
+                     device=dev)
+    st = _lib.stream_ptr(dev)
+    sizes = (ctypes.c_int64 * 3)()
+    args = (indptr.data_ptr(), indices.data_ptr(), values.data_ptr(), num_rows, num_cols, E, k,
+            G, GS, NS)
+    _lib.check(L.maxk_tile_plan_build(*args, None, 0, None, None, 0, None, None, None, sizes,
+                                      ws.data_ptr(), ws.numel(), st), "maxk_tile_plan_build(count)")
+    if sizes[2] > 0xFFFF:
         return None
-    chunk_ok = torch.arange(maxch, **i64)[None, :] < nch[:, None]          # [NWG, maxch]
-    # record stream: (workgroup, wave) major, then chunk, then half
-    nrec = pad.sum(-1)                                                    # [NWG, 16, maxch]
-    rlen = nrec.sum(-1).flatten()                                         # [NWG*16]
-    rstart = torch.cumsum(rlen, 0) - rlen
-    seg_off = rstart.view(NWG, WAVES, 1) + torch.cumsum(nrec, -1) - nrec  # first record of (wg,w,c)
-    total = int(rlen.sum()) + 512                                          # + 4 KB over-read pad
-    recs = torch.zeros(total, 2, dtype=torch.int32, device=dev)
-    recs[:, 0] = (BUF_ROWS - 1) << 24                                     # padding: slot 0, zero row
-    order = torch.argsort(seg, stable=True)
-    sseg = seg[order]
-    first = torch.searchsorted(sseg, sseg)
-    rank = torch.arange(E, **i64) - first
-    del first
-    h = sseg & 1
-    base_seg = sseg >> 1                                                  # (wg, w, c) flat
-    pos = seg_off.flatten()[base_seg] + h * pad.view(-1, 2)[base_seg, 0] + rank
-    del sseg, rank, base_seg, h
-    so = slot[order]
-    w0 = so | (((c % 3) * BUF_ROWS + rin)[order] << 24)
-    recs[pos, 0] = torch.where(w0 >= (1 << 31), w0 - (1 << 32), w0).to(torch.int32)
-    recs[pos, 1] = values[order].contiguous().view(torch.int32)
-    del order, pos, so, seg, slot, rin, c
-    # header stream: e(0), e(1), then e(c + 2) per chunk
-    wv = torch.arange(WAVES, **i64)
-
-    def piece_rows(cc: torch.Tensor) -> torch.Tensor:                   # cc [M] -> [NWG,16,M,3]
-        li = wv[None, :, None, None] * 3 + torch.arange(3, **i64)[None, None, None, :]
-        r = cc[None, None, :, None] * CHUNK_ROWS + li                     # row-list index
-        ok = (li < CHUNK_ROWS) & (r < nrows[:, None, None, None])
-        idx = torch.clamp(wg_start[:-1, None, None, None] + r, max=max(urow.numel() - 1, 0))
-        return torch.where(ok, urow[idx].long(), -1)
-
-    hlen = (nch + 2).repeat_interleave(WAVES)                             # [NWG*16]
-    hstart = torch.cumsum(hlen, 0) - hlen
-    hdrs = torch.zeros(int(hlen.sum()) + 8, 4, dtype=torch.int32, device=dev)
-    # e(i) for i in [0, maxch + 2): counts of chunk i-2, rows of chunk i
-    idx_e = torch.arange(maxch + 2, **i64)
-    rows_e = piece_rows(idx_e)                                            # [NWG,16,maxch+2,3]
-    cnt_e = torch.zeros(NWG, WAVES, maxch + 2, **i64)
-    cnt_e[..., 2:] = pad[..., 0] | (pad[..., 1] << 16)
-    ok_e = idx_e[None, :] < (nch + 2)[:, None]                            # [NWG, maxch+2]
-    okw = ok_e[:, None, :].expand(NWG, WAVES, maxch + 2)
-    hp = (hstart.view(NWG, WAVES, 1) + idx_e[None, None, :])[okw]
-    hdrs[hp, 0] = cnt_e[okw].to(torch.int32)
-    r3 = rows_e[okw]
-    hdrs[hp, 1] = r3[:, 0].to(torch.int32)
-    hdrs[hp, 2] = r3[:, 1].to(torch.int32)
-    hdrs[hp, 3] = r3[:, 2].to(torch.int32)
-    return {"headers": hdrs, "header_start": hstart.contiguous(), "records": recs,
-            "record_start": rstart.contiguous(), "num_chunks": nch.to(torch.int32).contiguous(),
-            "num_groups": G, "group_size": GS, "splits": NS, "num_rows": V, "num_cols": num_cols,
-            "k": k,
+    i32 = dict(dtype=torch.int32, device=dev)
+    i64 = dict(dtype=torch.int64, device=dev)
+    hdrs = torch.empty(sizes[0], 4, **i32)
+    recs = torch.empty(sizes[1], 2, **i32)
+    hstart, rstart = torch.empty(NWG * WAVES, **i64), torch.empty(NWG * WAVES, **i64)
+    nch = torch.empty(NWG, **i32)
+    edge_record = torch.empty(E, **i32)
+    _lib.check(L.maxk_tile_plan_build(*args, hdrs.data_ptr(), sizes[0], hstart.data_ptr(),
+                                      recs.data_ptr(), sizes[1], rstart.data_ptr(), nch.data_ptr(),
+                                      edge_record.data_ptr(), sizes, ws.data_ptr(), ws.numel(), st),
+               "maxk_tile_plan_build")
+    del ws
+    return {"headers": hdrs, "header_start": hstart, "records": recs, "record_start": rstart,
+            "num_chunks": nch, "edge_record": edge_record,
+            "num_groups": G, "group_size": GS, "splits": NS, "num_rows": num_rows,
+            "num_cols": num_cols, "k": k,
             "zero_row": torch.zeros(256, dtype=torch.float32, device=dev)}
+
+
+def set_values(plan, values: torch.Tensor) -> None:
+    """Rewrite the plan's record values from the graph's edge values (fp32[E])
+    after they changed in place (maxk_tile_plan_set_values)."""
+    L = _lib.load()
+    _lib.check(L.maxk_tile_plan_set_values(plan["edge_record"].data_ptr(), values.data_ptr(),
+                                           plan["edge_record"].numel(), plan["records"].data_ptr(),
+                                           _lib.stream_ptr(values.device)),
+               "maxk_tile_plan_set_values")
 
 
 def emulate(plan, grad: torch.Tensor, sel: torch.Tensor) -> torch.Tensor:

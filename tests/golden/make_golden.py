@@ -29,6 +29,14 @@ Outputs (tests/golden/*.npz, numpy, no pickle):
   kernel_k{K}.npz  from reference code: mask_bits = packbits(MaxK.apply(x,K) != 0),
                    Y = sparse.mm(adj, MaxK(x)), grad_x = d<Y, G>/dx through
                    MaxK.backward and sparse.mm
+  inputs_h256.npz  the SURVEY.md §8(c) shape: V=2048, h=256, degrees 0/1/63/64/
+                   65/129/257/700/1500 among Poisson-ish ones (> 13 blocks of
+                   12 warp4 chunks), seeded
+  kernel_h256_k{K}.npz  (K = 32, 64: the shapes of the TILE backward and the
+                   north-star config) mask_bits, Y, and grad_x compacted to the
+                   selected positions (grad_sel[r, j] = grad_x[r, j-th selected
+                   column], row-major column order) -- grad_x is zero elsewhere
+                   because MaxK.backward masks it (utils/models.py:52-59)
 """
 from __future__ import annotations
 
@@ -89,6 +97,31 @@ def main():
         np.savez(os.path.join(HERE, f"kernel_k{k}.npz"),
                  mask_bits=np.packbits(xm.detach().numpy() != 0, axis=1),
                  Y=y.detach().numpy(), grad_x=xt.grad.numpy(), k=np.int32(k))
+
+    # ---- SURVEY.md §8(c) shape: V=2048, h=256 (TILE / north-star k) --------
+    rng = np.random.default_rng(256)
+    v, h = 2048, 256
+    from spgemm_new_amd.graphs import small_csr
+    indptr, indices = small_csr(v, seed=29, extra_degrees=(0, 1, 63, 64, 65, 129, 257, 700, 1500))
+    values = rng.random(len(indices), dtype=np.float32)
+    x = rng.random((v, h), dtype=np.float32)
+    G = rng.random((v, h), dtype=np.float32)
+    rows = np.repeat(np.arange(v), np.diff(indptr))
+    adj = torch.sparse_coo_tensor(torch.from_numpy(np.stack([rows, indices]).astype(np.int64)),
+                                  torch.from_numpy(values), (v, v)).coalesce()
+    np.savez_compressed(os.path.join(HERE, "inputs_h256.npz"), indptr=indptr, indices=indices,
+                        values=values, x=x, G=G)
+    for k in (32, 64):
+        xt = torch.from_numpy(x).requires_grad_(True)
+        xm = ref.MaxK.apply(xt, k)
+        y = torch.sparse.mm(adj, xm)
+        y.backward(torch.from_numpy(G))
+        mask = xm.detach().numpy() != 0
+        gx = xt.grad.numpy()
+        assert np.all(gx[~mask] == 0) and np.all(mask.sum(1) == k)
+        np.savez_compressed(os.path.join(HERE, f"kernel_h256_k{k}.npz"),
+                            mask_bits=np.packbits(mask, axis=1), Y=y.detach().numpy(),
+                            grad_sel=gx[mask].reshape(v, k), k=np.int32(k))
     print("golden vectors written to", HERE)
 
 

@@ -7,8 +7,12 @@ reference on the same device:
 * forward vs rocSPARSE SpMM (torch.sparse.mm on the densified masked input),
   per element |got - ref| / max(1, |ref|) <= 1e-4;
 * backward via the exact adjoint identity <A . X^, G> = <X^_s, dXs> (both
-  sides summed in fp64), every backward algorithm agreeing within 1e-4, and
-  bit-exact linearity of the deterministic LOCAL path (dXs(2G) == 2 dXs(G));
+  sides summed in fp64), every backward algorithm (ATOMIC, STAGED, LOCAL, TILE)
+  agreeing with STAGED within 1e-4, bit-exact linearity of the deterministic
+  LOCAL path (dXs(2G) == 2 dXs(G)), TILE run-to-run identical and equal to
+  LOCAL bit for bit where its plan has one source range (Reddit k = 64);
+* config 5 (proteins, R = 8): fused forward vs 8 single calls, the
+  multi-relation adjoint identity, rel8 vs composed backward;
 * config 1 (Flickr h=64 k=16, the reference's own CPU case) against the fp64
   oracle at full size.
 """
@@ -28,8 +32,13 @@ def _rel(a, b):
     return float(((a - b).abs() / b.abs().clamp_min(1)).max())
 
 
-@pytest.mark.parametrize("graph,k", [("reddit", 32), ("products", 8), ("products", 64)])
+@pytest.mark.parametrize("graph,k", [("reddit", 32), ("reddit", 64), ("products", 8),
+                                     ("products", 16), ("products", 32), ("products", 64)])
 def test_full_size_properties(dev, graph, k):
+    """Every backward algorithm that serves the shape (TILE included: it is the
+    one AUTO and bench.py pick on Reddit k = 32 / 64 and products k = 64) at
+    BASELINE full size: the adjoint identity to 1e-6, agreement with STAGED
+    within 1e-4, and what AUTO picks is one of them."""
     V, E = CONFIGS[graph]
     h = 256
     indptr, indices = synthetic_csr_gpu(V, E, device=dev)
@@ -46,20 +55,88 @@ def test_full_size_properties(dev, graph, k):
     xm = torch.zeros_like(X).scatter_(1, sel.long(), data)
     ref = torch.sparse.mm(a, xm)
     assert _rel(y, ref) <= TOL
-    del a, ref
+    del a, ref, xm
     # backward: adjoint identity, algorithms agree
     algos = [_lib.MAXK_BWD_STAGED, _lib.MAXK_BWD_ATOMIC]
     if g.local_plan(k) is not None:   # slow on products (78 source bands) but must be right
         algos.append(_lib.MAXK_BWD_LOCAL)
-    outs = {a_: g.backward(Gr, sel, algo=a_) for a_ in algos}
+    tile_plan = g.tile_plan(k)
+    if tile_plan is not None:
+        algos.append(_lib.MAXK_BWD_TILE)
+    if graph == "reddit":
+        assert tile_plan is not None   # the benched backward must be covered here
     lhs = float((y.double() * Gr.double()).sum())
-    for a_, dx in outs.items():
+    ref = g.backward(Gr, sel, algo=_lib.MAXK_BWD_STAGED)
+    outs = {}
+    for a_ in algos:
+        dx = g.backward(Gr, sel, algo=a_)
         rhs = float((data.double() * dx.double()).sum())
         assert abs(lhs - rhs) / abs(lhs) <= 1e-6, (a_, lhs, rhs)
-        assert _rel(dx, outs[_lib.MAXK_BWD_STAGED]) <= TOL, a_
+        assert _rel(dx, ref) <= TOL, a_
+        if a_ in (_lib.MAXK_BWD_LOCAL, _lib.MAXK_BWD_TILE):
+            outs[a_] = dx
+        else:
+            del dx
     if _lib.MAXK_BWD_LOCAL in outs:
         dx2 = g.backward(2 * Gr, sel, algo=_lib.MAXK_BWD_LOCAL)
         assert torch.equal(dx2, 2 * outs[_lib.MAXK_BWD_LOCAL])
+        del dx2
+    if _lib.MAXK_BWD_TILE in outs:
+        t = outs[_lib.MAXK_BWD_TILE]
+        assert torch.equal(t, g.backward(Gr, sel, algo=_lib.MAXK_BWD_TILE))   # deterministic
+        if _lib.MAXK_BWD_LOCAL in outs and tile_plan["splits"] == 1 and k == 64:
+            # k = 64, one source range: both add each destination's edges in
+            # source-row order with one fp32 FMA each (tools/exp_tile_local_bits.py)
+            assert torch.equal(t, outs[_lib.MAXK_BWD_LOCAL])
+    auto = g.backward(Gr, sel)
+    assert g.last_bwd_algo in {"staged", "atomic", "local", "tile"}
+    assert _rel(auto, ref) <= TOL
+
+
+def test_full_size_tile_plan_shape_reddit(dev):
+    """The Reddit k=32 plan the bench runs: 128 groups x 2 source ranges = 256
+    workgroups (tile_combine_kernel in use), and its dx through the C ABI equals
+    the split-free LOCAL order only up to fp32 rounding -- checked above; here
+    the structure the VERDICT asked to exercise is asserted explicitly."""
+    V, E = CONFIGS["reddit"]
+    indptr, indices = synthetic_csr_gpu(V, E, device=dev)
+    g = S.MaxKGraph(indptr, indices)
+    plan = g.tile_plan(32)
+    assert plan is not None
+    cus = torch.cuda.get_device_properties(dev).multi_processor_count
+    assert plan["num_groups"] * plan["splits"] <= cus and plan["splits"] >= 2
+    assert int(plan["num_chunks"].max()) > 1000
+
+
+def test_full_size_proteins_multi_relation(dev):
+    """BASELINE config 5 at full size on one GPU (ogbn-proteins shape, R = 8,
+    k = 32, h = 256): the fused forward equals 8 single-relation forwards
+    within 1e-4; the relation-interleaved backward satisfies the multi-relation
+    adjoint identity sum_q <A_q.X^, G_q> = <X^_s, dXs> and agrees with the
+    composed backward."""
+    V, E = CONFIGS["proteins"]
+    h, k, R = 256, 32, 8
+    indptr, indices = synthetic_csr_gpu(V, E, device=dev)
+    gen = torch.Generator(device=dev)
+    gen.manual_seed(5)
+    vals = torch.rand((indices.numel(), R), generator=gen, device=dev)
+    X = torch.rand((V, h), generator=gen, device=dev)
+    data, sel = S.topk_cbsr(X, k)
+    g = S.MaxKGraph(indptr, indices, vals[:, 0].contiguous())
+    y = g.forward_multi(data, sel, vals, h)
+    for q in range(R):
+        yq = g.forward(data, sel, h, values=vals[:, q].contiguous())
+        assert _rel(y[q], yq) <= TOL, q
+        del yq
+    Gr = torch.rand((R, V, h), generator=gen, device=dev)
+    lhs = float((y.double() * Gr.double()).sum())
+    del y
+    dx = g.backward_multi(Gr, sel, vals, algo=_lib.MAXK_BWD_LOCAL)
+    assert g.last_bwd_algo == "local_rel8"
+    rhs = float((data.double() * dx.double()).sum())
+    assert abs(lhs - rhs) / abs(lhs) <= 1e-6
+    comp = g.backward_multi(Gr, sel, vals, algo=_lib.MAXK_BWD_STAGED)
+    assert _rel(dx, comp) <= TOL
 
 
 def test_flickr_config1_full(dev, oracle):

@@ -617,11 +617,12 @@ def test_out_of_range_selectors(dev, oracle, g_small, algo):
 
 
 @pytest.mark.parametrize("k,algo", [(32, _lib.MAXK_BWD_LOCAL), (8, _lib.MAXK_BWD_LOCAL),
-                                    (8, _lib.MAXK_BWD_ATOMIC)])
-def test_hipgraph_full_step(dev, oracle, g_small, monkeypatch, k, algo):
+                                    (8, _lib.MAXK_BWD_ATOMIC), (32, _lib.MAXK_BWD_TILE),
+                                    (64, _lib.MAXK_BWD_TILE), (32, _lib.MAXK_BWD_AUTO)])
+def test_hipgraph_full_step(dev, oracle, g_small, monkeypatch, k, algo):  # noqa: C901
     """A whole step captured once and replayed on new inputs: HIP top-k,
-    forward (packed records at k=8), LOCAL / ATOMIC backward over several
-    source bands, dense gradient scatter.  Plans are built by a warm-up call
+    forward (packed records at k=8), LOCAL / ATOMIC / TILE / AUTO backward
+    (LOCAL over several source bands), dense gradient scatter.  Plans are built by a warm-up call
     before capture; the calls themselves allocate nothing and never sync."""
     from spgemm_new_amd import ops
     monkeypatch.setattr(ops, "LOCAL_BAND_BYTES", 200 * 1024)   # several bands
@@ -898,3 +899,30 @@ def test_forward_accumulate(dev, oracle, g_small, k, h):
     g.forward(T(data, dev), T(sel, dev), h, out=out, accumulate=True)
     ref = oracle.np_forward(indptr, indices, values, data, sel, h) + base
     assert oracle.parity_error(out.cpu().numpy(), ref) <= TOL
+
+
+def test_auto_under_capture_keeps_tile(dev, g_small):
+    """AUTO reached for the first time inside a hipGraph capture (nothing can
+    be timed there): with the TILE plan built beforehand it runs TILE, not the
+    STAGED fallback, and the replay matches the eager TILE result."""
+    indptr, indices, values = g_small
+    v, h, k = len(indptr) - 1, 256, 32
+    g = S.MaxKGraph(T(indptr, dev), T(indices, dev), T(values, dev))
+    assert g.tile_plan(k) is not None
+    gr = torch.rand((v, h), device=dev)
+    x = torch.rand((v, h), device=dev)
+    _, s = S.topk_cbsr(x, k)
+    dx = torch.empty((v, k), device=dev)
+    ref = g.backward(gr, s, algo=_lib.MAXK_BWD_TILE)
+    torch.cuda.synchronize()
+    graph = torch.cuda.CUDAGraph()
+    stream = torch.cuda.Stream()
+    stream.wait_stream(torch.cuda.current_stream())
+    with torch.cuda.stream(stream):
+        with torch.cuda.graph(graph, stream=stream):
+            g.backward(gr, s, out=dx)
+    torch.cuda.current_stream().wait_stream(stream)
+    assert g.last_bwd_algo == "tile"
+    graph.replay()
+    torch.cuda.synchronize()
+    assert torch.equal(dx, ref)

@@ -20,7 +20,8 @@ def test_harness_built():
 
 @pytest.mark.gpu
 def test_harness_runs_and_validates(tmp_path):
-    """main.cu's output lines for k = 16 / 32 / 64, every backward algorithm,
+    """main.cu's output lines for k = 16 / 32 / 64, every backward algorithm (TILE
+    at k = 32 / 64, its plan built by maxk_tile_plan_build),
     and the --check validations (forward vs dense SpMM, backward algorithms
     against each other) on two small graphs read from raw int32 files."""
     for name, seed in (("g1", 3), ("g2", 4)):
@@ -38,13 +39,15 @@ def test_harness_runs_and_validates(tmp_path):
     for g in ("g1", "g2"):
         assert (g, 16, "dense_spmm") in times
         for k in (16, 32, 64):
-            for kern in ("maxk", "maxk_backward", "maxk_backward_atomic", "maxk_backward_staged",
-                         "maxk_backward_local"):
+            algos = ["maxk_backward_atomic", "maxk_backward_staged", "maxk_backward_local"]
+            if k in (32, 64):
+                algos.append("maxk_backward_tile")   # the TILE plan through the C ABI
+            for kern in ["maxk", "maxk_backward"] + algos:
                 assert times[(g, k, kern)] > 0, (g, k, kern)
-            assert times[(g, k, "maxk_backward")] == min(
-                times[(g, k, a)] for a in ("maxk_backward_atomic", "maxk_backward_staged",
-                                           "maxk_backward_local"))
+            assert times[(g, k, "maxk_backward")] == min(times[(g, k, a)] for a in algos)
     checks = [ln for ln in lines if "validation" in ln]
-    assert len(checks) == 2 * 3 * 3, checks          # per graph and k: fwd + staged + local
+    # per graph: k=16 fwd + staged + local; k=32 and k=64 also tile
+    assert len(checks) == 2 * (3 + 4 + 4), checks
     assert all("validation pass!" in ln for ln in checks), checks
+    assert sum("backward tile vs atomic" in ln for ln in checks) == 4
     assert np.isfinite(list(times.values())).all()

@@ -1,10 +1,13 @@
-"""TILE backward: the plan format (CPU, replayed by spgemm_new_amd.tile.emulate
-against the float64 oracle) and the kernel (GPU, against the oracle and the
-other backward algorithms)."""
+"""TILE backward: the plan format (CPU: the torch reference builder's plan,
+tests/tile_ref.py, replayed by spgemm_new_amd.tile.emulate against the float64
+oracle), the device plan builder (GPU: maxk_tile_plan_build bit-identical to
+the reference builder) and the kernel (GPU, against the oracle and the other
+backward algorithms)."""
 import numpy as np
 import pytest
 import torch
 
+import tile_ref
 from spgemm_new_amd import tile
 
 TOL = 1e-4  # fp32 summation order vs the float64 oracle (north_star tolerance)
@@ -41,8 +44,8 @@ def _inputs(V, C, seed, k=32, h=256):
 def test_plan_emulated_matches_oracle(oracle, V, C, deg, shape, hubs, k):
     indptr, idx, vals = _graph(V, C, deg, seed=V + C, hub_rows=hubs)
     grad, sel = _inputs(V, C, seed=V, k=k)
-    plan = tile.build(torch.from_numpy(indptr), torch.from_numpy(idx), torch.from_numpy(vals),
-                      V, C, cus=16, shape=shape, k=k)
+    plan = tile_ref.build(torch.from_numpy(indptr), torch.from_numpy(idx), torch.from_numpy(vals),
+                          V, C, cus=16, shape=shape, k=k)
     assert plan is not None
     got = tile.emulate(plan, torch.from_numpy(grad), torch.from_numpy(sel)).numpy()
     ref = oracle.np_backward(indptr, idx, vals, grad, sel)
@@ -52,10 +55,10 @@ def test_plan_emulated_matches_oracle(oracle, V, C, deg, shape, hubs, k):
 def test_plan_invariants():
     V, C = 400, 1000
     indptr, idx, vals = _graph(V, C, 15, seed=3)
-    plan = tile.build(torch.from_numpy(indptr), torch.from_numpy(idx), torch.from_numpy(vals),
-                      V, C, cus=8)
+    plan = tile_ref.build(torch.from_numpy(indptr), torch.from_numpy(idx), torch.from_numpy(vals),
+                          V, C, cus=8)
     G, GS, NS = plan["num_groups"], plan["group_size"], plan["splits"]
-    assert G * GS >= C and GS <= tile.MAX_GROUP
+    assert G * GS >= C and GS <= tile.max_group(32)
     hdrs, recs = plan["headers"], plan["records"]
     hs, rs = plan["header_start"].tolist(), plan["record_start"].tolist()
     nch = plan["num_chunks"].tolist()
@@ -77,6 +80,95 @@ def test_plan_invariants():
                     assert bool(((rowf // tile.BUF_ROWS) == (c - 2) % 3).all())
                     ro += n0 + n1
     assert n_real == int((torch.from_numpy(vals) != 0).sum())
+
+
+@pytest.mark.parametrize("k", [32, 64])
+@pytest.mark.parametrize("C", [1, 63, 1000, 2048, 2049, 4096, 100_000, 232_965, 2_449_029])
+@pytest.mark.parametrize("cus", [8, 256])
+def test_shape_library_matches_reference(C, cus, k):
+    """maxk_tile_plan_shape (C ABI, host code: no GPU needed) == the reference rule."""
+    assert tile.choose_shape(C, cus, k) == tile_ref.choose_shape(C, cus, k)
+
+
+_KEYS = ("headers", "header_start", "records", "record_start", "num_chunks")
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("k", [32, 64])
+@pytest.mark.parametrize("V,C,deg,shape,hubs", [
+    (300, 300, 12, None, 0), (800, 800, 6, None, 12), (500, 2600, 9, None, 0),
+    (700, 900, 20, (3, 300, 2), 0), (200, 64, 4, (1, 64, 1), 0), (3000, 3000, 40, None, 0),
+    (4000, 1500, 30, (2, 750, 5), 0), (1, 5, 3, None, 0),
+])
+def test_device_plan_matches_reference_builder(dev, V, C, deg, shape, hubs, k):
+    """maxk_tile_plan_build (device) == the torch reference builder, bit for
+    bit, and edge_record points every CSR edge at its own record."""
+    indptr, idx, vals = _graph(V, C, deg, seed=V + C, hub_rows=hubs)
+    if idx.size == 0:
+        pytest.skip("empty graph")
+    args = [torch.from_numpy(a).to(dev) for a in (indptr, idx, vals)]
+    got = tile.build(*args, V, C, cus=16, shape=shape, k=k)
+    ref = tile_ref.build(*args, V, C, cus=16, shape=shape, k=k)
+    assert (got is None) == (ref is None)
+    if got is None:
+        return
+    for key in ("num_groups", "group_size", "splits"):
+        assert got[key] == ref[key], key
+    for key in _KEYS:
+        a, b = got[key].cpu(), ref[key].cpu().to(got[key].dtype)
+        assert a.shape == b.shape and torch.equal(a, b), key
+    rec = got["records"].cpu()
+    er = got["edge_record"].cpu().long()
+    assert torch.equal(rec[er, 1], args[2].cpu().view(torch.int32))
+    # set_values rewrites exactly the value words
+    new = torch.rand(idx.size, device=dev)
+    tile.set_values(got, new)
+    rec2 = got["records"].cpu()
+    assert torch.equal(rec2[er, 1], new.cpu().view(torch.int32))
+    assert torch.equal(rec2[:, 0], rec[:, 0])
+
+
+@pytest.mark.gpu
+def test_tile_values_changed_in_place(dev, oracle):
+    """The graph's values mutated in place after the TILE plan was built: TILE
+    must see the new values (same as STAGED on the new values)."""
+    import spgemm_new_amd as S
+    from spgemm_new_amd import _lib
+    V = 3000
+    indptr, idx, vals = _graph(V, V, 40, seed=21)
+    grad, sel = _inputs(V, V, seed=21)
+    g = S.MaxKGraph(torch.from_numpy(indptr).to(dev), torch.from_numpy(idx).to(dev),
+                    torch.from_numpy(vals).to(dev))
+    G, sl = torch.from_numpy(grad).to(dev), torch.from_numpy(sel).to(dev)
+    g.backward(G, sl, algo=_lib.MAXK_BWD_TILE)
+    g.values.mul_(-2.0).add_(0.25)          # an optimizer step on the edge weights
+    got = g.backward(G, sl, algo=_lib.MAXK_BWD_TILE)
+    staged = g.backward(G, sl, algo=_lib.MAXK_BWD_STAGED)
+    ref = oracle.np_backward(indptr, idx, g.values.cpu().numpy(), grad, sel)
+    assert oracle.parity_error(got.cpu().numpy(), ref) < TOL
+    assert (got - staged).abs().max().item() <= 1e-4 * max(1.0, staged.abs().max().item())
+
+
+@pytest.mark.gpu
+def test_auto_with_foreign_values_after_tile(dev):
+    """AUTO chose TILE for the graph's own values; a later AUTO call with other
+    values must not get TILE back (its records hold the graph's values)."""
+    import spgemm_new_amd as S
+    V = 3000
+    indptr, idx, vals = _graph(V, V, 40, seed=5)
+    grad, sel = _inputs(V, V, seed=5)
+    g = S.MaxKGraph(torch.from_numpy(indptr).to(dev), torch.from_numpy(idx).to(dev),
+                    torch.from_numpy(vals).to(dev))
+    G, sl = torch.from_numpy(grad).to(dev), torch.from_numpy(sel).to(dev)
+    g._bwd_choice[(32, 256, True)] = S._lib.MAXK_BWD_TILE   # as if AUTO had measured TILE fastest
+    own = g.backward(G, sl)
+    assert g.last_bwd_algo == "tile"
+    w = torch.rand(idx.size, device=dev)
+    other = g.backward(G, sl, values=w)
+    assert g.last_bwd_algo != "tile"
+    ref = g.backward(G, sl, values=w, algo=S._lib.MAXK_BWD_STAGED)
+    assert (other - ref).abs().max().item() <= 1e-4 * max(1.0, ref.abs().max().item())
+    assert torch.equal(own, g.backward(G, sl))
 
 
 @pytest.mark.gpu
@@ -104,6 +196,11 @@ def test_tile_backward_gpu_matches_oracle(dev, oracle, V, C, deg, k):
     assert torch.equal(got, again)
     loc = g.backward(G, sl, algo=_lib.MAXK_BWD_LOCAL)
     assert (got - loc).abs().max().item() <= 1e-4 * max(1.0, loc.abs().max().item())
+    if g.tile_plan(k)["splits"] == 1:
+        # one source range: TILE adds each destination's edges in source-row
+        # order, one FMA per edge, as LOCAL does -> bit-identical.  With
+        # splits > 1 the ranges' partial sums are added at the end instead.
+        assert torch.equal(got, loc)
 
 
 @pytest.mark.gpu
