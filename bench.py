@@ -149,6 +149,28 @@ def cpu_baseline(indptr, indices, values, x_masked, grad, mask, k, h, budget_s):
     }
 
 
+TRAIN_STEP_DOC = ("one MaxK-SAGE layer training step (utils/models.py:230, 242-253): top-k -> "
+                  "SpGEMM -> fc_self(x) + fc_neigh(agg) (Linear h x h, hipBLASLt) -> loss <out, G> "
+                  "-> backward (Linear, SSpMM, dense scatter) -> SGD step")
+
+
+def train_step_fn(h, k, graph, X, G, values=None, num_rel=1):
+    """One training step of a MaxK-SAGE layer (spgemm_new_amd.layers) on the
+    whole graph: the aggregation op in its model context."""
+    from spgemm_new_amd.layers import MaxKRelSAGELayer, MaxKSAGELayer
+    torch.manual_seed(0)
+    layer = (MaxKSAGELayer(h, k) if num_rel == 1 else MaxKRelSAGELayer(h, k, num_rel)).to(X.device)
+    opt = torch.optim.SGD(layer.parameters(), lr=1e-3)
+    x = X.clone().requires_grad_(True)
+
+    def step():
+        opt.zero_grad(set_to_none=True)
+        out = layer(graph, x) if num_rel == 1 else layer(graph, x, values)
+        out.backward(G)
+        opt.step()
+    return step
+
+
 def workload_key(args, bwd_algo):
     return f"{args.graph}_h{args.h}_k{args.k}_{bwd_algo}"
 
@@ -221,7 +243,7 @@ def bench_multi_partitioned(args, indptr, indices, vals, data, sel, V, E, h, k, 
     ranks); the backward is reported beside it."""
     from spgemm_new_amd.distributed import PartitionedMaxK
     kw = {"panel_cost": args.panel_cost} if args.panel_cost else {}
-    model = PartitionedMaxK(indptr, indices, vals, rank, world, dev, **kw)
+    model = PartitionedMaxK(indptr, indices, vals, rank, world, dev, local_block=True, **kw)
     r0, r1 = model.bounds[rank], model.bounds[rank + 1]
     data_l, sel_l = model.local_rows(data), model.local_rows(sel)
     G_l = torch.rand((R, r1 - r0, h), generator=gen, device=dev)
@@ -281,15 +303,20 @@ def _cpu_model():
     return "unknown"
 
 
-def bench_multi(args, S, indptr, indices, data, sel, V, E, h, k, dev, world, rank=0, dist=None):
+def bench_multi(args, S, indptr, indices, data, sel, V, E, h, k, dev, world, rank=0, dist=None,
+                edges=None):
     """BASELINE config 5 (ogbn-proteins, R edge-feature relations): the fused
     multi-relation forward Y[q] = A_q . X^ (one CSR + CBSR gather shared by R
     relations) timed against R single-relation forwards.  Bytes per fused call
     (SURVEY.md §8d): E*(4 + 4R + 5k) + R*4hV; unfused: R*(8E + 5kE + 4hV)."""
+    from spgemm_new_amd.graphs import synthetic_values
     R = args.relations
     gen = torch.Generator(device=dev)
     gen.manual_seed(args.seed + 7)
-    vals = torch.rand((E, R), generator=gen, device=dev)
+    e0, e1 = edges or (0, E)
+    # relation q's edge values: hashes of (seed + 7 + q, edge id) -> this rank's edges only
+    vals = torch.stack([synthetic_values(args.seed + 7 + q, e0, e1, device=dev)
+                        for q in range(R)], dim=1).contiguous()
     b_fused = E * (4 + 4 * R + 5 * k) + R * 4 * h * V
     if dist is not None:
         return bench_multi_partitioned(args, indptr, indices, vals, data, sel, V, E, h, k, R, dev,
@@ -328,6 +355,10 @@ def bench_multi(args, S, indptr, indices, data, sel, V, E, h, k, dev, world, ran
     t_b = timed(backward)
     b_unf = R * (8 * E + 5 * k * E + 4 * h * V)
     val = b_fused / (t_f / 1e3) / 1e9
+    X = torch.rand((V, h), generator=gen, device=dev)
+    step = train_step_fn(h, k, (indptr, indices), X, G.sum(0), values=vals, num_rel=R)
+    t_train = timed(step)
+    del X
     result = {
         "metric": f"fused {R}-relation SpGEMM forward GB/s, {args.graph} h={h} k={k}",
         "value": round(val, 2), "unit": "GB/s", "n_gpus": world, "steps": args.steps,
@@ -337,6 +368,11 @@ def bench_multi(args, S, indptr, indices, data, sel, V, E, h, k, dev, world, ran
         "config": {"workload": f"{args.graph} fused multi-relation forward", "graph": args.graph,
                    "num_nodes": V, "num_edges": E, "hidden": h, "k": k, "relations": R,
                    "parallelism": "single"},
+        "train_step_ms": round(t_train, 4),
+        "train_step": (f"one {R}-relation MaxK-SAGE layer training step (spgemm_new_amd.layers."
+                       "MaxKRelSAGELayer): top-k -> fused R-relation SpGEMM -> fc_self(x) + "
+                       "sum_q agg_q W_q (bmm, hipBLASLt) -> loss <out, G> -> backward (bmm, "
+                       "relation-interleaved SSpMM, dense scatter) -> SGD step"),
         "roofline": {"bound": "hbm", "achieved": round(val, 1), "peak": HBM_PEAK_GBS,
                      "unit": "GB/s", "frac": round(val / HBM_PEAK_GBS, 4), "traffic": None,
                      "kernel": "spgemm_forward_multi", "algorithmic_bytes_per_launch": b_fused},
@@ -351,7 +387,8 @@ def main():
     args = parse()
     import spgemm_new_amd as S
     from spgemm_new_amd import _lib
-    from spgemm_new_amd.graphs import CONFIGS, synthetic_csr_gpu
+    from spgemm_new_amd.graphs import (CONFIGS, synthetic_columns, synthetic_indptr,
+                                       synthetic_values)
     from spgemm_new_amd.ops import topk_cbsr
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -383,15 +420,27 @@ def main():
     V, E = CONFIGS[args.graph]
     h, k = args.h, args.k
     t0 = time.time()
-    indptr, indices = synthetic_csr_gpu(V, E, seed=args.seed, device=dev,
-                                        self_loops=(args.graph == "flickr"))
+    # the synthetic graph: every rank computes the (cheap) global indptr, then
+    # generates only the edges of its own row block (columns and values are
+    # hashes of the edge id, so the blocks are exactly rows of the N=1 graph)
+    indptr = synthetic_indptr(V, E, seed=args.seed, device=dev)
+    rows = None
+    if partitioned:
+        from spgemm_new_amd.distributed import row_partition
+        b = row_partition(indptr, world)
+        rows = (b[rank], b[rank + 1])
+    r0, r1 = rows or (0, V)
+    e0, e1 = int(indptr[r0]), int(indptr[r1])
+    indices = synthetic_columns(indptr, seed=args.seed, rows=rows,
+                                self_loops=(args.graph == "flickr"))
+    values = synthetic_values(args.seed, e0, e1, device=dev)   # main.cu:83-84 U(0,1)
     gen = torch.Generator(device=dev)
     gen.manual_seed(args.seed + 1)
-    values = torch.rand(E, generator=gen, device=dev)          # main.cu:83-84 U(0,1)
     X = torch.rand((V, h), generator=gen, device=dev)
     G = torch.rand((V, h), generator=gen, device=dev)
     data, sel = topk_cbsr(X, k, order=args.cbsr_order)  # HIP CBSR producer
-    log(f"[bench] graph {args.graph} V={V} E={E} built in {time.time() - t0:.1f}s")
+    log(f"[bench] graph {args.graph} V={V} E={E}: rows [{r0}, {r1}) ({e1 - e0} edges) built "
+        f"in {time.time() - t0:.1f}s")
 
     algo = {"auto": _lib.MAXK_BWD_AUTO, "atomic": _lib.MAXK_BWD_ATOMIC,
             "staged": _lib.MAXK_BWD_STAGED, "local": _lib.MAXK_BWD_LOCAL,
@@ -404,11 +453,11 @@ def main():
 
     if args.relations > 1:
         return bench_multi(args, S, indptr, indices, data, sel, V, E, h, k, dev, world, rank,
-                           dist if partitioned else None)
+                           dist if partitioned else None, (e0, e1))
 
     if partitioned:
         from spgemm_new_amd.distributed import PartitionedMaxK
-        model = PartitionedMaxK(indptr, indices, values, rank, world, dev, **kw)
+        model = PartitionedMaxK(indptr, indices, values, rank, world, dev, local_block=True, **kw)
         data_l, sel_l = model.local_rows(data), model.local_rows(sel)
         G_l = model.local_rows(G)
 
@@ -583,6 +632,9 @@ def main():
             SpGEMMFunction.apply(xg, (indptr, indices, values), k).backward(G)
         result["autograd_step_ms"] = round(ev_ms(autograd_step), 4)
         del xg
+        result["train_step_ms"] = round(ev_ms(train_step_fn(h, k, (indptr, indices, values), X, G)),
+                                        4)
+        result["train_step"] = TRAIN_STEP_DOC
         result["scatter_ms"] = round(ev_ms(lambda: cbsr_scatter(dx_tmp, sel, h)), 4)
         if not args.no_vendor and rank == 0:
             result["vendor_baseline"] = vendor_baseline(g, indptr, indices, values, X, sel, y, fms,

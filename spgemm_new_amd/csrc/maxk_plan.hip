@@ -216,7 +216,8 @@ size_t scan_temp_bytes(int64_t n)
 constexpr int kTileWaves = 16;
 constexpr int kTileRows = 47;
 constexpr int kTileBufRows = 48;
-constexpr int kTileRecPad = 512;   // records of over-read padding after the stream
+constexpr int kTileRecPad = 512;   // records of over-read padding after the stream (the
+                                   // kernel's prefetch window is static_asserted against it)
 constexpr int kTileHdrPad = 8;     // header entries of padding
 
 __device__ __forceinline__ int tile_split(int r, int V, int NS)

@@ -1776,8 +1776,6 @@ constexpr int kTileWaves = 16;
 constexpr int kTileRows = 47;  // gradient rows per chunk; row 47 of a buffer is zero
 constexpr int kTileBufRows = 48;
 static_assert(kTileRows + 1 == kTileBufRows, "chunk rows + zero row = buffer rows");
-constexpr int kTileHdr = 3;
-constexpr int kTilePro = 4;
 
 typedef float tile_acc_t __attribute__((ext_vector_type(32)));
 typedef unsigned tile_sel_t __attribute__((ext_vector_type(16)));
@@ -2230,6 +2228,9 @@ __global__ __launch_bounds__(kTileWaves * kWave) void bwd_tile_kernel(
 #ifndef TILE_PF_AHEAD
 #define TILE_PF_AHEAD 128  // dwords: the window starts 512 B past the chunk's records
 #endif
+    // the window must stay inside the record stream's padding: 512 records =
+    // 1024 dwords after the last wave's stream (kTileRecPad in maxk_plan.hip)
+    static_assert(TILE_PF_AHEAD + 4 * kWave <= 2 * 512, "TILE prefetch past the record padding");
 #ifndef TILE_NO_PREFETCH
     auto prefetch = [&]() { tile_prefetch(rb + (ro >> 2) + TILE_PF_AHEAD + lane * 4, pf); };
 #define TILE_VMCNT "7"

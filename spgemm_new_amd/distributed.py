@@ -71,12 +71,16 @@ def row_partition(indptr: torch.Tensor, world: int, row_cost: int = 16) -> list[
 class HaloPlan:
     """Static exchange plan of one rank (built once per graph)."""
 
-    def __init__(self, indptr, indices, bounds, rank, world, device):
+    def __init__(self, indptr, indices, bounds, rank, world, device, local_block: bool = False):
         self.rank, self.world, self.bounds = rank, world, bounds
         r0, r1 = bounds[rank], bounds[rank + 1]
         e0, e1 = int(indptr[r0]), int(indptr[r1])
         self.num_own = r1 - r0
-        cols = indices[e0:e1].to(device).long()
+        # local_block: `indices` holds only this rank's edges [e0, e1)
+        cols = (indices if local_block else indices[e0:e1]).to(device).long()
+        if cols.numel() != e1 - e0:
+            raise RuntimeError(f"rank {rank}: expected {e1 - e0} edges of rows [{r0}, {r1}), "
+                               f"got {cols.numel()}")
         own = (cols >= r0) & (cols < r1)
         halo = torch.unique(cols[~own])                        # sorted global ids
         self.num_halo = halo.numel()
@@ -137,16 +141,23 @@ class PartitionedMaxK:
 
     def __init__(self, indptr, indices, values, rank: int, world: int, device,
                  engine=None, row_cost: int = 16, overlap: bool = True, records: bool = True,
-                 **engine_kw):
+                 local_block: bool = False, overlap_backward: bool | None = None, **engine_kw):
+        """indptr: the GLOBAL row pointer (V + 1 entries, cheap); indices /
+        values: the global arrays, or with ``local_block=True`` only this rank's
+        edges (rows [bounds[rank], bounds[rank + 1]) of ``row_partition(indptr,
+        world, row_cost)``), so no rank materialises the whole graph."""
         self.rank, self.world, self.device = rank, world, torch.device(device)
         self.bounds = row_partition(indptr, world, row_cost)
-        self.plan = HaloPlan(indptr, indices, self.bounds, rank, world, self.device)
+        self.plan = HaloPlan(indptr, indices, self.bounds, rank, world, self.device,
+                             local_block=local_block)
         p = self.plan
         e0, e1 = p.edge_range
         if values.dim() not in (1, 2):
             raise RuntimeError("values must be fp32[E] or fp32[E, R]")
         self.num_rel = 1 if values.dim() == 1 else values.shape[1]
-        lv_all = values[e0:e1].to(self.device).contiguous()
+        lv_all = (values if local_block else values[e0:e1]).to(self.device).contiguous()
+        if lv_all.shape[0] != e1 - e0:
+            raise RuntimeError("values must match indices")
         self.values_local = lv_all                       # [E_local] or [E_local, R]
         lv = lv_all if self.num_rel == 1 else lv_all[:, 0].contiguous()
         make = engine or _default_engine
@@ -182,6 +193,11 @@ class PartitionedMaxK:
             self.local_halo = part(~is_own, p.num_own, p.num_halo)
         self.local = make(p.local_indptr, p.local_indices, lv, p.num_own + p.num_halo,
                           **engine_kw)
+        # backward overlap: the halo columns' dXs first, their reverse exchange in
+        # flight while the own columns' dXs are computed (disjoint column sets, so
+        # nothing is added twice); each part sweeps the rank's gradient rows
+        self.overlap_backward = (self.overlap and world > 1) if overlap_backward is None \
+            else bool(overlap_backward and self.overlap)
         self._bufs = {}
         self._fwd_sel = None     # sel_own of the last forward
         self._halo_part = None   # its halo selectors: [num_halo, k] (view of records or rows)
@@ -228,12 +244,25 @@ class PartitionedMaxK:
 
     # --------------------------------------------------------------- compute
     def gather_halo_cbsr(self, data_own: torch.Tensor, sel_own: torch.Tensor):
-        """All-to-all-v of packed CBSR rows -> (data, sel) for own + halo columns."""
+        """All-to-all-v of packed CBSR rows -> (data, sel) for own + halo columns,
+        written straight into the block's buffers (own rows copied while the
+        exchange is in flight, halo records unpacked into the tail)."""
+        p = self.plan
         k = data_own.shape[1]
-        recv = self._exchange(self._pack(data_own, sel_own), 5 * k, torch.uint8)
-        h_data, h_sel = self._unpack(recv, k)
-        self._fwd_sel, self._halo_part = sel_own, h_sel
-        return torch.cat([data_own, h_data]).contiguous(), torch.cat([sel_own, h_sel]).contiguous()
+        n = p.num_own + p.num_halo
+        recv = self._buf(("recv", k), (p.num_halo, 5 * k), torch.uint8)
+        work = a2a(recv, self._pack(data_own, sel_own), p.recv_counts, p.send_counts,
+                   async_op=True)
+        data = self._buf(("data_all", k), (n, k), torch.float32)
+        sel = self._buf(("sel_all_fwd", k), (n, k), torch.uint8)
+        data[: p.num_own] = data_own
+        sel[: p.num_own] = sel_own
+        work.wait()
+        hd = recv[:, : 4 * k]
+        data[p.num_own:] = (hd if (5 * k) % 4 == 0 else hd.contiguous()).view(torch.float32)
+        sel[p.num_own:] = recv[:, 4 * k:]
+        self._fwd_sel, self._halo_part = sel_own, sel[p.num_own:]
+        return data, sel
 
     def forward(self, data_own: torch.Tensor, sel_own: torch.Tensor, dim_origin: int = 256):
         p = self.plan
@@ -304,14 +333,19 @@ class PartitionedMaxK:
         p = self.plan
         k = dxs.shape[1]
         back = self._exchange(dxs[p.num_own:], k, torch.float32, reverse=True)
-        own = dxs[: p.num_own]
+        return self._add_returns(back, dxs[: p.num_own])
+
+    def _add_returns(self, back: torch.Tensor, own: torch.Tensor) -> torch.Tensor:
+        """own[node] += the partial sums the peers returned for it (fixed order)."""
+        p = self.plan
+        k = own.shape[1]
         order, seg_off, nodes = self._ret
         if own.is_cuda and nodes.numel() > 0:
             from . import _lib
             _lib.check(_lib.load().maxk_segment_rows_add(
                 back.data_ptr(), k, order.data_ptr(), seg_off.data_ptr(), nodes.data_ptr(),
                 nodes.numel(), own.data_ptr(), _lib.stream_ptr(own.device)), "maxk_segment_rows_add")
-        else:
+        elif nodes.numel() > 0:
             own.index_add_(0, p.send_local, back)
         return own
 
@@ -319,8 +353,20 @@ class PartitionedMaxK:
                  halo_sel: torch.Tensor | None = None):
         """dXs of the own nodes.  The block's selectors: sel_own + halo_sel when
         given (last_halo_selectors() of that forward), else the last forward's
-        when sel_own is its tensor (or None), else exchanged again."""
-        return self._return_halo(self.local.backward(grad_own, self._block_sel(sel_own, halo_sel)))
+        when sel_own is its tensor (or None), else exchanged again.  With
+        overlap_backward the halo columns go first and their partial sums
+        travel while the own columns are computed."""
+        sel = self._block_sel(sel_own, halo_sel)
+        if not self.overlap_backward:
+            return self._return_halo(self.local.backward(grad_own, sel))
+        p = self.plan
+        k = sel.shape[1]
+        dh = self.local_halo.backward(grad_own, sel[p.num_own:])
+        back = self._buf(("back", k), (sum(p.send_counts), k), torch.float32)
+        work = a2a(back, dh, p.send_counts, p.recv_counts, async_op=True)
+        own = self.local_own.backward(grad_own, sel[: p.num_own])   # overlaps the exchange
+        work.wait()
+        return self._add_returns(back, own)
 
     # ------------------------------------------------- multi-relation (config 5)
     def forward_multi(self, data_own: torch.Tensor, sel_own: torch.Tensor,
@@ -332,9 +378,12 @@ class PartitionedMaxK:
         data, sel = self.gather_halo_cbsr(data_own, sel_own)
         return self.local.forward_multi(data, sel, self.values_local, dim_origin)
 
-    def backward_multi(self, grad_own: torch.Tensor, sel_own: torch.Tensor | None = None):
-        """dXs = sum_q (A_q^T G_q) at sel for own nodes; grad_own fp32[R, own rows, h]."""
-        dxs = self.local.backward_multi(grad_own, self._block_sel(sel_own), self.values_local)
+    def backward_multi(self, grad_own: torch.Tensor, sel_own: torch.Tensor | None = None,
+                       halo_sel: torch.Tensor | None = None):
+        """dXs = sum_q (A_q^T G_q) at sel for own nodes; grad_own fp32[R, own rows, h]
+        (selectors as in backward())."""
+        dxs = self.local.backward_multi(grad_own, self._block_sel(sel_own, halo_sel),
+                                        self.values_local)
         return self._return_halo(dxs)
 
     def algorithmic_bytes(self, k: int, h: int) -> int:

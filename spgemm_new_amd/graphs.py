@@ -5,7 +5,9 @@
   kernels/main.cu:57-58).
 * ``synthetic_csr_gpu`` builds Reddit- / ogbn-products-shaped graphs directly in
   HBM (the datasets are not available offline): power-law out-degrees with the
-  requested mean, columns uniform without duplicates, sorted per row.
+  requested mean, columns uniform without duplicates, sorted per row.  Columns
+  (``synthetic_columns``) and edge values (``synthetic_values``) are hashes of
+  (seed, edge id), so a rank of the row partition generates only its rows.
 * ``small_csr`` builds the small CPU graphs used by the parity tests, with a
   degree mix that exercises degree-0 rows, rows split across panels and the
   reference's 64-nnz chunk boundaries (63/64/65, >200).
@@ -73,37 +75,91 @@ def powerlaw_degrees(num_rows: int, num_edges: int, gen: torch.Generator, device
     return deg
 
 
-def synthetic_csr_gpu(num_rows: int, num_edges: int, seed: int = 123, device="cuda",
-                      alpha: float = 2.2, self_loops: bool = False):
-    """(indptr int32[V+1], indices int32[E]) on `device`; columns uniform in
-    [0, V), no duplicates within a row, ascending within a row."""
+_M64 = (1 << 64) - 1
+
+
+def _i64(c: int) -> int:
+    """A 64-bit constant as the int64 torch stores (two's complement)."""
+    c &= _M64
+    return c - (1 << 64) if c >= 1 << 63 else c
+
+
+def _mix64(x: torch.Tensor) -> torch.Tensor:
+    """splitmix64's finalizer on int64 tensors (wrapping multiplies, logical shifts):
+    a counter-based hash, so edge e's column or value depends on (seed, e) only."""
+    x = x ^ ((x >> 30) & ((1 << 34) - 1))
+    x = x * _i64(0xBF58476D1CE4E5B9)
+    x = x ^ ((x >> 27) & ((1 << 37) - 1))
+    x = x * _i64(0x94D049BB133111EB)
+    return x ^ ((x >> 31) & ((1 << 33) - 1))
+
+
+def _key(seed: int, stream: int) -> int:
+    return _i64((seed * 0x9E3779B97F4A7C15 + stream * 0xD1B54A32D192ED03) & _M64)
+
+
+def synthetic_indptr(num_rows: int, num_edges: int, seed: int = 123, device="cuda",
+                     alpha: float = 2.2) -> torch.Tensor:
+    """indptr int32[V+1] of the synthetic graph: power-law out-degrees summing
+    to num_edges (cheap: V numbers; every rank of a partitioned run computes the
+    same one)."""
     gen = torch.Generator(device=device)
     gen.manual_seed(seed)
     deg = powerlaw_degrees(num_rows, num_edges, gen, device, alpha)
     indptr64 = torch.zeros(num_rows + 1, dtype=torch.int64, device=device)
     indptr64[1:] = torch.cumsum(deg, 0)
-    rows = torch.repeat_interleave(torch.arange(num_rows, device=device), deg)
-    cols = torch.randint(0, num_rows, (num_edges,), generator=gen, device=device,
-                         dtype=torch.int64)
+    return indptr64.to(torch.int32)
+
+
+def synthetic_columns(indptr: torch.Tensor, seed: int = 123, rows: tuple[int, int] | None = None,
+                      self_loops: bool = False) -> torch.Tensor:
+    """Columns int32 of rows [r0, r1) (all rows by default) of the synthetic
+    graph with this indptr: uniform in [0, V), distinct and ascending within a
+    row.  Edge e's column is a hash of (seed, e, attempt) -- duplicates within a
+    row are redrawn with the next attempt at their sorted position -- so a row
+    range is generated without the rest of the graph and equals the same rows
+    of the whole graph (a rank of the 1-D partition builds only its block)."""
+    V = indptr.numel() - 1
+    r0, r1 = rows if rows is not None else (0, V)
+    dev = indptr.device
+    ip = indptr[r0:r1 + 1].to(torch.int64)
+    e0, n = int(ip[0]), int(ip[-1] - ip[0])
+    deg = ip[1:] - ip[:-1]
+    row = torch.repeat_interleave(torch.arange(r0, r1, device=dev), deg, output_size=n)
+    pos = torch.arange(e0, e0 + n, device=dev, dtype=torch.int64)   # global edge ids
+    cols = (_mix64(pos ^ _key(seed, 0)) & ((1 << 62) - 1)) % V
     if self_loops:
         # the first slot of every non-empty row is the diagonal
-        first = indptr64[:-1][deg > 0]
-        cols[first] = torch.arange(num_rows, device=device)[deg > 0]
-    for _ in range(32):
-        key = rows * num_rows + cols
-        key, perm = torch.sort(key)
+        nz = deg > 0
+        cols[(ip[:-1] - e0)[nz]] = torch.arange(r0, r1, device=dev)[nz]
+    for attempt in range(1, 33):
+        key, perm = torch.sort(row * V + cols)      # rows ascending already: stays row-major
         cols = cols[perm]
         dup = torch.zeros_like(key, dtype=torch.bool)
         dup[1:] = key[1:] == key[:-1]
-        nd = int(dup.sum())
-        if nd == 0:
+        if not bool(dup.any()):
             break
-        cols[dup] = torch.randint(0, num_rows, (nd,), generator=gen, device=device,
-                                  dtype=torch.int64)
+        cols[dup] = (_mix64(pos[dup] ^ _key(seed, attempt)) & ((1 << 62) - 1)) % V
     else:
         raise RuntimeError("duplicate removal did not converge")
-    del rows
-    return indptr64.to(torch.int32), cols.to(torch.int32)
+    return cols.to(torch.int32)
+
+
+def synthetic_values(seed: int, e0: int, e1: int, device="cuda") -> torch.Tensor:
+    """fp32 U(0,1) edge values of global edges [e0, e1) (main.cu:83-84's
+    distribution), a hash of (seed, e): any slice equals the same slice of the
+    whole array."""
+    pos = torch.arange(e0, e1, device=device, dtype=torch.int64)
+    bits = (_mix64(pos ^ _key(seed, 101)) >> 40) & ((1 << 24) - 1)   # 24 random bits
+    return bits.to(torch.float32) * (1.0 / (1 << 24))
+
+
+def synthetic_csr_gpu(num_rows: int, num_edges: int, seed: int = 123, device="cuda",
+                      alpha: float = 2.2, self_loops: bool = False):
+    """(indptr int32[V+1], indices int32[E]) on `device`; columns uniform in
+    [0, V), no duplicates within a row, ascending within a row."""
+    indptr = synthetic_indptr(num_rows, num_edges, seed, device, alpha)
+    return indptr, synthetic_columns(indptr, seed, self_loops=self_loops)
 
 
 def small_csr(num_rows: int = 3000, seed: int = 123, extra_degrees=(0, 1, 63, 64, 65, 129, 257,

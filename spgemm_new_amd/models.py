@@ -124,3 +124,30 @@ class PartitionedSpGEMMFunction(Function):
     def backward(ctx, grad_output):
         dxs = ctx.model.backward(grad_output.contiguous(), ctx.sel, halo_sel=ctx.halo_sel)
         return cbsr_scatter(dxs, ctx.sel, ctx.h), None, None
+
+
+class PartitionedSpGEMMMultiFunction(Function):
+    """SpGEMMMultiFunction for one rank of a row-partitioned graph whose
+    PartitionedMaxK holds the relations' values fp32[E, R]: forward = top-k of
+    the own rows, one halo exchange shared by the R relations, fused local
+    forward -> [R, own rows, h]; backward = local multi-relation SSpMM, one
+    reverse exchange, dense scatter.
+
+        y_own = PartitionedSpGEMMMultiFunction.apply(x_own, model, maxk)
+    """
+
+    @staticmethod
+    def forward(ctx, features_own, model, maxk):
+        if features_own.dim() != 2 or features_own.shape[0] != model.plan.num_own:
+            raise RuntimeError("features must be the rank's own rows [num_own, h]")
+        x = features_own.contiguous()
+        data, sel = topk_cbsr(x, maxk, order="column")
+        out = model.forward_multi(data, sel, x.size(1))
+        ctx.model, ctx.sel, ctx.h = model, sel, x.size(1)
+        ctx.halo_sel = model.last_halo_selectors()
+        return out
+
+    @staticmethod
+    def backward(ctx, grad_output):
+        dxs = ctx.model.backward_multi(grad_output.contiguous(), ctx.sel, halo_sel=ctx.halo_sel)
+        return cbsr_scatter(dxs, ctx.sel, ctx.h), None, None

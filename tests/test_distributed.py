@@ -342,3 +342,81 @@ def test_partitioned_autograd_two_layers():
     ey = np.abs(y_part - y2.detach().cpu().numpy()) / np.maximum(1, np.abs(y2.detach().cpu().numpy()))
     eg = np.abs(g_part - xg.grad.cpu().numpy()) / np.maximum(1, np.abs(xg.grad.cpu().numpy()))
     assert ey.max() <= 1e-4 and eg.max() <= 1e-4, (ey.max(), eg.max())
+
+
+def _local_block_worker(rank, world, port, q):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from spgemm_new_amd.distributed import PartitionedMaxK, row_partition
+        from spgemm_new_amd.graphs import synthetic_columns, synthetic_indptr, synthetic_values
+        V, E, h, k = 1500, 40000, 64, 8
+        indptr = synthetic_indptr(V, E, seed=7, device="cpu")
+        b = row_partition(indptr, world)
+        r0, r1 = b[rank], b[rank + 1]
+        e0, e1 = int(indptr[r0]), int(indptr[r1])
+        # this rank generates only its rows (and their edge values)
+        cols = synthetic_columns(indptr, seed=7, rows=(r0, r1))
+        vals = synthetic_values(7, e0, e1, device="cpu")
+        m = PartitionedMaxK(indptr, cols, vals, rank, world, "cpu", engine=OracleEngine,
+                            local_block=True)
+        m_sync = PartitionedMaxK(indptr, cols, vals, rank, world, "cpu", engine=OracleEngine,
+                                 local_block=True, overlap_backward=False)
+        assert m.overlap_backward and not m_sync.overlap_backward
+        data, sel = random_cbsr(V, k, h, seed=3)
+        grad = np.random.default_rng(4).random((V, h), dtype=np.float32)
+        sel_l = m.local_rows(torch.from_numpy(sel))
+        d_l, g_l = m.local_rows(torch.from_numpy(data)), m.local_rows(torch.from_numpy(grad))
+        y = m.forward(d_l, sel_l, h)
+        dx = m.backward(g_l, sel_l)
+        m_sync.forward(d_l, sel_l, h)
+        assert torch.equal(dx, m_sync.backward(g_l, sel_l))   # overlap changes no sum order
+        ys, dxs = [None] * world, [None] * world
+        dist.all_gather_object(ys, y.numpy())
+        dist.all_gather_object(dxs, dx.numpy())
+        if rank == 0:
+            from oracle import oracle as O
+            from spgemm_new_amd.graphs import synthetic_csr_gpu
+            ip, ix = synthetic_csr_gpu(V, E, seed=7, device="cpu")   # the whole graph, once
+            vv = synthetic_values(7, 0, E, device="cpu").numpy()
+            ipn, ixn = ip.numpy(), ix.numpy()
+            q.put((O.parity_error(np.concatenate(ys), O.np_forward(ipn, ixn, vv, data, sel, h)),
+                   O.parity_error(np.concatenate(dxs), O.np_backward(ipn, ixn, vv, grad, sel))))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_partitioned_local_block_generation(world):
+    """Each rank generates only its own rows of the synthetic graph
+    (synthetic_columns / synthetic_values by row range, local_block=True) and
+    the partitioned forward / backward -- with and without the overlapped
+    reverse exchange -- equal the oracle on the whole graph."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_local_block_worker, args=(r, world, port, q))
+             for r in range(world)]
+    for p in procs:
+        p.start()
+    for p in procs:
+        p.join(timeout=240)
+    assert all(p.exitcode == 0 for p in procs), [p.exitcode for p in procs]
+    ey, ed = q.get(timeout=5)
+    assert ey <= 1e-5 and ed <= 1e-5, (ey, ed)
+
+
+def test_synthetic_row_range_equals_whole_graph():
+    """synthetic_columns over a row range == the same rows of the whole graph
+    (columns distinct and ascending per row), self loops included."""
+    from spgemm_new_amd.graphs import synthetic_columns, synthetic_csr_gpu, synthetic_values
+    ip, ix = synthetic_csr_gpu(3000, 90000, seed=5, device="cpu", self_loops=True)
+    for r0, r1 in ((0, 1), (17, 1234), (2999, 3000), (0, 3000)):
+        e0, e1 = int(ip[r0]), int(ip[r1])
+        assert torch.equal(synthetic_columns(ip, 5, rows=(r0, r1), self_loops=True), ix[e0:e1])
+    ipn, ixn = ip.numpy(), ix.numpy()
+    for r in range(3000):
+        seg = ixn[ipn[r]:ipn[r + 1]]
+        assert np.all(np.diff(seg) > 0) and (seg.size == 0 or r in seg)
+    assert torch.equal(synthetic_values(5, 100, 200, "cpu"), synthetic_values(5, 0, 300, "cpu")[100:200])

@@ -34,3 +34,33 @@ def test_training_two_ranks_rehearsal():
     assert out.returncode == 0, out.stderr[-3000:]
     losses = [float(l.split()[3]) for l in out.stdout.splitlines() if l.startswith("step")]
     assert len(losses) == 30 and min(losses[-5:]) < 0.8 * losses[0], losses
+
+
+@pytest.mark.gpu
+def test_training_multi_relation_loss_falls():
+    """--relations 8 (ogbn-proteins' edge features): every layer aggregates the 8
+    relations with the fused SpGEMM (SpGEMMMultiFunction) and its relation-
+    interleaved backward (k = 32), then a per-relation neighbour weight."""
+    import train_maxk_sage
+    losses = train_maxk_sage.main(["--graph", "proteins", "--nodes", "3000", "--steps", "40",
+                                   "--hidden", "64", "--maxk", "32", "--layers", "2",
+                                   "--feat", "50", "--classes", "7", "--relations", "8"])
+    assert all(l == l for l in losses)
+    assert min(losses[-5:]) < 0.8 * losses[0], losses
+
+
+@pytest.mark.gpu
+def test_training_multi_relation_two_ranks_rehearsal():
+    """Multi-relation SAGE on a row-partitioned graph (PartitionedSpGEMMMultiFunction:
+    one halo exchange per layer shared by the relations), 2 ranks on one GPU, gloo."""
+    import subprocess
+    env = dict(os.environ, BENCH_BACKEND="gloo")
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
+           "--master-addr", "127.0.0.1", "--master-port", "29623",
+           os.path.join(ROOT, "examples", "train_maxk_sage.py"), "--graph", "proteins",
+           "--nodes", "3000", "--steps", "30", "--hidden", "64", "--maxk", "16", "--layers", "2",
+           "--feat", "50", "--classes", "7", "--relations", "4"]
+    out = subprocess.run(cmd, cwd=ROOT, capture_output=True, text=True, timeout=600, env=env)
+    assert out.returncode == 0, out.stderr[-3000:]
+    losses = [float(l.split()[3]) for l in out.stdout.splitlines() if l.startswith("step")]
+    assert len(losses) == 30 and min(losses[-5:]) < 0.8 * losses[0], losses

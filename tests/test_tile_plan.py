@@ -223,3 +223,35 @@ def test_tile_backward_gpu_groups_and_zero_rows(dev, oracle):
     ref = oracle.np_backward(indptr, idx, vals, grad, sel)
     assert np.isfinite(got).all()
     assert oracle.parity_error(got, ref) < TOL
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("k", [32, 64])
+def test_tile_one_range_is_sequential_fma(dev, k):
+    """With one source range TILE adds each destination's edges in source-row
+    order, one fp32 FMA per edge, so every dXs entry equals the host replay
+    acc = fma(val, G[row, sel], acc) in CSR order bit for bit (fma emulated as
+    the exact fp64 product plus acc, rounded once).  LOCAL matches it at k = 64;
+    at k = 32 LOCAL rounds the product before the add in some entries
+    (tools/exp_tile_local_bits.py), a last-bit difference."""
+    import spgemm_new_amd as S
+    from spgemm_new_amd import _lib, ops
+    V = 2000
+    indptr, idx, vals = _graph(V, V, 30, seed=41)
+    grad, sel = _inputs(V, V, seed=41, k=k)
+    g = S.MaxKGraph(torch.from_numpy(indptr).to(dev), torch.from_numpy(idx).to(dev),
+                    torch.from_numpy(vals).to(dev))
+    ng = -(-V // tile.max_group(k))
+    plan = tile.build(g.indptr, g.indices, g.values, V, V, shape=(ng, -(-V // ng), 1), k=k)
+    plan["values_key"] = ops._tensor_key(g.values)
+    plan["part"] = torch.empty(1, device=dev)
+    g._tile[k] = plan
+    got = g.backward(torch.from_numpy(grad).to(dev), torch.from_numpy(sel).to(dev),
+                     algo=_lib.MAXK_BWD_TILE).cpu().numpy()
+    rows = np.repeat(np.arange(V), np.diff(indptr))
+    acc = np.zeros((V, k), np.float32)
+    for e in range(idx.size):          # CSR order = source-row order per destination
+        c = idx[e]
+        prod = np.float64(vals[e]) * grad[rows[e], sel[c].astype(np.int64)].astype(np.float64)
+        acc[c] = (prod + acc[c].astype(np.float64)).astype(np.float32)
+    assert np.array_equal(got, acc)
