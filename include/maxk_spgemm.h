@@ -107,6 +107,20 @@ int maxk_spgemm_forward_packed(const int32_t *sched, int64_t num_panels, const i
                                int num_rows, int dim_origin, int dim_k, float *out,
                                void *workspace, size_t workspace_bytes, void *stream);
 
+/* Forward that also writes the EDGE selectors edge_sel[e * dim_k + l] =
+ * cbsr_sel[indices[e] * dim_k + l] for every edge e (CSR order, uint8[E,
+ * dim_k]): the selector bytes the forward gathers anyway, stored sequentially,
+ * so the backward (MAXK_BWD_STAGED_EDGE) reads them in edge order instead of
+ * gathering one selector line per edge again (the dominant cost of the
+ * push backward on large graphs, e.g. ogbn-products).  packed = NULL reads
+ * cbsr_data / cbsr_sel; packed = maxk_cbsr_pack records (k = 4, 8, 16) reads
+ * those.  Same schedule and workspace as maxk_spgemm_forward; overwrites out. */
+int maxk_spgemm_forward_esel(const int32_t *sched, int64_t num_panels, const int32_t *indptr,
+                             const int32_t *indices, const float *values, const float *cbsr_data,
+                             const uint8_t *cbsr_sel, const void *packed, int num_rows,
+                             int dim_origin, int dim_k, float *out, uint8_t *edge_sel,
+                             void *workspace, size_t workspace_bytes, void *stream);
+
 /* ---------------------------------------------------------------------------
  * Halo records (the multi-GPU path; the reference is
  * single-GPU and has no counterpart).  maxk_cbsr_gather_records writes record
@@ -214,6 +228,9 @@ int maxk_spgemm_forward_multi(const int32_t *sched, int64_t num_panels, const in
 #define MAXK_BWD_STAGED 2      /* push to per-edge staging rows + CSC segmented sum */
 #define MAXK_BWD_LOCAL 3       /* destination-owned LDS accumulation (maxk_sspmm_backward_local) */
 #define MAXK_BWD_TILE 4        /* gradient rows staged once per CU (maxk_sspmm_backward_tile) */
+#define MAXK_BWD_STAGED_EDGE 5 /* STAGED reading EDGE selectors: cbsr_sel is uint8[num_edges,
+                                  dim_k] in CSR edge order (maxk_spgemm_forward_esel's edge_sel)
+                                  instead of the node CBSR selectors; workspace as STAGED */
 size_t maxk_backward_workspace_bytes(int algo, int64_t num_edges, int dim_k,
                                      int64_t csc_num_panels);
 int maxk_sspmm_backward(int algo, const int32_t *sched, int64_t num_panels,

@@ -28,6 +28,7 @@ MAXK_BWD_ATOMIC = 1
 MAXK_BWD_STAGED = 2
 MAXK_BWD_LOCAL = 3
 MAXK_BWD_TILE = 4
+MAXK_BWD_STAGED_EDGE = 5
 MAXK_TOPK_ORDER_COLUMN = 0
 MAXK_TOPK_ORDER_VALUE = 1
 MAXK_TOPK_ORDER_LANE = 2
@@ -69,6 +70,8 @@ SIGNATURES = {
     "maxk_tile_plan_set_values": (_I, [_P, _P, _L, _P, _P]),
     "maxk_cbsr_packed_row_bytes": (_S, [_I]),
     "maxk_cbsr_pack": (_I, [_P, _P, _I, _I, _P, _P]),
+    "maxk_spgemm_forward_esel": (_I, [_P, _L, _P, _P, _P, _P, _P, _P, _I, _I, _I, _P, _P, _P, _S,
+                                      _P]),
     "maxk_spgemm_forward_packed": (_I, [_P, _L, _P, _P, _P, _P, _I, _I, _I, _P, _P, _S, _P]),
     "maxk_csc_workspace_bytes": (_S, [_L, _I]),
     "maxk_csc_build": (_I, [_P, _L, _I, _P, _P, _P, _S, _P]),

@@ -217,11 +217,25 @@ struct Packed {
     static constexpr int RS = K == 4 ? 32 : (K == 8 ? 64 : (K == 16 ? 128 : 0));
 };
 
-template <int K, int RS = 0>
+// ESEL: also write the gathered selector bytes in edge order, esel[e * K + l]
+// (the backward's STAGED_EDGE pass then reads them sequentially instead of
+// gathering one selector line per edge a second time).
+// lane i <- lane i ^ 1 / i ^ 2 (DPP quad_perm [1,0,3,2] / [2,3,0,1])
+__device__ __forceinline__ uint32_t dpp_xor1(uint32_t v)
+{
+    return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0xB1, 0xF, 0xF, false);
+}
+__device__ __forceinline__ uint32_t dpp_xor2(uint32_t v)
+{
+    return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x4E, 0xF, 0xF, false);
+}
+
+template <int K, int RS = 0, bool ESEL = false>
 __device__ __forceinline__ void fwd_edges_vec(int e0, int e1, const int32_t *__restrict__ idx,
                                               const float *__restrict__ val,
                                               const float *__restrict__ data,
-                                              const uint8_t *__restrict__ sel, float *acc)
+                                              const uint8_t *__restrict__ sel, float *acc,
+                                              uint8_t *__restrict__ esel)
 {
     using Lay = FwdLayout<K>;
     constexpr int VEC = Lay::VEC, LPE = Lay::LPE, EPS = Lay::EPS;
@@ -278,6 +292,21 @@ __device__ __forceinline__ void fwd_edges_vec(int e0, int e1, const int32_t *__r
             for (int u = 0; u < U; ++u) {
                 const int t = (s0 + u) * EPS + slot;
                 if (t < n) rmw_acc<VEC>(my_acc, sb[u], v[u], d[u]);
+                if constexpr (ESEL) {
+                    // one dword store per 4 selector bytes: neighbouring lanes of the
+                    // edge hand theirs over (byte / short stores ran at ~1 TB/s)
+                    // (DPP quad permutes: no LDS traffic beside the accumulation's)
+                    uint32_t w = (uint32_t)sb[u];
+                    if constexpr (VEC == 2) w |= dpp_xor1(w) << 16;
+                    if constexpr (VEC == 1) {
+                        w |= dpp_xor1(w) << 8;
+                        w |= dpp_xor2(w) << 16;
+                    }
+                    constexpr int SPL = 4 / VEC;  // lanes per stored dword
+                    if (t < n && sub % SPL == 0)
+                        __builtin_nontemporal_store(
+                            w, reinterpret_cast<uint32_t *>(esel + (size_t)(base + t) * K + sub * VEC));
+                }
             }
         }
     }
@@ -288,7 +317,8 @@ __device__ __forceinline__ void fwd_edges_scalar(int e0, int e1, int k,
                                                  const int32_t *__restrict__ idx,
                                                  const float *__restrict__ val,
                                                  const float *__restrict__ data,
-                                                 const uint8_t *__restrict__ sel, float *acc)
+                                                 const uint8_t *__restrict__ sel, float *acc,
+                                                 uint8_t *__restrict__ esel)
 {
     const int lane = lane_id();
     if (k <= kWave) {
@@ -302,6 +332,7 @@ __device__ __forceinline__ void fwd_edges_scalar(int e0, int e1, int k,
                 const float v = val[my];
                 const size_t off = (size_t)c * k + l;
                 my_acc[sel[off]] += v * data[off];
+                if (esel) esel[(size_t)my * k + l] = sel[off];
             }
         }
     } else {
@@ -311,21 +342,23 @@ __device__ __forceinline__ void fwd_edges_scalar(int e0, int e1, int k,
             for (int l = lane; l < k; l += kWave) {
                 const size_t off = (size_t)c * k + l;
                 acc[sel[off]] += v * data[off];
+                if (esel) esel[(size_t)e * k + l] = sel[off];
             }
         }
     }
 }
 
-template <int K, int RS = 0>
+template <int K, int RS = 0, bool ESEL = false>
 __device__ __forceinline__ void fwd_edges(int e0, int e1, int k, const int32_t *__restrict__ idx,
                                           const float *__restrict__ val,
                                           const float *__restrict__ data,
-                                          const uint8_t *__restrict__ sel, float *acc)
+                                          const uint8_t *__restrict__ sel, float *acc,
+                                          uint8_t *__restrict__ esel = nullptr)
 {
     if constexpr (K > 0)
-        fwd_edges_vec<K, RS>(e0, e1, idx, val, data, sel, acc);
+        fwd_edges_vec<K, RS, ESEL>(e0, e1, idx, val, data, sel, acc, esel);
     else
-        fwd_edges_scalar(e0, e1, k, idx, val, data, sel, acc);
+        fwd_edges_scalar(e0, e1, k, idx, val, data, sel, acc, ESEL ? esel : nullptr);
 }
 
 // Row flushes: sum the `copies` LDS row copies, zero them, and store / add.
@@ -383,13 +416,13 @@ __device__ __forceinline__ void zero_lds(float *acc, int n)
 
 // Panel-scheduled forward.  Rows [i0, i1) are finished and owned by this
 // wave (plain store); row i1 is in progress at the panel end -> carry.
-template <int K, int RS = 0, bool ACC = false>
+template <int K, int RS = 0, bool ACC = false, bool ESEL = false>
 __global__ __launch_bounds__(kBlock) void fwd_panel_kernel(
     const int2 *__restrict__ sched, int64_t num_panels, const int32_t *__restrict__ indptr,
     const int32_t *__restrict__ idx, const float *__restrict__ val,
     const float *__restrict__ data, const uint8_t *__restrict__ sel, int num_rows, int dim,
     int k, float *__restrict__ out, float *__restrict__ carry, int32_t *__restrict__ carry_row,
-    float *__restrict__ owner)
+    float *__restrict__ owner, uint8_t *__restrict__ esel)
 {
     extern __shared__ __attribute__((aligned(16))) float lds[];
     const int dimp = (dim + 3) & ~3;
@@ -408,7 +441,7 @@ __global__ __launch_bounds__(kBlock) void fwd_panel_kernel(
     const bool split_first = i0 < i1 && j0 > indptr[i0];
     for (int r = i0; r < i1; ++r) {
         const int re = indptr[r + 1];
-        if (e < re) fwd_edges<K, RS>(e, re, k, idx, val, data, sel, acc);
+        if (e < re) fwd_edges<K, RS, ESEL>(e, re, k, idx, val, data, sel, acc, esel);
         if (r == i0 && split_first)
             flush_row<kStore>(acc, copies, owner + (size_t)w * dimp, dim);
         else
@@ -419,7 +452,7 @@ __global__ __launch_bounds__(kBlock) void fwd_panel_kernel(
     if (i1 < num_rows) {
         const int eb = e > indptr[i1] ? e : indptr[i1];
         if (eb < j1) {
-            fwd_edges<K, RS>(eb, j1, k, idx, val, data, sel, acc);
+            fwd_edges<K, RS, ESEL>(eb, j1, k, idx, val, data, sel, acc, esel);
             has_carry = 1;
         }
     }
@@ -1074,7 +1107,18 @@ __device__ __forceinline__ void bwd_edges_atomic_u(int e0, int e1, const int32_t
 // edge, 4 selected columns per lane, U selector loads in flight.
 // (The same lane mapping with 4 float atomics per lane for ATOMIC measured 4x
 // slower: lane-strided atomics do not coalesce.)
+// ESEL: sel holds the edge selectors (uint8[E, K], CSR edge order, written by
+// the forward): read sequentially at the edge's own index instead of gathered
+// at its destination's row.
+// P rows are padded to KP floats: at K = 8 a 32-B row is half a 64-B DRAM
+// sector, and scattered half-sector writes cost a read-modify-write (products
+// k=8 STAGED 6.2 ms); a full 64-B row (zeros in the pad) is written whole.
 template <int K>
+struct PRow {
+    static constexpr int KP = K == 8 ? 16 : K;
+};
+
+template <int K, bool ESEL = false>
 __device__ __forceinline__ void bwd_edges_stage_vec(int e0, int e1,
                                                     const int32_t *__restrict__ idx,
                                                     const float *__restrict__ val,
@@ -1082,7 +1126,8 @@ __device__ __forceinline__ void bwd_edges_stage_vec(int e0, int e1,
                                                     const uint8_t *__restrict__ sel,
                                                     const float *gs, float *__restrict__ P)
 {
-    constexpr int LPE = K / 4;
+    constexpr int KP = PRow<K>::KP;
+    constexpr int LPE = KP / 4;
     constexpr int EPS = kWave / LPE;
     constexpr int STEPS = kWave / EPS;
     constexpr int U = STEPS < 8 ? STEPS : 8;
@@ -1106,7 +1151,9 @@ __device__ __forceinline__ void bwd_edges_stage_vec(int e0, int e1,
             for (int u = 0; u < U; ++u) {
                 const int t = (s0 + u) * EPS + slot;
                 const int c = __shfl(my_c, t < kWave ? t : 0);
-                sb[u] = t < n ? *reinterpret_cast<const uint32_t *>(sel + (size_t)c * K + sub * 4) : 0u;
+                const size_t row = ESEL ? (size_t)(base + t) : (size_t)c;
+                sb[u] = t < n && sub * 4 < K
+                            ? *reinterpret_cast<const uint32_t *>(sel + row * K + sub * 4) : 0u;
             }
 #pragma unroll
             for (int u = 0; u < U; ++u) {
@@ -1114,14 +1161,16 @@ __device__ __forceinline__ void bwd_edges_stage_vec(int e0, int e1,
                 const int p = __shfl(my_p, t < kWave ? t : 0);
                 const float v = __shfl(my_v, t < kWave ? t : 0);
                 if (t < n) {
-                    f4 o;
-                    o.x = v * gs[sb[u] & 0xff];
-                    o.y = v * gs[(sb[u] >> 8) & 0xff];
-                    o.z = v * gs[(sb[u] >> 16) & 0xff];
-                    o.w = v * gs[sb[u] >> 24];
+                    f4 o = f4{0.f, 0.f, 0.f, 0.f};
+                    if (sub * 4 < K) {
+                        o.x = v * gs[sb[u] & 0xff];
+                        o.y = v * gs[(sb[u] >> 8) & 0xff];
+                        o.z = v * gs[(sb[u] >> 16) & 0xff];
+                        o.w = v * gs[sb[u] >> 24];
+                    }
                     // non-temporal: plain stores measured slower (Reddit 6.60 -> 6.97 ms,
                     // products 7.85 -> 8.20 ms): the staging lines would evict selector lines
-                    __builtin_nontemporal_store(o, reinterpret_cast<f4 *>(P + (size_t)p * K + sub * 4));
+                    __builtin_nontemporal_store(o, reinterpret_cast<f4 *>(P + (size_t)p * KP + sub * 4));
                 }
             }
         }
@@ -1133,19 +1182,20 @@ __device__ __forceinline__ void bwd_edges_stage_scalar(int e0, int e1, int k,
                                                        const float *__restrict__ val,
                                                        const int32_t *__restrict__ csc_pos,
                                                        const uint8_t *__restrict__ sel,
-                                                       const float *gs, float *__restrict__ P)
+                                                       const float *gs, float *__restrict__ P,
+                                                       bool esel)
 {
     const int lane = lane_id();
     for (int e = e0; e < e1; ++e) {
-        const int c = idx[e];
+        const size_t row = esel ? (size_t)e : (size_t)idx[e];
         const float v = val[e];
         const size_t p = (size_t)csc_pos[e];
-        for (int l = lane; l < k; l += kWave) P[p * k + l] = v * gs[sel[(size_t)c * k + l]];
+        for (int l = lane; l < k; l += kWave) P[p * k + l] = v * gs[sel[row * k + l]];
     }
 }
 
 // Panel-scheduled backward push (ATOMIC when P == nullptr, STAGED otherwise).
-template <int K, bool STAGED>
+template <int K, bool STAGED, bool ESEL = false>
 __global__ __launch_bounds__(kBlock) void bwd_panel_kernel(
     const int2 *__restrict__ sched, int64_t num_panels, const int32_t *__restrict__ indptr,
     const int32_t *__restrict__ idx, const float *__restrict__ val,
@@ -1169,9 +1219,9 @@ __global__ __launch_bounds__(kBlock) void bwd_panel_kernel(
         stage_row(gs, grad + (size_t)r * dim, dim);
         if constexpr (STAGED) {
             if constexpr (K > 0)
-                bwd_edges_stage_vec<K>(eb, ee, idx, val, csc_pos, sel, gs, P);
+                bwd_edges_stage_vec<K, ESEL>(eb, ee, idx, val, csc_pos, sel, gs, P);
             else
-                bwd_edges_stage_scalar(eb, ee, k, idx, val, csc_pos, sel, gs, P);
+                bwd_edges_stage_scalar(eb, ee, k, idx, val, csc_pos, sel, gs, P, ESEL);
         } else {
             if constexpr (K >= 1 && K <= kWave)
                 bwd_edges_atomic_u<K>(eb, ee, idx, val, sel, gs, dxs);
@@ -1192,6 +1242,7 @@ __device__ __forceinline__ f4 seg_sum_vec(int q0, int q1, const float *__restric
     const int lane = lane_id();
     const int sub = lane % LPE;
     const int slot = lane / LPE;
+    constexpr int KP = PRow<K>::KP;  // P row stride
     f4 s = f4{0.f, 0.f, 0.f, 0.f};
     constexpr int U = 4;
     int q = q0 + slot;
@@ -1200,7 +1251,7 @@ __device__ __forceinline__ f4 seg_sum_vec(int q0, int q1, const float *__restric
 #pragma unroll
         for (int u = 0; u < U; ++u)
             t[u] = __builtin_nontemporal_load(
-                reinterpret_cast<const f4 *>(P + (size_t)(q + u * EPS) * K + sub * 4));
+                reinterpret_cast<const f4 *>(P + (size_t)(q + u * EPS) * KP + sub * 4));
 #pragma unroll
         for (int u = 0; u < U; ++u) {
             s.x += t[u].x; s.y += t[u].y; s.z += t[u].z; s.w += t[u].w;
@@ -1208,7 +1259,7 @@ __device__ __forceinline__ f4 seg_sum_vec(int q0, int q1, const float *__restric
     }
     for (; q < q1; q += EPS) {
         const f4 t = __builtin_nontemporal_load(
-            reinterpret_cast<const f4 *>(P + (size_t)q * K + sub * 4));
+            reinterpret_cast<const f4 *>(P + (size_t)q * KP + sub * 4));
         s.x += t.x; s.y += t.y; s.z += t.z; s.w += t.w;
     }
 #pragma unroll
@@ -2463,13 +2514,14 @@ struct FwdPanel {
     static int run(const int32_t *sched, int64_t P, const int32_t *indptr, const int32_t *idx,
                    const float *val, const float *data, const uint8_t *sel, int V, int dim, int k,
                    float *out, float *carry, int32_t *carry_row, float *owner, bool acc,
-                   hipStream_t st)
+                   hipStream_t st, uint8_t *esel = nullptr)
     {
         const int64_t blocks = ceil_div(P, kWavesPerBlock);
-        auto kern = acc ? fwd_panel_kernel<K, 0, true> : fwd_panel_kernel<K, 0, false>;
+        auto kern = esel ? fwd_panel_kernel<K, 0, false, true>
+                         : acc ? fwd_panel_kernel<K, 0, true> : fwd_panel_kernel<K, 0, false>;
         hipLaunchKernelGGL(kern, dim3((unsigned)blocks), dim3(kBlock), fwd_lds_bytes<K>(k), st,
                            reinterpret_cast<const int2 *>(sched), P, indptr, idx, val, data, sel,
-                           V, dim, k, out, carry, carry_row, owner);
+                           V, dim, k, out, carry, carry_row, owner, esel);
         int rc = launch_status();
         if (rc) return rc;
         return fwd_fixup(sched, P, carry, owner, carry_row, out, dim, acc, st);
@@ -2480,17 +2532,19 @@ template <int K>
 struct FwdPanelPacked {
     static int run(const int32_t *sched, int64_t P, const int32_t *indptr, const int32_t *idx,
                    const float *val, const uint8_t *rec, int V, int dim, int k, float *out,
-                   float *carry, int32_t *carry_row, float *owner, hipStream_t st)
+                   float *carry, int32_t *carry_row, float *owner, hipStream_t st,
+                   uint8_t *esel = nullptr)
     {
         if constexpr (Packed<K>::RS == 0) {
             return MAXK_E_DIM;
         } else {
             constexpr int RS = Packed<K>::RS;
             const int64_t blocks = ceil_div(P, kWavesPerBlock);
-            hipLaunchKernelGGL((fwd_panel_kernel<K, RS>), dim3((unsigned)blocks), dim3(kBlock),
+            auto kern = esel ? fwd_panel_kernel<K, RS, false, true> : fwd_panel_kernel<K, RS>;
+            hipLaunchKernelGGL(kern, dim3((unsigned)blocks), dim3(kBlock),
                                fwd_lds_bytes<K>(k), st, reinterpret_cast<const int2 *>(sched), P,
                                indptr, idx, val, reinterpret_cast<const float *>(rec),
-                               rec + 4 * K, V, dim, k, out, carry, carry_row, owner);
+                               rec + 4 * K, V, dim, k, out, carry, carry_row, owner, esel);
             int rc = launch_status();
             if (rc) return rc;
             return fwd_fixup(sched, P, carry, owner, carry_row, out, dim, false, st);
@@ -2513,7 +2567,7 @@ struct FwdRecords {
             hipLaunchKernelGGL(kern, dim3((unsigned)blocks), dim3(kBlock), fwd_lds_bytes<K>(k), st,
                                reinterpret_cast<const int2 *>(sched), P, indptr, idx, val,
                                reinterpret_cast<const float *>(rec), rec + 4 * K, V, dim, k, out,
-                               carry, carry_row, owner);
+                               carry, carry_row, owner, (uint8_t *)nullptr);
             int rc = launch_status();
             if (rc) return rc;
             return fwd_fixup(sched, P, carry, owner, carry_row, out, dim, acc, st);
@@ -2625,10 +2679,15 @@ struct BwdPanel {
     static int run(bool staged, const int32_t *sched, int64_t P, const int32_t *indptr,
                    const int32_t *idx, const float *val, const float *grad, const uint8_t *sel,
                    const int32_t *csc_pos, int V, int dim, int k, float *dxs, float *Pbuf,
-                   hipStream_t st)
+                   hipStream_t st, bool esel = false)
     {
         const int64_t blocks = ceil_div(P, kWavesPerBlock);
-        if (staged)
+        if (staged && esel)
+            hipLaunchKernelGGL((bwd_panel_kernel<K, true, true>), dim3((unsigned)blocks),
+                               dim3(kBlock), row_lds_bytes(), st,
+                               reinterpret_cast<const int2 *>(sched), P, indptr, idx, val, grad,
+                               sel, csc_pos, V, dim, k, dxs, Pbuf);
+        else if (staged)
             hipLaunchKernelGGL((bwd_panel_kernel<K, true>), dim3((unsigned)blocks), dim3(kBlock),
                                row_lds_bytes(), st, reinterpret_cast<const int2 *>(sched), P,
                                indptr, idx, val, grad, sel, csc_pos, V, dim, k, dxs, Pbuf);
@@ -2866,6 +2925,38 @@ int maxk_spgemm_forward_packed(const int32_t *sched, int64_t num_panels, const i
     }
 }
 
+int maxk_spgemm_forward_esel(const int32_t *sched, int64_t num_panels, const int32_t *indptr,
+                             const int32_t *indices, const float *values, const float *cbsr_data,
+                             const uint8_t *cbsr_sel, const void *packed, int num_rows,
+                             int dim_origin, int dim_k, float *out, uint8_t *edge_sel,
+                             void *workspace, size_t workspace_bytes, void *stream)
+{
+    if (!sched || !indptr || !out || !edge_sel || num_panels < 1 || num_rows < 0) return MAXK_E_ARG;
+    if (!dims_ok(dim_origin, dim_k)) return MAXK_E_DIM;
+    if (packed && maxk_cbsr_packed_row_bytes(dim_k) == 0) return MAXK_E_DIM;
+    if (num_rows == 0) return MAXK_OK;
+    if (!indices || !values || (!packed && (!cbsr_data || !cbsr_sel))) return MAXK_E_ARG;
+    if (!workspace || workspace_bytes < maxk_forward_workspace_bytes(num_panels, dim_origin))
+        return MAXK_E_WORKSPACE;
+    const size_t dimp = (size_t)((dim_origin + 3) & ~3);
+    float *carry = static_cast<float *>(workspace);
+    int32_t *carry_row = reinterpret_cast<int32_t *>(
+        static_cast<char *>(workspace) + align_up((size_t)num_panels * dimp * sizeof(float), 256));
+    float *owner = fwd_owner_slots(workspace, num_panels, dim_origin);
+    hipStream_t st = as_stream(stream);
+    if (packed) {
+        const uint8_t *rec = static_cast<const uint8_t *>(packed);
+        switch (dim_k) {
+        case 4: return FwdPanelPacked<4>::run(sched, num_panels, indptr, indices, values, rec, num_rows, dim_origin, dim_k, out, carry, carry_row, owner, st, edge_sel);
+        case 8: return FwdPanelPacked<8>::run(sched, num_panels, indptr, indices, values, rec, num_rows, dim_origin, dim_k, out, carry, carry_row, owner, st, edge_sel);
+        default: return FwdPanelPacked<16>::run(sched, num_panels, indptr, indices, values, rec, num_rows, dim_origin, dim_k, out, carry, carry_row, owner, st, edge_sel);
+        }
+    }
+    return dispatch_k<FwdPanel>(dim_k, sched, num_panels, indptr, indices, values, cbsr_data,
+                                cbsr_sel, num_rows, dim_origin, dim_k, out, carry, carry_row, owner,
+                                false, st, edge_sel);
+}
+
 int maxk_cbsr_gather_records(const float *cbsr_data, const uint8_t *cbsr_sel, const int32_t *rows,
                              int64_t num_records, int dim_k, void *records, void *stream)
 {
@@ -2949,8 +3040,9 @@ int maxk_spgemm_forward_multi(const int32_t *sched, int64_t num_panels, const in
 size_t maxk_backward_workspace_bytes(int algo, int64_t num_edges, int dim_k,
                                      int64_t csc_num_panels)
 {
-    if (algo == MAXK_BWD_ATOMIC) return 0;
-    return align_up((size_t)num_edges * dim_k * sizeof(float), 256) +
+    if (algo == MAXK_BWD_ATOMIC) return 0;  // STAGED_EDGE: as STAGED
+    const int kp = dim_k == 8 ? 16 : dim_k;  // P rows padded to 64 B at k = 8 (PRow)
+    return align_up((size_t)num_edges * kp * sizeof(float), 256) +
            align_up((size_t)csc_num_panels * dim_k * sizeof(float), 256) +
            align_up((size_t)csc_num_panels * sizeof(int32_t), 256);
 }
@@ -2975,6 +3067,8 @@ int maxk_sspmm_backward(int algo, const int32_t *sched, int64_t num_panels,
     const bool staged_ready = csc_pos && csc_sched && csc_indptr && csc_num_panels >= 1 &&
                               workspace;
     if (algo == MAXK_BWD_AUTO) algo = staged_ready ? MAXK_BWD_STAGED : MAXK_BWD_ATOMIC;
+    const bool esel = algo == MAXK_BWD_STAGED_EDGE;  // cbsr_sel = edge selectors uint8[E, k]
+    if (esel) algo = MAXK_BWD_STAGED;
     if (algo == MAXK_BWD_ATOMIC) {
         const int e = zero_floats(dxs, (size_t)num_cols * dim_k, st);
         if (e) return e;
@@ -2983,17 +3077,19 @@ int maxk_sspmm_backward(int algo, const int32_t *sched, int64_t num_panels,
                                     dxs, (float *)nullptr, st);
     }
     if (algo != MAXK_BWD_STAGED || !staged_ready) return MAXK_E_ARG;
-    // workspace: [P rows (E*k floats)] [carry (CP*k floats)] [carry_row (CP ints)]
+    // workspace: [P rows (E*kp floats)] [carry (CP*k floats)] [carry_row (CP ints)]
     if (workspace_bytes < maxk_backward_workspace_bytes(algo, num_edges, dim_k, csc_num_panels))
         return MAXK_E_WORKSPACE;
-    const size_t pbytes = align_up((size_t)num_edges * dim_k * sizeof(float), 256);
+    const int kp = dim_k == 8 ? 16 : dim_k;
+    const size_t pbytes = align_up((size_t)num_edges * kp * sizeof(float), 256);
     const size_t carry_bytes = align_up((size_t)csc_num_panels * dim_k * sizeof(float), 256);
     float *Pbuf = static_cast<float *>(workspace);
     float *carry = reinterpret_cast<float *>(static_cast<char *>(workspace) + pbytes);
     int32_t *carry_row = reinterpret_cast<int32_t *>(static_cast<char *>(workspace) + pbytes +
                                                      carry_bytes);
     int rc = dispatch_k<BwdPanel>(dim_k, true, sched, num_panels, indptr, indices, values, grad,
-                                  cbsr_sel, csc_pos, num_rows, dim_origin, dim_k, dxs, Pbuf, st);
+                                  cbsr_sel, csc_pos, num_rows, dim_origin, dim_k, dxs, Pbuf, st,
+                                  esel);
     if (rc) return rc;
     return dispatch_k<BwdSegsum>(dim_k, csc_sched, csc_num_panels, csc_indptr, Pbuf, num_cols,
                                  dim_k, dxs, carry, carry_row, st);

@@ -69,6 +69,11 @@ AUTOTUNE_REPS = int(os.environ.get("MAXK_AUTOTUNE_REPS", 3))
 MIN_PANELS = int(os.environ.get("MAXK_MIN_PANELS", 16384))
 # TILE backward among the AUTO candidates (k = 32, h = 256)
 TILE_AUTO = os.environ.get("MAXK_TILE", "1") != "0"
+# STAGED_EDGE backward (edge selectors written by the forward) among the AUTO candidates
+ESEL_AUTO = os.environ.get("MAXK_ESEL", "1") != "0"
+# edge-selector buffers kept per graph (one per live selector tensor: a forward
+# per layer before the backwards)
+ESEL_CACHE = int(os.environ.get("MAXK_ESEL_CACHE", 4))
 
 
 def tile_shape_ok(dim_k: int, dim_origin: int) -> bool:
@@ -117,6 +122,21 @@ def _validate_csr(indptr: torch.Tensor, indices: torch.Tensor, num_cols: int) ->
         raise RuntimeError("indptr must be non-decreasing")
     if flags[3]:
         raise RuntimeError(f"indices out of range: every column must be in [0, {num_cols})")
+
+
+def _min_ms(fn, reps: int | None = None) -> float:
+    """fn's minimum time over a few calls (HIP events on the current stream),
+    after one untimed call."""
+    fn()
+    ms = float("inf")
+    for _ in range(AUTOTUNE_REPS if reps is None else reps):
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        fn()
+        e1.record()
+        e1.synchronize()
+        ms = min(ms, e0.elapsed_time(e1))
+    return ms
 
 
 class MaxKGraph:
@@ -184,6 +204,9 @@ class MaxKGraph:
         self._tile = {}
         self._ws = {}
         self._bwd_choice = {}
+        self._bwd_alt = {}        # AUTO's best algorithm other than STAGED_EDGE, per key
+        self._esel_on = set()     # (k, h): forwards write edge selectors (AUTO chose STAGED_EDGE)
+        self._esel = []           # [(sel key, sel, uint8 buffer[E * k])], most recent last
         self.last_bwd_algo = None
 
     # ------------------------------------------------------------------ utils
@@ -331,6 +354,47 @@ class MaxKGraph:
         blocks_per_cu = max(1, (160 * 1024) // max(per_block, 1))
         return plan["num_waves"] <= cus * blocks_per_cu * 4
 
+    def edge_selectors(self, sel: torch.Tensor):
+        """The edge selectors of ``sel`` (uint8[E * k], CSR edge order) when a
+        forward wrote them for this selector tensor (MAXK_BWD_STAGED_EDGE), else None."""
+        key = _tensor_key(sel)
+        for k_, s_, buf in reversed(self._esel):
+            if k_ == key and s_ is sel:
+                return buf
+        return None
+
+    def _esel_slot(self, sel: torch.Tensor) -> torch.Tensor:
+        """A buffer for the edge selectors of ``sel`` (recycles the oldest entry);
+        the entry holds ``sel`` so its address is not reused while cached."""
+        n = max(1, self.num_edges * sel.shape[1])
+        key = _tensor_key(sel)
+        for i, (k_, s_, buf) in enumerate(self._esel):
+            if s_ is sel:
+                del self._esel[i]
+                break
+        else:
+            buf = None
+            if len(self._esel) >= max(1, ESEL_CACHE):
+                _, _, buf = self._esel.pop(0)
+            if buf is None or buf.numel() < n:
+                buf = torch.empty(n, dtype=torch.uint8, device=self.device)
+        self._esel.append((key, sel, buf))
+        return buf
+
+    def make_edge_selectors(self, sel: torch.Tensor) -> torch.Tensor:
+        """Edge selectors for ``sel`` without a caller's forward: one forward
+        pass writing them (HIP, maxk_spgemm_forward_esel) into scratch output."""
+        buf = self.edge_selectors(sel)
+        if buf is None:
+            k = sel.shape[1]
+            dummy = self._workspace(("esel_data", k), self.num_cols * k * 4)
+            dummy = dummy[: self.num_cols * k * 4].view(torch.float32).view(self.num_cols, k)
+            y = torch.empty((self.num_rows, 256), dtype=torch.float32, device=self.device)
+            spgemm_forward(self, dummy, sel, 256, out=y, edge_sel=True)
+            del y
+            buf = self.edge_selectors(sel)
+        return buf
+
     def autotune_backward(self, grad, sel, out, values=None) -> int:
         """MAXK_BWD_AUTO: the fastest algorithm for this graph and k, measured once
         (each candidate run once, then timed AUTOTUNE_REPS times with HIP events on
@@ -366,20 +430,34 @@ class MaxKGraph:
             cands.append(_lib.MAXK_BWD_LOCAL)
         if tile_ok and self.tile_plan(k) is not None:
             cands.append(_lib.MAXK_BWD_TILE)
-        best, best_ms = None, float("inf")
+        penalty = 0.0
+        if ESEL_AUTO and grad.shape[1] <= 256:
+            # STAGED_EDGE is charged what writing the edge selectors adds to the
+            # forward (forward with them minus forward without, same inputs)
+            self.make_edge_selectors(sel)
+            cands.append(_lib.MAXK_BWD_STAGED_EDGE)
+            dummy = self._workspace(("esel_data", k), self.num_cols * k * 4)
+            dummy = dummy[: self.num_cols * k * 4].view(torch.float32).view(self.num_cols, k)
+            yd = torch.empty((self.num_rows, grad.shape[1]), dtype=torch.float32,
+                             device=self.device)
+            t_plain = _min_ms(lambda: spgemm_forward(self, dummy, sel, grad.shape[1], out=yd))
+            t_esel = _min_ms(lambda: spgemm_forward(self, dummy, sel, grad.shape[1], out=yd,
+                                                    edge_sel=True))
+            penalty = max(0.0, t_esel - t_plain)
+            del yd
+        best, best_ms, alt, alt_ms = None, float("inf"), None, float("inf")
         for a in cands:
-            sspmm_backward(self, grad, sel, out, values, a)
-            ms = float("inf")
-            for _ in range(AUTOTUNE_REPS):   # min of a few: one timing flipped close calls
-                e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-                e0.record()
-                sspmm_backward(self, grad, sel, out, values, a)
-                e1.record()
-                e1.synchronize()
-                ms = min(ms, e0.elapsed_time(e1))
+            ms = _min_ms(lambda: sspmm_backward(self, grad, sel, out, values, a))
+            if a == _lib.MAXK_BWD_STAGED_EDGE:
+                ms += penalty
+            elif ms < alt_ms:
+                alt, alt_ms = a, ms
             if ms < best_ms:
                 best, best_ms = a, ms
         self._bwd_choice[key] = best
+        self._bwd_alt[key] = alt
+        if best == _lib.MAXK_BWD_STAGED_EDGE:
+            self._esel_on.add((k, grad.shape[1]))
         self.bwd_timings = getattr(self, "bwd_timings", {})
         self.bwd_timings[key] = best_ms
         return best
@@ -393,10 +471,12 @@ class MaxKGraph:
     # ---------------------------------------------------------------- compute
     def forward(self, cbsr_data: torch.Tensor, cbsr_sel: torch.Tensor, dim_origin: int = 256,
                 out: torch.Tensor | None = None, values: torch.Tensor | None = None,
-                accumulate: bool = False) -> torch.Tensor:
+                accumulate: bool = False, edge_sel: bool | None = None) -> torch.Tensor:
         """Y = A . scatter(CBSR)  (spmm_maxk.cu:17-106).  Returns fp32[V, dim_origin];
-        accumulate=True adds into out instead."""
-        return spgemm_forward(self, cbsr_data, cbsr_sel, dim_origin, out, values, accumulate)
+        accumulate=True adds into out instead.  edge_sel: also write the edge
+        selectors for the STAGED_EDGE backward (None: when AUTO chose it)."""
+        return spgemm_forward(self, cbsr_data, cbsr_sel, dim_origin, out, values, accumulate,
+                              edge_sel)
 
     def forward_records(self, records: torch.Tensor, dim_k: int, dim_origin: int = 256,
                         out: torch.Tensor | None = None, values: torch.Tensor | None = None,
@@ -556,7 +636,9 @@ def _check_cbsr(g: MaxKGraph, data, sel):
 
 
 def spgemm_forward(g: MaxKGraph, data, sel, dim_origin: int = 256, out=None, values=None,
-                   accumulate: bool = False):
+                   accumulate: bool = False, edge_sel: bool | None = None):
+    """edge_sel: also write the edge selectors of sel (kept by the graph for the
+    STAGED_EDGE backward); None = when AUTO chose that backward for (k, h)."""
     _check_cbsr(g, data, sel)
     k = data.shape[1]
     values = _check_values(g, values)
@@ -572,11 +654,24 @@ def spgemm_forward(g: MaxKGraph, data, sel, dim_origin: int = 256, out=None, val
     L = _lib.load()
     nbytes = L.maxk_forward_workspace_bytes(g.num_panels, dim_origin)
     ws = g._workspace(("fwd", dim_origin), nbytes)
+    if edge_sel is None:
+        edge_sel = (k, dim_origin) in g._esel_on
+    edge_sel = edge_sel and not accumulate and g.num_edges > 0
     rs = L.maxk_cbsr_packed_row_bytes(k) if FWD_PACKED and not accumulate else 0
+    rec = None
     if rs:  # k in {4, 8, 16}: one cache line per gathered neighbour (packed records)
         rec = g._workspace(("packed", k), g.num_cols * rs)
         _lib.check(L.maxk_cbsr_pack(data.data_ptr(), sel.data_ptr(), g.num_cols, k, rec.data_ptr(),
                                     _stream(out)), "maxk_cbsr_pack")
+    if edge_sel:
+        es = g._esel_slot(sel)
+        _lib.check(L.maxk_spgemm_forward_esel(
+            g.sched.data_ptr(), g.num_panels, g.indptr.data_ptr(), g.indices.data_ptr(),
+            values.data_ptr(), data.data_ptr(), sel.data_ptr(), _lib.ptr(rec), g.num_rows,
+            dim_origin, k, out.data_ptr(), es.data_ptr(), ws.data_ptr(), ws.numel(), _stream(out)),
+            "maxk_spgemm_forward_esel")
+        return out
+    if rs:
         _lib.check(L.maxk_spgemm_forward_packed(
             g.sched.data_ptr(), g.num_panels, g.indptr.data_ptr(), g.indices.data_ptr(),
             values.data_ptr(), rec.data_ptr(), g.num_rows, dim_origin, k, out.data_ptr(),
@@ -706,6 +801,10 @@ def sspmm_backward(g: MaxKGraph, grad, sel, out=None, values=None, algo: int = _
         _on_device(g, grad_input=out)
     if algo == _lib.MAXK_BWD_AUTO:
         algo = g.autotune_backward(grad, sel, out, values)
+        if algo == _lib.MAXK_BWD_STAGED_EDGE and g.edge_selectors(sel) is None:
+            # this selector tensor went through no edge-selector forward: the best
+            # of the others (never a second forward pass on the hot path)
+            algo = g._bwd_alt.get((k, dim_origin, values is g.values), _lib.MAXK_BWD_STAGED)
     if g.num_edges == 0:
         algo = _lib.MAXK_BWD_ATOMIC  # nothing to stage: the call just zeroes dXs
     L = _lib.load()
@@ -741,14 +840,18 @@ def sspmm_backward(g: MaxKGraph, grad, sel, out=None, values=None, algo: int = _
     csc_pos = csc_indptr = csc_sched = None
     CP = 0
     ws = None
-    if algo == _lib.MAXK_BWD_STAGED:
+    sel_arg = sel
+    if algo == _lib.MAXK_BWD_STAGED_EDGE:
+        sel_arg = g.make_edge_selectors(sel)   # written by this sel's forward (else made here)
+    if algo in (_lib.MAXK_BWD_STAGED, _lib.MAXK_BWD_STAGED_EDGE):
         csc_pos, csc_indptr, csc_sched, CP = g.csc()
         nbytes = L.maxk_backward_workspace_bytes(algo, g.num_edges, k, CP)
         ws = g._workspace(("bwd", k), nbytes)
-    g.last_bwd_algo = {_lib.MAXK_BWD_ATOMIC: "atomic", _lib.MAXK_BWD_STAGED: "staged"}[algo]
+    g.last_bwd_algo = {_lib.MAXK_BWD_ATOMIC: "atomic", _lib.MAXK_BWD_STAGED: "staged",
+                       _lib.MAXK_BWD_STAGED_EDGE: "staged_edge"}[algo]
     _lib.check(L.maxk_sspmm_backward(
         algo, g.bwd_sched.data_ptr(), g.bwd_num_panels, g.indptr.data_ptr(), g.indices.data_ptr(),
-        values.data_ptr(), grad.data_ptr(), sel.data_ptr(), g.num_rows, g.num_cols, g.num_edges,
+        values.data_ptr(), grad.data_ptr(), sel_arg.data_ptr(), g.num_rows, g.num_cols, g.num_edges,
         dim_origin, k,
         out.data_ptr(), _lib.ptr(csc_pos), _lib.ptr(csc_sched), CP, _lib.ptr(csc_indptr),
         _lib.ptr(ws), 0 if ws is None else ws.numel(), _stream(out)), "maxk_sspmm_backward")

@@ -926,3 +926,57 @@ def test_auto_under_capture_keeps_tile(dev, g_small):
     graph.replay()
     torch.cuda.synchronize()
     assert torch.equal(dx, ref)
+
+
+@pytest.mark.parametrize("k", [4, 8, 16, 32, 64, 5])
+def test_edge_selector_forward_and_staged_edge(dev, oracle, g_small, k):
+    """maxk_spgemm_forward_esel: the same Y as the plain forward (packed records
+    at k = 4/8/16, generic k = 5) plus edge_sel[e] = sel[indices[e]]; the
+    STAGED_EDGE backward reading them equals STAGED bit for bit (same products
+    and sums, only the selector source differs) and the oracle."""
+    indptr, indices, values = g_small
+    v, h = len(indptr) - 1, 256
+    data, sel = random_cbsr(v, k, h, seed=k + 1)
+    g = S.MaxKGraph(T(indptr, dev), T(indices, dev), T(values, dev))
+    d, s = T(data, dev), T(sel, dev)
+    y0 = g.forward(d, s, h, edge_sel=False)
+    assert g.edge_selectors(s) is None
+    y1 = S.spgemm_forward(g, d, s, h, edge_sel=True)
+    assert torch.equal(y0, y1)
+    es = g.edge_selectors(s)
+    assert es is not None
+    assert torch.equal(es[: len(indices) * k].view(-1, k).cpu(),
+                       torch.from_numpy(sel[indices.astype(np.int64)]))
+    grad = T(np.random.default_rng(k).random((v, h), dtype=np.float32), dev)
+    a = g.backward(grad, s, algo=_lib.MAXK_BWD_STAGED_EDGE)
+    assert g.last_bwd_algo == "staged_edge"
+    b = g.backward(grad, s, algo=_lib.MAXK_BWD_STAGED)
+    assert torch.equal(a, b)
+    ref = oracle.np_backward(indptr, indices, values, grad.cpu().numpy(), sel)
+    assert oracle.parity_error(a.cpu().numpy(), ref) <= TOL
+
+
+def test_staged_edge_auto_flow(dev, g_small):
+    """AUTO with STAGED_EDGE forced to win: later forwards write the edge
+    selectors; a backward for a selector tensor whose forward wrote none takes
+    the best other algorithm; results agree with STAGED."""
+    from spgemm_new_amd import ops
+    indptr, indices, values = g_small
+    v, h, k = len(indptr) - 1, 256, 16
+    g = S.MaxKGraph(T(indptr, dev), T(indices, dev), T(values, dev))
+    g._bwd_choice[(k, h, True)] = _lib.MAXK_BWD_STAGED_EDGE
+    g._bwd_alt[(k, h, True)] = _lib.MAXK_BWD_ATOMIC
+    g._esel_on.add((k, h))
+    data, sel = random_cbsr(v, k, h, seed=3)
+    d, s = T(data, dev), T(sel, dev)
+    grad = T(np.random.default_rng(4).random((v, h), dtype=np.float32), dev)
+    g.forward(d, s, h)                        # writes the edge selectors of s
+    a = g.backward(grad, s)
+    assert g.last_bwd_algo == "staged_edge"
+    s2 = s.clone()                            # no forward wrote its edge selectors
+    b = g.backward(grad, s2)
+    assert g.last_bwd_algo == "atomic"
+    ref = g.backward(grad, s, algo=_lib.MAXK_BWD_STAGED)
+    assert torch.equal(a, ref)
+    assert (b - ref).abs().max().item() <= 1e-4 * max(1.0, ref.abs().max().item())
+    assert ops.ESEL_CACHE >= 1
