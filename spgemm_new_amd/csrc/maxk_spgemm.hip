@@ -220,6 +220,12 @@ struct Packed {
 // ESEL: also write the gathered selector bytes in edge order, esel[e * K + l]
 // (the backward's STAGED_EDGE pass then reads them sequentially instead of
 // gathering one selector line per edge a second time).
+#ifndef FWD_ESEL_DPP
+#define FWD_ESEL_DPP 0
+#endif
+#ifndef FWD_ESEL_NT
+#define FWD_ESEL_NT 0  // plain stores: products k=8 +0.26 ms vs +0.34 nt, k=32 +0.89 vs +1.04
+#endif
 // lane i <- lane i ^ 1 / i ^ 2 (DPP quad_perm [1,0,3,2] / [2,3,0,1])
 __device__ __forceinline__ uint32_t dpp_xor1(uint32_t v)
 {
@@ -295,17 +301,29 @@ __device__ __forceinline__ void fwd_edges_vec(int e0, int e1, const int32_t *__r
                 if constexpr (ESEL) {
                     // one dword store per 4 selector bytes: neighbouring lanes of the
                     // edge hand theirs over (byte / short stores ran at ~1 TB/s)
-                    // (DPP quad permutes: no LDS traffic beside the accumulation's)
                     uint32_t w = (uint32_t)sb[u];
+#if FWD_ESEL_DPP  // DPP quad permutes (no LDS op)
                     if constexpr (VEC == 2) w |= dpp_xor1(w) << 16;
                     if constexpr (VEC == 1) {
                         w |= dpp_xor1(w) << 8;
                         w |= dpp_xor2(w) << 16;
                     }
+#else
+                    if constexpr (VEC == 2) w |= (uint32_t)__shfl_xor((int)w, 1) << 16;
+                    if constexpr (VEC == 1) {
+                        w |= (uint32_t)__shfl_xor((int)w, 1) << 8;
+                        w |= (uint32_t)__shfl_xor((int)w, 2) << 16;
+                    }
+#endif
                     constexpr int SPL = 4 / VEC;  // lanes per stored dword
-                    if (t < n && sub % SPL == 0)
-                        __builtin_nontemporal_store(
-                            w, reinterpret_cast<uint32_t *>(esel + (size_t)(base + t) * K + sub * VEC));
+                    if (t < n && sub % SPL == 0) {
+                        uint32_t *dst = reinterpret_cast<uint32_t *>(esel + (size_t)(base + t) * K + sub * VEC);
+#if FWD_ESEL_NT
+                        __builtin_nontemporal_store(w, dst);
+#else
+                        *dst = w;
+#endif
+                    }
                 }
             }
         }

@@ -430,27 +430,30 @@ class MaxKGraph:
             cands.append(_lib.MAXK_BWD_LOCAL)
         if tile_ok and self.tile_plan(k) is not None:
             cands.append(_lib.MAXK_BWD_TILE)
-        penalty = 0.0
+        pair = None
         if ESEL_AUTO and grad.shape[1] <= 256:
-            # STAGED_EDGE is charged what writing the edge selectors adds to the
-            # forward (forward with them minus forward without, same inputs)
+            # STAGED_EDGE moves work into the forward (it writes the edge
+            # selectors) and the two share the caches, so every candidate is
+            # timed as forward + backward (dummy CBSR values, this sel), the
+            # forward writing the edge selectors only for STAGED_EDGE
             self.make_edge_selectors(sel)
             cands.append(_lib.MAXK_BWD_STAGED_EDGE)
             dummy = self._workspace(("esel_data", k), self.num_cols * k * 4)
             dummy = dummy[: self.num_cols * k * 4].view(torch.float32).view(self.num_cols, k)
             yd = torch.empty((self.num_rows, grad.shape[1]), dtype=torch.float32,
                              device=self.device)
-            t_plain = _min_ms(lambda: spgemm_forward(self, dummy, sel, grad.shape[1], out=yd))
-            t_esel = _min_ms(lambda: spgemm_forward(self, dummy, sel, grad.shape[1], out=yd,
-                                                    edge_sel=True))
-            penalty = max(0.0, t_esel - t_plain)
-            del yd
+
+            def pair(a):
+                spgemm_forward(self, dummy, sel, grad.shape[1], out=yd,
+                               edge_sel=a == _lib.MAXK_BWD_STAGED_EDGE)
+                sspmm_backward(self, grad, sel, out, values, a)
         best, best_ms, alt, alt_ms = None, float("inf"), None, float("inf")
         for a in cands:
-            ms = _min_ms(lambda: sspmm_backward(self, grad, sel, out, values, a))
-            if a == _lib.MAXK_BWD_STAGED_EDGE:
-                ms += penalty
-            elif ms < alt_ms:
+            if pair is not None:
+                ms = _min_ms(lambda: pair(a))
+            else:
+                ms = _min_ms(lambda: sspmm_backward(self, grad, sel, out, values, a))
+            if a != _lib.MAXK_BWD_STAGED_EDGE and ms < alt_ms:
                 alt, alt_ms = a, ms
             if ms < best_ms:
                 best, best_ms = a, ms

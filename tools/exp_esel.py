@@ -1,5 +1,6 @@
 """Products (config 3): forward with / without edge selectors, and the
-backward algorithms including STAGED_EDGE, each the minimum of 5 timed calls."""
+backward algorithms including STAGED_EDGE, each the minimum of 5 timed calls;
+the forward pair is measured three times, interleaved."""
 import sys
 
 import torch
@@ -19,15 +20,19 @@ vals = torch.rand(E, generator=gen, device=dev)
 X = torch.rand((V, 256), generator=gen, device=dev)
 G = torch.rand((V, 256), generator=gen, device=dev)
 g = S.MaxKGraph(ip, ix, vals)
+print("lib", _lib.LIB_PATH)
 for k in [int(a) for a in sys.argv[2:]] or (8, 16, 32):
     data, sel = S.topk_cbsr(X, k)
     y = torch.empty((V, 256), device=dev)
     dx = torch.empty((V, k), device=dev)
-    f0 = ops._min_ms(lambda: g.forward(data, sel, 256, out=y, edge_sel=False), 5)
-    f1 = ops._min_ms(lambda: g.forward(data, sel, 256, out=y, edge_sel=True), 5)
+    fw = []
+    for _ in range(3):
+        f0 = ops._min_ms(lambda: g.forward(data, sel, 256, out=y, edge_sel=False), 5)
+        f1 = ops._min_ms(lambda: g.forward(data, sel, 256, out=y, edge_sel=True), 5)
+        fw.append(f"{f0:.3f}/{f1:.3f}")
     res = {}
     for name, a in (("atomic", _lib.MAXK_BWD_ATOMIC), ("staged", _lib.MAXK_BWD_STAGED),
                     ("staged_edge", _lib.MAXK_BWD_STAGED_EDGE)):
         res[name] = ops._min_ms(lambda: g.backward(G, sel, out=dx, algo=a), 5)
-    print(f"{graph} k={k}: fwd {f0:.3f} fwd+esel {f1:.3f} (+{f1 - f0:.3f}) | " +
+    print(f"{graph} k={k}: fwd plain/esel {' '.join(fw)} | " +
           " ".join(f"{n} {t:.3f}" for n, t in res.items()), flush=True)
