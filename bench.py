@@ -195,7 +195,7 @@ def pmc_traffic(key, call, algo=None, bands=1):
         parts = [None if "bwd_local_kernel" not in k else k["bwd_local_kernel"] * bands]
     elif algo == "tile":
         parts = [k.get("bwd_tile_kernel"), k.get("tile_combine_kernel", 0.0)]
-    elif algo == "staged":
+    elif algo in ("staged", "staged_edge"):
         parts = [k.get("bwd_panel_kernel"), k.get("bwd_segsum_kernel"), fix]
     else:
         parts = [k.get("bwd_panel_kernel")]

@@ -8,7 +8,7 @@ export TMPDIR=/tmp
 tag=${1:-run}; shift
 out=gpurun_out/prof_$tag
 mkdir -p "$out"
-BENCH=(python3 bench.py --steps 3 --warmup 1 --no-cpu-baseline "$@")
+BENCH=(python3 bench.py --steps 3 --warmup 1 --no-cpu-baseline --no-vendor "$@")
 run() {  # run <name> <rocprof args...>
     local name=$1; shift
     timeout -k 10 600 rocprofv3 "$@" -d "$out/$name" -o "$name" --output-format csv -T \
