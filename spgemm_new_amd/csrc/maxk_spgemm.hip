@@ -2297,6 +2297,9 @@ __global__ __launch_bounds__(kTileWaves * kWave) void bwd_tile_kernel(
 #ifndef TILE_PF_AHEAD
 #define TILE_PF_AHEAD 128  // dwords: the window starts 512 B past the chunk's records
 #endif
+#ifndef TILE_ABLATE
+#define TILE_ABLATE 0  // development timing ablations (results wrong): 1 / 2 above
+#endif
     // the window must stay inside the record stream's padding: 512 records =
     // 1024 dwords after the last wave's stream (kTileRecPad in maxk_plan.hip)
     static_assert(TILE_PF_AHEAD + 4 * kWave <= 2 * 512, "TILE prefetch past the record padding");
@@ -2324,14 +2327,26 @@ __global__ __launch_bounds__(kTileWaves * kWave) void bwd_tile_kernel(
                      : "=&s"(pa), "=&s"(pb) : "s"(rb), "s"(ro), "s"(ro + 64) : "memory");
         // this wave's DMA of chunk c and header of chunk c landed; after the
         // barrier everyone's have, and chunk c-1's buffer is free
+#if TILE_ABLATE & 1  // timing ablation (wrong results): no chunk barrier
+        asm volatile("s_waitcnt vmcnt(" TILE_VMCNT ")" : "+v"(h), "+v"(pf)::"memory");
+#else
         asm volatile("s_waitcnt vmcnt(" TILE_VMCNT ")\n\ts_barrier" : "+v"(h), "+v"(pf)::"memory");
+#endif
         const uint32_t cnt = (uint32_t)__builtin_amdgcn_readfirstlane(h.x);
+        // (every step must issue exactly 3 DMA + 1 header load + 1 prefetch: the
+        // counted vmcnt above relies on it.  A step that issues fewer lets the wave
+        // read a header that has not landed -> garbage record counts -> s_loads past
+        // the record stream -> memory-access fault; measured with a "no DMA" ablation.)
         dma(c + 2, __builtin_amdgcn_readfirstlane(h.y), __builtin_amdgcn_readfirstlane(h.z),
             __builtin_amdgcn_readfirstlane(h.w));
         h = tile_load_hdr(hs + c + 5);
         prefetch();
         const uint32_t g0n = (cnt & 0xffffu) >> 2, gn = g0n + (cnt >> 18);
         uint32_t n = 0u - gn, m = 0u - g0n;
+#if TILE_ABLATE & 2  // timing ablation: no record processing
+        n = 0u;
+        m = 0u;
+#endif
         uint32_t ga[16], gb[16];
 #pragma unroll
         for (int i = 0; i < 16; ++i) {
