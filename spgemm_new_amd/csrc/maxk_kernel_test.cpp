@@ -15,7 +15,8 @@
 //                   this is the library's HIP dense SpMM on the same input)
 //   maxk            forward SpGEMM (merge-path schedule, no pre-zeroing)
 //   maxk_backward   backward SSpMM, the fastest of the algorithms below
-//   maxk_backward_{atomic,staged,local,tile}   (tile: k in {32, 64}; its plan
+//   maxk_backward_{atomic,staged,staged_edge,local,tile}   (staged_edge: the
+//                   edge selectors written by maxk_spgemm_forward_esel; tile: k in {32, 64}; its plan
 //                   from maxk_tile_plan_build, as MaxKGraph.tile_plan builds it)
 // Each time is the mean of 4 runs after 4 warm-ups, each run followed by a
 // device synchronise (spmm_base.h:58-75).  --check compares the forward
@@ -263,6 +264,19 @@ void test_graph(const std::string &dir, const std::string &graph, int idx, int c
             std::printf("%s maxk_backward_staged %g\n", out.c_str(), t);
             compare("staged");
             best = std::min(best, t);
+            // STAGED_EDGE: the forward stores the edge selectors, the backward reads them
+            uint8_t *esel = dev_alloc<uint8_t>((size_t)E * k);
+            MAXKCHECK(maxk_spgemm_forward_esel(sched, P, indptr, indices, val, data, sel, nullptr, V,
+                                               kDimOrigin, k, y, esel, fws, fws_b, st));
+            const double te = time_ms([&] {
+                MAXKCHECK(maxk_sspmm_backward(MAXK_BWD_STAGED_EDGE, sched, P, indptr, indices, val,
+                                              dense, esel, V, V, E, kDimOrigin, k, dxs, csc_pos,
+                                              csched, CP, csc_indptr, ws, b, st));
+            });
+            std::printf("%s maxk_backward_staged_edge %g\n", out.c_str(), te);
+            compare("staged_edge");
+            best = std::min(best, te);
+            HIPCHECK(hipFree(esel));
             HIPCHECK(hipFree(ws));
         }
         if (64 % k == 0 && E > 0) {

@@ -39,15 +39,16 @@ def test_harness_runs_and_validates(tmp_path):
     for g in ("g1", "g2"):
         assert (g, 16, "dense_spmm") in times
         for k in (16, 32, 64):
-            algos = ["maxk_backward_atomic", "maxk_backward_staged", "maxk_backward_local"]
+            algos = ["maxk_backward_atomic", "maxk_backward_staged", "maxk_backward_staged_edge",
+                     "maxk_backward_local"]
             if k in (32, 64):
                 algos.append("maxk_backward_tile")   # the TILE plan through the C ABI
             for kern in ["maxk", "maxk_backward"] + algos:
                 assert times[(g, k, kern)] > 0, (g, k, kern)
             assert times[(g, k, "maxk_backward")] == min(times[(g, k, a)] for a in algos)
     checks = [ln for ln in lines if "validation" in ln]
-    # per graph: k=16 fwd + staged + local; k=32 and k=64 also tile
-    assert len(checks) == 2 * (3 + 4 + 4), checks
+    # per graph: k=16 fwd + staged + staged_edge + local; k=32 and k=64 also tile
+    assert len(checks) == 2 * (4 + 5 + 5), checks
     assert all("validation pass!" in ln for ln in checks), checks
     assert sum("backward tile vs atomic" in ln for ln in checks) == 4
     assert np.isfinite(list(times.values())).all()
