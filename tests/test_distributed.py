@@ -420,3 +420,71 @@ def test_synthetic_row_range_equals_whole_graph():
         seg = ixn[ipn[r]:ipn[r + 1]]
         assert np.all(np.diff(seg) > 0) and (seg.size == 0 or r in seg)
     assert torch.equal(synthetic_values(5, 100, 200, "cpu"), synthetic_values(5, 0, 300, "cpu")[100:200])
+
+
+def _fullsize_worker(rank, world, port, q, graph, R):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from spgemm_new_amd.distributed import PartitionedMaxK, row_partition
+        from spgemm_new_amd.graphs import (CONFIGS, synthetic_columns, synthetic_indptr,
+                                           synthetic_values)
+        from spgemm_new_amd.ops import topk_cbsr
+        dev = torch.device("cuda:0")
+        V, E = CONFIGS[graph]
+        h, k = 256, 32
+        indptr = synthetic_indptr(V, E, device=dev)
+        b = row_partition(indptr, world)
+        r0, r1 = b[rank], b[rank + 1]
+        e0, e1 = int(indptr[r0]), int(indptr[r1])
+        cols = synthetic_columns(indptr, rows=(r0, r1))          # this rank's rows only
+        if R == 1:
+            vals = synthetic_values(123, e0, e1, device=dev)
+        else:
+            vals = torch.stack([synthetic_values(130 + q, e0, e1, device=dev) for q in range(R)],
+                               1).contiguous()
+        m = PartitionedMaxK(indptr, cols, vals, rank, world, dev, local_block=True)
+        gen = torch.Generator(device=dev)
+        gen.manual_seed(7 + rank)
+        x = torch.rand((r1 - r0, h), generator=gen, device=dev)
+        data, sel = topk_cbsr(x, k)
+        if R == 1:
+            G = torch.rand((r1 - r0, h), generator=gen, device=dev)
+            y = m.forward(data, sel, h)
+            dx = m.backward(G, sel)
+        else:
+            G = torch.rand((R, r1 - r0, h), generator=gen, device=dev)
+            y = m.forward_multi(data, sel, h)
+            dx = m.backward_multi(G, sel)
+        # adjoint identity over the whole graph: sum_ranks <Y_own, G_own> = sum_ranks <X^_own, dXs_own>
+        s = torch.tensor([float((y.double() * G.double()).sum()),
+                          float((data.double() * dx.double()).sum()),
+                          float(m.plan.num_halo)], dtype=torch.float64)
+        dist.all_reduce(s)
+        if rank == 0:
+            q.put(s.tolist())
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("graph,R", [("products", 1), ("proteins", 8)])
+def test_partitioned_full_size_two_ranks_one_gpu(graph, R):
+    """BASELINE config 4 (ogbn-products row-partitioned) and config 5 (proteins,
+    8 relations) at full size, 2 ranks sharing cuda:0 (gloo stands in for RCCL):
+    each rank generates only its block, the halo exchange runs both ways, and
+    the whole-graph adjoint identity holds to 1e-6."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_fullsize_worker, args=(r, 2, port, q, graph, R))
+             for r in range(2)]
+    for p in procs:
+        p.start()
+    for p in procs:
+        p.join(timeout=600)
+    assert all(p.exitcode == 0 for p in procs), [p.exitcode for p in procs]
+    lhs, rhs, halo = q.get(timeout=5)
+    assert halo > 0
+    assert abs(lhs - rhs) / abs(lhs) <= 1e-6, (lhs, rhs)
