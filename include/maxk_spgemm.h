@@ -320,6 +320,9 @@ int maxk_sspmm_backward_tile(const void *headers, const int64_t *header_start,
  *    edge values changed; the plan's structure does not depend on them). */
 int maxk_tile_plan_shape(int num_cols, int num_cus, int dim_k, int *num_groups, int *group_size,
                          int *splits);
+/* The plan format the library was built with (host out): LDS ring buffers and rows per
+ * buffer (chunks hold rows - 1 source rows; the header stream leads by buffers - 1). */
+int maxk_tile_format(int *num_buffers, int *buffer_rows);
 size_t maxk_tile_plan_workspace_bytes(int64_t num_edges, int num_workgroups);
 int maxk_tile_plan_build(const int32_t *indptr, const int32_t *indices, const float *values,
                          int num_rows, int num_cols, int64_t num_edges, int dim_k, int num_groups,

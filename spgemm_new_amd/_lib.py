@@ -62,6 +62,7 @@ SIGNATURES = {
                                             _P]),
     "maxk_sspmm_backward_tile": (_I, [_P, _P, _P, _P, _P, _I, _I, _I, _P, _P, _P, _I, _I, _I, _I,
                                       _P, _P, _P]),
+    "maxk_tile_format": (_I, [ctypes.POINTER(_I), ctypes.POINTER(_I)]),
     "maxk_tile_plan_shape": (_I, [_I, _I, _I, ctypes.POINTER(_I), ctypes.POINTER(_I),
                                   ctypes.POINTER(_I)]),
     "maxk_tile_plan_workspace_bytes": (_S, [_L, _I]),

@@ -30,6 +30,7 @@
 #include <stdint.h>
 
 #include "../../include/maxk_spgemm.h"
+#include "tile_format.h"
 
 namespace {
 
@@ -213,9 +214,7 @@ size_t scan_temp_bytes(int64_t n)
 // Segments are numbered in record-stream order, (wg, wave)-major:
 //   seg = ((chunk_base[wg] * 16 + wave * nch[wg] + chunk) * 2 + half),
 // and within a segment the records keep CSR edge order (two stable sorts).
-constexpr int kTileWaves = 16;
-constexpr int kTileRows = 47;
-constexpr int kTileBufRows = 48;
+constexpr int kTileLead = kTileBufs - 1;  // header entries before chunk 0's counts
 constexpr int kTileRecPad = 512;   // records of over-read padding after the stream (the
                                    // kernel's prefetch window is static_asserted against it)
 constexpr int kTileHdrPad = 8;     // header entries of padding
@@ -333,7 +332,7 @@ __global__ void tile_sizes_kernel(const int32_t *__restrict__ chunk_base, int NW
                                   const int32_t *__restrict__ max_pad, int64_t *__restrict__ sizes)
 {
     const int64_t chunks = chunk_base[NWG];
-    sizes[0] = kTileWaves * (chunks + 2 * (int64_t)NWG) + kTileHdrPad;
+    sizes[0] = kTileWaves * (chunks + kTileLead * (int64_t)NWG) + kTileHdrPad;
     sizes[1] = rec_off[chunks * 2 * kTileWaves] + kTileRecPad;
     sizes[2] = *max_pad;
 }
@@ -347,11 +346,12 @@ __global__ void tile_starts_kernel(const int32_t *__restrict__ chunk_base,
     if (t >= NWG * kTileWaves) return;
     const int b = t / kTileWaves, w = t % kTileWaves;
     const int64_t nch = chunk_base[b + 1] - chunk_base[b];
-    header_start[t] = kTileWaves * ((int64_t)chunk_base[b] + 2 * (int64_t)b) + w * (nch + 2);
+    header_start[t] =
+        kTileWaves * ((int64_t)chunk_base[b] + kTileLead * (int64_t)b) + w * (nch + kTileLead);
     record_start[t] = rec_off[((int64_t)chunk_base[b] * kTileWaves + w * nch) * 2];
 }
 
-// header entry t of (workgroup b, wave w), index i: counts of chunk i - 2 and
+// header entry t of (workgroup b, wave w), index i: counts of chunk i - kTileLead and
 // the source rows of the wave's three DMA pieces of chunk i (-1 = zero row)
 __global__ void tile_headers_kernel(const int32_t *__restrict__ chunk_base,
                                     const int32_t *__restrict__ wg_start,
@@ -362,26 +362,28 @@ __global__ void tile_headers_kernel(const int32_t *__restrict__ chunk_base,
     const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (t >= capacity) return;
     int4 out = make_int4(0, 0, 0, 0);
-    const int64_t total = kTileWaves * ((int64_t)chunk_base[NWG] + 2 * (int64_t)NWG);
+    const int64_t total = kTileWaves * ((int64_t)chunk_base[NWG] + kTileLead * (int64_t)NWG);
     if (t < total) {
         int lo = 0, hi = NWG;  // last b with 16 * (chunk_base[b] + 2b) <= t
         while (hi - lo > 1) {
             const int mid = (lo + hi) >> 1;
-            if (kTileWaves * ((int64_t)chunk_base[mid] + 2 * (int64_t)mid) <= t) lo = mid; else hi = mid;
+            if (kTileWaves * ((int64_t)chunk_base[mid] + kTileLead * (int64_t)mid) <= t) lo = mid;
+            else hi = mid;
         }
         const int b = lo;
         const int64_t nch = chunk_base[b + 1] - chunk_base[b];
-        const int64_t local = t - kTileWaves * ((int64_t)chunk_base[b] + 2 * (int64_t)b);
-        const int w = (int)(local / (nch + 2));
-        const int i = (int)(local % (nch + 2));
-        if (i >= 2) {
-            const int64_t s0 = (((int64_t)chunk_base[b] * kTileWaves + w * nch + (i - 2)) << 1);
+        const int64_t local = t - kTileWaves * ((int64_t)chunk_base[b] + kTileLead * (int64_t)b);
+        const int w = (int)(local / (nch + kTileLead));
+        const int i = (int)(local % (nch + kTileLead));
+        if (i >= kTileLead) {
+            const int64_t s0 =
+                (((int64_t)chunk_base[b] * kTileWaves + w * nch + (i - kTileLead)) << 1);
             out.x = pad[s0] | (pad[s0 + 1] << 16);
         }
         const int nrows = wg_start[b + 1] - wg_start[b];
         int rr[3];
-        for (int p = 0; p < 3; ++p) {
-            const int li = w * 3 + p;
+        for (int p = 0; p < kTilePieces; ++p) {
+            const int li = w * kTilePieces + p;
             const int64_t r = (int64_t)i * kTileRows + li;
             rr[p] = (li < kTileRows && r < nrows) ? urow[wg_start[b] + r] : -1;
         }
@@ -418,7 +420,8 @@ __global__ void tile_records_kernel(const int32_t *__restrict__ segs, const int3
     tile_edge_place(e, wgs[i], uidx[i] - 1, indices, wg_start, GS, k, wave, slot, half, chunk, rin);
     const int64_t pos = rec_off[s] + (j - first);
     if (pos >= capacity) return;
-    const uint32_t w0 = (uint32_t)slot | ((uint32_t)((chunk % 3) * kTileBufRows + rin) << 24);
+    const uint32_t w0 =
+        (uint32_t)slot | ((uint32_t)((chunk % kTileBufs) * kTileBufRows + rin) << 24);
     recs[pos] = make_int2((int)w0, __float_as_int(values[e]));
     if (edge_record) edge_record[e] = (int32_t)pos;
 }
@@ -584,6 +587,14 @@ int maxk_local_bands_build(const int32_t *woff, const int32_t *edge_rc, int num_
                        static_cast<hipStream_t>(stream), woff, edge_rc, num_waves, num_rows,
                        num_bands, seg_edge_off);
     return launch_status();
+}
+
+int maxk_tile_format(int *num_buffers, int *buffer_rows)
+{
+    if (!num_buffers || !buffer_rows) return MAXK_E_ARG;
+    *num_buffers = kTileBufs;
+    *buffer_rows = kTileBufRows;
+    return MAXK_OK;
 }
 
 int maxk_tile_plan_shape(int num_cols, int num_cus, int dim_k, int *num_groups, int *group_size,

@@ -29,6 +29,7 @@
 #include <stdint.h>
 
 #include "../../include/maxk_spgemm.h"
+#include "tile_format.h"
 
 #define MAXK_VERSION_STRING "maxk-mi355x 0.1 (gfx950, wave64)"
 
@@ -1841,10 +1842,17 @@ __global__ __launch_bounds__(kBlock) void bwd_local_rel8_kernel(
 // Record = int32x2 {slot | (buffer * 48 + row) << 24, value bits}.
 // Per chunk: the first 4 record groups are s_loaded before the barrier and
 // run software-pipelined in pairs; further groups run in an s_load loop.
-constexpr int kTileWaves = 16;
-constexpr int kTileRows = 47;  // gradient rows per chunk; row 47 of a buffer is zero
-constexpr int kTileBufRows = 48;
-static_assert(kTileRows + 1 == kTileBufRows, "chunk rows + zero row = buffer rows");
+// ring and chunk sizes: tile_format.h (shared with the plan builder)
+constexpr int kTileLead = kTileBufs - 1;  // chunks the DMA runs ahead of the records
+// outstanding VMEM ops allowed when a step waits for its chunk's DMA: the
+// wave issues exactly kTilePieces DMA + 1 header load + 1 prefetch per step
+#ifndef TILE_NO_PREFETCH
+constexpr int kTileStepOps = kTilePieces + 2;
+#else
+constexpr int kTileStepOps = kTilePieces + 1;
+#endif
+constexpr int kTileVmcnt = (kTileStepOps - kTilePieces) + kTileStepOps * (kTileLead - 1);
+static_assert(kTileVmcnt <= 63, "vmcnt field");
 
 typedef float tile_acc_t __attribute__((ext_vector_type(32)));
 typedef unsigned tile_sel_t __attribute__((ext_vector_type(16)));
@@ -2239,7 +2247,7 @@ __global__ __launch_bounds__(kTileWaves * kWave) void bwd_tile_kernel(
     const float *__restrict__ zero_row, const uint8_t *__restrict__ sel, int num_cols,
     int group_size, int splits, float *__restrict__ dxs, float *__restrict__ part)
 {
-    __shared__ __attribute__((aligned(16))) float tb[3 * kTileBufRows * kMaxDim];
+    __shared__ __attribute__((aligned(16))) float tb[kTileBufs * kTileBufRows * kMaxDim];
     const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const int lane = lane_id(), half = K == 32 ? lane >> 5 : 0, ent = lane & (K - 1);
     const uint64_t lo = K == 32 ? 0x00000000ffffffffull : ~0ull;
@@ -2282,14 +2290,18 @@ __global__ __launch_bounds__(kTileWaves * kWave) void bwd_tile_kernel(
     uint32_t ro = 0;  // byte offset of the next record group in this wave's stream
     const int nch = num_chunks[blockIdx.x];
     auto dma = [&](int c, int r0, int r1, int r2) {
-        const uint32_t buf = tb_base + (uint32_t)(c % 3) * kTileBufRows * 1024u;
+        static_assert(kTilePieces == 3, "three DMA pieces per wave and chunk");
+        const uint32_t buf = tb_base + (uint32_t)(c % kTileBufs) * kTileBufRows * 1024u;
         const int rows[3] = {r0, r1, r2};
 #pragma unroll
         for (int i = 0; i < 3; ++i) {
             const int r = __builtin_amdgcn_readfirstlane(rows[i]);
             const float *src = r >= 0 ? grad + (size_t)r * kMaxDim : zero_row;
+            // pieces past the buffer's rows (a ring of fewer than 48-row buffers)
+            // all write the zero row again: same bytes, same place
+            const int row = wv * 3 + i < kTileBufRows ? wv * 3 + i : kTileBufRows - 1;
             tile_glds(src + lane * 4,
-                      __builtin_amdgcn_readfirstlane(buf + (uint32_t)(wv * 3 + i) * 1024u));
+                      __builtin_amdgcn_readfirstlane(buf + (uint32_t)row * 1024u));
         }
     };
     // records about 1 KB ahead pulled into L2 for the s_loads (one load per chunk)
@@ -2305,21 +2317,23 @@ __global__ __launch_bounds__(kTileWaves * kWave) void bwd_tile_kernel(
     static_assert(TILE_PF_AHEAD + 4 * kWave <= 2 * 512, "TILE prefetch past the record padding");
 #ifndef TILE_NO_PREFETCH
     auto prefetch = [&]() { tile_prefetch(rb + (ro >> 2) + TILE_PF_AHEAD + lane * 4, pf); };
-#define TILE_VMCNT "7"
 #else
     auto prefetch = [&]() {};
-#define TILE_VMCNT "5"
 #endif
-    // header e(i) = {n0 | n1 << 16 of chunk i-2, the wave's DMA rows of chunk i};
-    // queue: H(0); per "iteration" i = -2, -1, 0, ...: DMA(i+2), H(i+3), prefetch
-    const tile_hdr_t e0 = hs[0], e1 = hs[1];
-    tile_hdr_t h0 = tile_load_hdr(hs + 2);
-    dma(0, e0.y, e0.z, e0.w);
-    tile_hdr_t h1 = tile_load_hdr(hs + 3);
-    prefetch();
-    dma(1, e1.y, e1.z, e1.w);
-    tile_hdr_t h2 = tile_load_hdr(hs + 4);
-    prefetch();
+    // header e(i) = {n0 | n1 << 16 of chunk i - L, the wave's DMA rows of chunk i},
+    // L = kTileLead; queue: H(L); per "iteration" i = -L, ..., -1, 0, 1, ...:
+    // DMA(i + L), H(i + 2L + 1), prefetch -- so every step issues the same ops
+    tile_hdr_t e[kTileLead];   // plain loads, waited for by the compiler before any DMA
+#pragma unroll
+    for (int i = 0; i < kTileLead; ++i) e[i] = hs[i];
+    tile_hdr_t hh[kTileBufs];
+    hh[0] = tile_load_hdr(hs + kTileLead);
+#pragma unroll
+    for (int i = 0; i < kTileLead; ++i) {
+        dma(i, e[i].y, e[i].z, e[i].w);
+        hh[i + 1] = tile_load_hdr(hs + kTileLead + 1 + i);
+        prefetch();
+    }
     auto step = [&](int c, tile_hdr_t &h) {
         // the chunk's first record group, in flight across the barrier
         tile_g16_t pa, pb;
@@ -2328,18 +2342,19 @@ __global__ __launch_bounds__(kTileWaves * kWave) void bwd_tile_kernel(
         // this wave's DMA of chunk c and header of chunk c landed; after the
         // barrier everyone's have, and chunk c-1's buffer is free
 #if TILE_ABLATE & 1  // timing ablation (wrong results): no chunk barrier
-        asm volatile("s_waitcnt vmcnt(" TILE_VMCNT ")" : "+v"(h), "+v"(pf)::"memory");
+        asm volatile("s_waitcnt vmcnt(%2)" : "+v"(h), "+v"(pf) : "n"(kTileVmcnt) : "memory");
 #else
-        asm volatile("s_waitcnt vmcnt(" TILE_VMCNT ")\n\ts_barrier" : "+v"(h), "+v"(pf)::"memory");
+        asm volatile("s_waitcnt vmcnt(%2)\n\ts_barrier" : "+v"(h), "+v"(pf) : "n"(kTileVmcnt)
+                     : "memory");
 #endif
         const uint32_t cnt = (uint32_t)__builtin_amdgcn_readfirstlane(h.x);
         // (every step must issue exactly 3 DMA + 1 header load + 1 prefetch: the
         // counted vmcnt above relies on it.  A step that issues fewer lets the wave
         // read a header that has not landed -> garbage record counts -> s_loads past
         // the record stream -> memory-access fault; measured with a "no DMA" ablation.)
-        dma(c + 2, __builtin_amdgcn_readfirstlane(h.y), __builtin_amdgcn_readfirstlane(h.z),
+        dma(c + kTileLead, __builtin_amdgcn_readfirstlane(h.y), __builtin_amdgcn_readfirstlane(h.z),
             __builtin_amdgcn_readfirstlane(h.w));
-        h = tile_load_hdr(hs + c + 5);
+        h = tile_load_hdr(hs + c + 2 * kTileLead + 1);
         prefetch();
         const uint32_t g0n = (cnt & 0xffffu) >> 2, gn = g0n + (cnt >> 18);
         uint32_t n = 0u - gn, m = 0u - g0n;
@@ -2358,12 +2373,14 @@ __global__ __launch_bounds__(kTileWaves * kWave) void bwd_tile_kernel(
         tile_group_loop(rb, ro + 128, n, m, lo, hi, selv, acc0, acc1);
         ro += 32 * gn;
     };
-    for (int c = 0; c < nch; c += 3) {
-        step(c, h0);
-        if (c + 1 < nch) step(c + 1, h1);
-        if (c + 2 < nch) step(c + 2, h2);
+    for (int c = 0; c < nch; c += kTileBufs) {
+#pragma unroll
+        for (int j = 0; j < kTileBufs; ++j)
+            if (c + j < nch) step(c + j, hh[j]);
     }
-    asm volatile("s_waitcnt vmcnt(0)" : "+v"(pf), "+v"(h0), "+v"(h1), "+v"(h2)::"memory");
+    asm volatile("s_waitcnt vmcnt(0)" : "+v"(pf)::"memory");
+#pragma unroll
+    for (int j = 0; j < kTileBufs; ++j) asm volatile("" : "+v"(hh[j])::"memory");
     float *out = split == 0 ? dxs : part + (size_t)(split - 1) * num_cols * K;
 #pragma unroll
     for (int s = 0; s < 64; ++s) {

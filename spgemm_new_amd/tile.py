@@ -11,15 +11,16 @@ module builds, once per graph, the streams the kernel walks:
 * source rows are cut into ``splits`` equal ranges; workgroup
   ``b = group * splits + range``;
 * a workgroup's distinct source rows (those with an edge into its group, in
-  ascending order) are cut into chunks of 47 rows; chunk c sits in LDS buffer
-  ``c % 3``, row 47 of every buffer is a zero row;
-* per (workgroup, wave) a header stream of int32x4 entries: e(0), e(1) =
-  {0, rows of chunks 0 and 1}, then e(c + 2) = {n0 | n1 << 16 of chunk c, rows
-  of chunk c + 2}, where "rows" are the source rows of the wave's three DMA
-  pieces (rows 3w .. 3w+2 of the chunk; -1 = the zero row);
+  ascending order) are cut into chunks of C = BR - 1 rows; chunk c sits in LDS
+  buffer ``c % NB`` of a ring of NB buffers of BR rows, the last row of every
+  buffer a zero row (NB, BR from ``ring_format()``; 3 x 48 by default);
+* per (workgroup, wave) a header stream of int32x4 entries: e(0) .. e(L-1) =
+  {0, rows of chunks 0 .. L-1}, then e(c + L) = {n0 | n1 << 16 of chunk c, rows
+  of chunk c + L}, L = NB - 1, where "rows" are the source rows of the wave's
+  three DMA pieces (rows 3w .. 3w+2 of the chunk; -1 = the zero row);
 * and a record stream: per chunk n0 records of half-0 destinations, then n1 of
   half-1 ones (each count a multiple of 4; padding record = slot 0, value 0,
-  the zero row); record = int32x2 {slot | ((c % 3) * 48 + row in chunk) << 24,
+  the zero row); record = int32x2 {slot | ((c % NB) * BR + row in chunk) << 24,
   value bits}: the slot register index reads bits 7:0, the selector word is
   w >> 2, its byte offset (w << 3) & 24 and the LDS byte address of the row
   w >> 14.
@@ -38,8 +39,21 @@ import torch
 from . import _lib
 
 WAVES = 16
-CHUNK_ROWS = 47
-BUF_ROWS = 48
+
+
+def ring_format() -> tuple[int, int, int]:
+    """(buffers, buffer rows, chunk rows) of the compiled library's TILE plan
+    format (tile_format.h via maxk_tile_format)."""
+    global _FMT
+    if _FMT is None:
+        L = _lib.load()
+        nb, br = ctypes.c_int(0), ctypes.c_int(0)
+        _lib.check(L.maxk_tile_format(ctypes.byref(nb), ctypes.byref(br)), "maxk_tile_format")
+        _FMT = (nb.value, br.value, br.value - 1)
+    return _FMT
+
+
+_FMT = None
 
 
 def max_group(k: int) -> int:
@@ -116,6 +130,8 @@ def set_values(plan, values: torch.Tensor) -> None:
 def emulate(plan, grad: torch.Tensor, sel: torch.Tensor) -> torch.Tensor:
     """CPU replay of bwd_tile_kernel over the plan (slow; small graphs): the
     LDS ring, the header and record streams and the record decode."""
+    NB, BR, _ = ring_format()
+    lead = NB - 1
     hdrs = plan["headers"].cpu()
     recs = plan["records"].cpu()
     hs = plan["header_start"].cpu().tolist()
@@ -131,7 +147,7 @@ def emulate(plan, grad: torch.Tensor, sel: torch.Tensor) -> torch.Tensor:
     else:
         jj = torch.arange(64)[:, None].expand(64, 64) * WAVES
     ent = torch.arange(64)[None, :] % K
-    lds = torch.zeros(3 * BUF_ROWS * 256)
+    lds = torch.zeros(NB * BR * 256)
     for b in range(G * NS):
         sp, g = b % NS, b // NS
         d0 = g * GS
@@ -143,10 +159,11 @@ def emulate(plan, grad: torch.Tensor, sel: torch.Tensor) -> torch.Tensor:
                 e = hdrs[hs[b * WAVES + wv] + c]
                 for i in range(3):
                     r = int(e[1 + i])
-                    base = ((c % 3) * BUF_ROWS + wv * 3 + i) * 256
+                    row = min(wv * 3 + i, BR - 1)      # pieces past the buffer: the zero row
+                    base = ((c % NB) * BR + row) * 256
                     lds[base: base + 256] = 0.0 if r < 0 else grad[r]
             for wv in range(WAVES):
-                e = hdrs[hs[b * WAVES + wv] + c + 2]
+                e = hdrs[hs[b * WAVES + wv] + c + lead]
                 n0, n1 = int(e[0]) & 0xFFFF, (int(e[0]) >> 16) & 0xFFFF
                 j = jj + wv
                 cols = torch.where(j < nd, sel[(d0 + j).clamp(max=C - 1), ent], 0)   # [slot, lane]

@@ -62,14 +62,16 @@ def test_plan_invariants():
     hdrs, recs = plan["headers"], plan["records"]
     hs, rs = plan["header_start"].tolist(), plan["record_start"].tolist()
     nch = plan["num_chunks"].tolist()
+    NB, BR, _ = tile.ring_format()
+    lead = NB - 1
     n_real = 0
     for b in range(G * NS):
         for wv in range(tile.WAVES):
             ro = rs[b * tile.WAVES + wv]
-            for c in range(nch[b] + 2):
+            for c in range(nch[b] + lead):
                 e = hdrs[hs[b * tile.WAVES + wv] + c]
                 assert all(int(r) == -1 or 0 <= int(r) < V for r in e[1:])
-                if c >= 2:
+                if c >= lead:
                     n0, n1 = int(e[0]) & 0xFFFF, int(e[0]) >> 16
                     assert n0 % 4 == 0 and n1 % 4 == 0
                     seg = recs[ro: ro + n0 + n1]
@@ -77,7 +79,7 @@ def test_plan_invariants():
                     n_real += int(real.sum())
                     # real records read rows of the chunk's own buffer
                     rowf = (seg[real][:, 0].long() & 0xFFFFFFFF) >> 24
-                    assert bool(((rowf // tile.BUF_ROWS) == (c - 2) % 3).all())
+                    assert bool(((rowf // BR) == (c - lead) % NB).all())
                     ro += n0 + n1
     assert n_real == int((torch.from_numpy(vals) != 0).sum())
 

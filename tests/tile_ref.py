@@ -8,7 +8,7 @@ from __future__ import annotations
 
 import torch
 
-from spgemm_new_amd.tile import BUF_ROWS, CHUNK_ROWS, WAVES
+from spgemm_new_amd.tile import WAVES, ring_format
 
 
 def max_group(k: int) -> int:
@@ -32,6 +32,8 @@ def build(indptr: torch.Tensor, indices: torch.Tensor, values: torch.Tensor, num
     """The TILE plan as a dict, or None when a chunk would overflow a wave's
     64-slot segment (many edges of few source rows into one wave's
     destinations; the other algorithms serve such graphs)."""
+    NB, BUF_ROWS, CHUNK_ROWS = ring_format()
+    lead = NB - 1
     dev = indices.device
     E = indices.numel()
     if E == 0 or num_rows < 1 or num_cols < 1:
@@ -99,11 +101,11 @@ def build(indptr: torch.Tensor, indices: torch.Tensor, values: torch.Tensor, num
     pos = seg_off.flatten()[base_seg] + h * pad.view(-1, 2)[base_seg, 0] + rank
     del sseg, rank, base_seg, h
     so = slot[order]
-    w0 = so | (((c % 3) * BUF_ROWS + rin)[order] << 24)
+    w0 = so | (((c % NB) * BUF_ROWS + rin)[order] << 24)
     recs[pos, 0] = torch.where(w0 >= (1 << 31), w0 - (1 << 32), w0).to(torch.int32)
     recs[pos, 1] = values[order].contiguous().view(torch.int32)
     del order, pos, so, seg, slot, rin, c
-    # header stream: e(0), e(1), then e(c + 2) per chunk
+    # header stream: e(0) .. e(lead - 1), then e(c + lead) per chunk
     wv = torch.arange(WAVES, **i64)
 
     def piece_rows(cc: torch.Tensor) -> torch.Tensor:                   # cc [M] -> [NWG,16,M,3]
@@ -113,16 +115,16 @@ def build(indptr: torch.Tensor, indices: torch.Tensor, values: torch.Tensor, num
         idx = torch.clamp(wg_start[:-1, None, None, None] + r, max=max(urow.numel() - 1, 0))
         return torch.where(ok, urow[idx].long(), -1)
 
-    hlen = (nch + 2).repeat_interleave(WAVES)                             # [NWG*16]
+    hlen = (nch + lead).repeat_interleave(WAVES)                          # [NWG*16]
     hstart = torch.cumsum(hlen, 0) - hlen
     hdrs = torch.zeros(int(hlen.sum()) + 8, 4, dtype=torch.int32, device=dev)
-    # e(i) for i in [0, maxch + 2): counts of chunk i-2, rows of chunk i
-    idx_e = torch.arange(maxch + 2, **i64)
+    # e(i) for i in [0, maxch + lead): counts of chunk i - lead, rows of chunk i
+    idx_e = torch.arange(maxch + lead, **i64)
     rows_e = piece_rows(idx_e)                                            # [NWG,16,maxch+2,3]
-    cnt_e = torch.zeros(NWG, WAVES, maxch + 2, **i64)
-    cnt_e[..., 2:] = pad[..., 0] | (pad[..., 1] << 16)
-    ok_e = idx_e[None, :] < (nch + 2)[:, None]                            # [NWG, maxch+2]
-    okw = ok_e[:, None, :].expand(NWG, WAVES, maxch + 2)
+    cnt_e = torch.zeros(NWG, WAVES, maxch + lead, **i64)
+    cnt_e[..., lead:] = pad[..., 0] | (pad[..., 1] << 16)
+    ok_e = idx_e[None, :] < (nch + lead)[:, None]                         # [NWG, maxch+lead]
+    okw = ok_e[:, None, :].expand(NWG, WAVES, maxch + lead)
     hp = (hstart.view(NWG, WAVES, 1) + idx_e[None, None, :])[okw]
     hdrs[hp, 0] = cnt_e[okw].to(torch.int32)
     r3 = rows_e[okw]
