@@ -319,9 +319,8 @@ class MaxKGraph:
     def tile_plan(self, dim_k: int = 32):
         """Plan of the TILE backward (k = 32 or 64, h = 256; spgemm_new_amd/tile.py),
         or None when the shape does not suit it (then the other algorithms serve
-        it).  Built once per k on the device (maxk_tile_plan_build).  The
-        records carry the graph's edge values: when ``self.values`` has changed
-        in place since, they are rewritten first (one scatter, tile.set_values)."""
+        it).  Built once per k on the device (maxk_tile_plan_build).  Its records
+        carry edge values; ``tile_values`` makes them hold a given values tensor."""
         if dim_k not in self._tile:
             from . import tile
             plan = None
@@ -331,17 +330,28 @@ class MaxKGraph:
                                   self.values[: self.num_edges], self.num_rows, self.num_cols,
                                   cus=cus, k=dim_k)
             if plan is not None:
+                # the values the records hold: key + the tensor (kept alive so its
+                # address cannot be reused by another tensor with the same key)
                 plan["values_key"] = _tensor_key(self.values)
+                plan["values_ref"] = self.values
                 G, NS = plan["num_groups"], plan["splits"]
                 plan["part"] = torch.empty(max(1, (NS - 1) * self.num_cols * dim_k),
                                            dtype=torch.float32, device=self.device)
             self._tile[dim_k] = plan
-        plan = self._tile[dim_k]
-        if plan is not None and plan["values_key"] != _tensor_key(self.values):
+        return self._tile[dim_k]
+
+    def tile_values(self, plan, values: torch.Tensor) -> None:
+        """Make the TILE records hold ``values`` (fp32[E]: the graph's own, changed
+        in place or not, or per-call ones): one scatter of E values into the
+        records (maxk_tile_plan_set_values) when they hold anything else.  While
+        a hipGraph is captured the scatter is always recorded, so replays pick
+        up values changed between them."""
+        key = _tensor_key(values)
+        if plan["values_key"] != key or plan["values_ref"] is not values or \
+                torch.cuda.is_current_stream_capturing():
             from . import tile
-            tile.set_values(plan, self.values[: self.num_edges])
-            plan["values_key"] = _tensor_key(self.values)
-        return plan
+            tile.set_values(plan, values[: self.num_edges])
+            plan["values_key"], plan["values_ref"] = key, values
 
     def local_fits(self, dim_k: int) -> bool:
         """True when the LOCAL plan's waves are all co-resident (one sweep of G)."""
@@ -407,12 +417,12 @@ class MaxKGraph:
         shape once made; MAXK_BWD_* pins one explicitly."""
         k = sel.shape[1]
         own = values is None or values is self.values
-        # TILE's records hold the graph's own values, so the choice is kept per
-        # (k, h, own values): a call with other values never gets TILE back
+        # kept per (k, h, own values): with other values TILE pays a scatter of the
+        # values into its records whenever they change, so the ranking can differ
         key = (k, grad.shape[1], own)
         if key in self._bwd_choice:
             return self._bwd_choice[key]
-        tile_ok = TILE_AUTO and own and tile_shape_ok(k, grad.shape[1])
+        tile_ok = TILE_AUTO and tile_shape_ok(k, grad.shape[1])
         if self.num_edges == 0:
             return _lib.MAXK_BWD_STAGED
         if torch.cuda.is_current_stream_capturing():
@@ -422,7 +432,7 @@ class MaxKGraph:
             hit = self._bwd_choice.get((k, grad.shape[1], True))
             if hit is not None and (own or hit != _lib.MAXK_BWD_TILE):
                 return hit
-            if tile_ok and self._tile.get(k) is not None:
+            if tile_ok and own and self._tile.get(k) is not None:
                 return _lib.MAXK_BWD_TILE
             return _lib.MAXK_BWD_STAGED
         cands = [_lib.MAXK_BWD_STAGED, _lib.MAXK_BWD_ATOMIC]
@@ -815,8 +825,7 @@ def sspmm_backward(g: MaxKGraph, grad, sel, out=None, values=None, algo: int = _
         plan = g.tile_plan(k) if tile_shape_ok(k, dim_origin) else None
         if plan is None:
             raise RuntimeError("TILE backward unsupported for this shape (k = 32 or 64, h = 256)")
-        if values is not g.values:
-            raise RuntimeError("TILE backward: the plan holds the graph's own edge values")
+        g.tile_values(plan, values)   # the records' values (refreshed when they changed)
         g.last_bwd_algo = "tile"
         NS = plan["splits"]
         _lib.check(L.maxk_sspmm_backward_tile(

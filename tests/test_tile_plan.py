@@ -152,9 +152,11 @@ def test_tile_values_changed_in_place(dev, oracle):
 
 
 @pytest.mark.gpu
-def test_auto_with_foreign_values_after_tile(dev):
-    """AUTO chose TILE for the graph's own values; a later AUTO call with other
-    values must not get TILE back (its records hold the graph's values)."""
+def test_tile_with_per_call_values(dev):
+    """TILE with values other than the graph's own (its records are rewritten
+    when the values they hold change): explicit and AUTO calls, alternating
+    with own-values calls, all equal STAGED on the same values; AUTO keeps a
+    separate choice for foreign values."""
     import spgemm_new_amd as S
     V = 3000
     indptr, idx, vals = _graph(V, V, 40, seed=5)
@@ -162,15 +164,51 @@ def test_auto_with_foreign_values_after_tile(dev):
     g = S.MaxKGraph(torch.from_numpy(indptr).to(dev), torch.from_numpy(idx).to(dev),
                     torch.from_numpy(vals).to(dev))
     G, sl = torch.from_numpy(grad).to(dev), torch.from_numpy(sel).to(dev)
-    g._bwd_choice[(32, 256, True)] = S._lib.MAXK_BWD_TILE   # as if AUTO had measured TILE fastest
-    own = g.backward(G, sl)
-    assert g.last_bwd_algo == "tile"
     w = torch.rand(idx.size, device=dev)
-    other = g.backward(G, sl, values=w)
-    assert g.last_bwd_algo != "tile"
-    ref = g.backward(G, sl, values=w, algo=S._lib.MAXK_BWD_STAGED)
-    assert (other - ref).abs().max().item() <= 1e-4 * max(1.0, ref.abs().max().item())
-    assert torch.equal(own, g.backward(G, sl))
+
+    def close(a, b):
+        return (a - b).abs().max().item() <= 1e-4 * max(1.0, b.abs().max().item())
+    ref_own = g.backward(G, sl, algo=S._lib.MAXK_BWD_STAGED)
+    ref_w = g.backward(G, sl, values=w, algo=S._lib.MAXK_BWD_STAGED)
+    for _ in range(2):   # own -> foreign -> own ...: the records follow
+        own = g.backward(G, sl, algo=S._lib.MAXK_BWD_TILE)
+        assert close(own, ref_own)
+        other = g.backward(G, sl, values=w, algo=S._lib.MAXK_BWD_TILE)
+        assert g.last_bwd_algo == "tile" and close(other, ref_w)
+    w.mul_(0.5)          # foreign values changed in place: refreshed too
+    assert close(g.backward(G, sl, values=w, algo=S._lib.MAXK_BWD_TILE), 0.5 * ref_w)
+    a_own = g.backward(G, sl)
+    a_w = g.backward(G, sl, values=w)
+    assert close(a_own, ref_own) and close(a_w, 0.5 * ref_w)
+    assert (32, 256, True) in g._bwd_choice and (32, 256, False) in g._bwd_choice
+
+
+@pytest.mark.gpu
+def test_tile_capture_sees_value_changes(dev):
+    """A captured TILE backward records the records refresh, so edge values
+    updated in place between replays are used."""
+    import spgemm_new_amd as S
+    V = 3000
+    indptr, idx, vals = _graph(V, V, 40, seed=8)
+    grad, sel = _inputs(V, V, seed=8)
+    g = S.MaxKGraph(torch.from_numpy(indptr).to(dev), torch.from_numpy(idx).to(dev),
+                    torch.from_numpy(vals).to(dev))
+    G, sl = torch.from_numpy(grad).to(dev), torch.from_numpy(sel).to(dev)
+    dx = torch.empty((V, 32), device=dev)
+    g.backward(G, sl, out=dx, algo=S._lib.MAXK_BWD_TILE)     # plan built outside the capture
+    torch.cuda.synchronize()
+    graph = torch.cuda.CUDAGraph()
+    stream = torch.cuda.Stream()
+    stream.wait_stream(torch.cuda.current_stream())
+    with torch.cuda.stream(stream):
+        with torch.cuda.graph(graph, stream=stream):
+            g.backward(G, sl, out=dx, algo=S._lib.MAXK_BWD_TILE)
+    torch.cuda.current_stream().wait_stream(stream)
+    g.values.mul_(3.0)
+    graph.replay()
+    torch.cuda.synchronize()
+    ref = g.backward(G, sl, algo=S._lib.MAXK_BWD_STAGED)
+    assert (dx - ref).abs().max().item() <= 1e-4 * max(1.0, ref.abs().max().item())
 
 
 @pytest.mark.gpu
@@ -245,7 +283,7 @@ def test_tile_one_range_is_sequential_fma(dev, k):
                     torch.from_numpy(vals).to(dev))
     ng = -(-V // tile.max_group(k))
     plan = tile.build(g.indptr, g.indices, g.values, V, V, shape=(ng, -(-V // ng), 1), k=k)
-    plan["values_key"] = ops._tensor_key(g.values)
+    plan["values_key"], plan["values_ref"] = ops._tensor_key(g.values), g.values
     plan["part"] = torch.empty(1, device=dev)
     g._tile[k] = plan
     got = g.backward(torch.from_numpy(grad).to(dev), torch.from_numpy(sel).to(dev),

@@ -27,7 +27,7 @@ for k in (32, 64):
     mg = tile.max_group(k)
     ng = -(-V // mg)
     plan = tile.build(g.indptr, g.indices, g.values, V, V, shape=(ng, -(-V // ng), 1), k=k)
-    plan["values_key"] = ops._tensor_key(g.values)
+    plan["values_key"], plan["values_ref"] = ops._tensor_key(g.values), g.values
     plan["part"] = torch.empty(1, device=dev)
     g._tile[k] = plan
     t = g.backward(Gr, sel, algo=_lib.MAXK_BWD_TILE)
