@@ -38,7 +38,8 @@ def parse():
     p.add_argument("--k", type=int, default=32)
     p.add_argument("--h", type=int, default=256)
     p.add_argument("--seed", type=int, default=123)
-    p.add_argument("--bwd-algo", default="auto", choices=["auto", "atomic", "staged", "local", "tile"])
+    p.add_argument("--bwd-algo", default="auto",
+                   choices=["auto", "atomic", "staged", "local", "tile", "staged_edge", "edge_gather"])
     p.add_argument("--panel-cost", type=int, default=None)
     p.add_argument("--row-cost", type=int, default=None)
     p.add_argument("--no-cpu-baseline", action="store_true")
@@ -195,7 +196,7 @@ def pmc_traffic(key, call, algo=None, bands=1):
         parts = [None if "bwd_local_kernel" not in k else k["bwd_local_kernel"] * bands]
     elif algo == "tile":
         parts = [k.get("bwd_tile_kernel"), k.get("tile_combine_kernel", 0.0)]
-    elif algo in ("staged", "staged_edge"):
+    elif algo in ("staged", "staged_edge", "edge_gather"):
         parts = [k.get("bwd_panel_kernel"), k.get("bwd_segsum_kernel"), fix]
     else:
         parts = [k.get("bwd_panel_kernel")]
@@ -444,7 +445,8 @@ def main():
 
     algo = {"auto": _lib.MAXK_BWD_AUTO, "atomic": _lib.MAXK_BWD_ATOMIC,
             "staged": _lib.MAXK_BWD_STAGED, "local": _lib.MAXK_BWD_LOCAL,
-            "tile": _lib.MAXK_BWD_TILE}[args.bwd_algo]
+            "tile": _lib.MAXK_BWD_TILE, "staged_edge": _lib.MAXK_BWD_STAGED_EDGE,
+            "edge_gather": _lib.MAXK_BWD_EDGE_GATHER}[args.bwd_algo]
     kw = {}
     if args.panel_cost:
         kw["panel_cost"] = args.panel_cost

@@ -168,6 +168,8 @@ int maxk_spgemm_forward_records(const int32_t *sched, int64_t num_panels, const 
 size_t maxk_csc_workspace_bytes(int64_t num_edges, int num_cols);
 int maxk_csc_build(const int32_t *indices, int64_t num_edges, int num_cols, int32_t *csc_indptr,
                    int32_t *csc_pos, void *workspace, size_t workspace_bytes, void *stream);
+/* csc_perm[csc_pos[e]] = e: the CSC slot -> CSR edge permutation (MAXK_BWD_EDGE_GATHER). */
+int maxk_csc_perm_build(const int32_t *csc_pos, int64_t num_edges, int32_t *csc_perm, void *stream);
 size_t maxk_local_plan_workspace_bytes(int64_t num_edges, int num_cols, int target_waves);
 int maxk_local_plan_build(const int32_t *indptr, const int32_t *indices, const float *values,
                           int num_rows, int num_cols, int64_t num_edges,
@@ -231,6 +233,11 @@ int maxk_spgemm_forward_multi(const int32_t *sched, int64_t num_panels, const in
 #define MAXK_BWD_STAGED_EDGE 5 /* STAGED reading EDGE selectors: cbsr_sel is uint8[num_edges,
                                   dim_k] in CSR edge order (maxk_spgemm_forward_esel's edge_sel)
                                   instead of the node CBSR selectors; workspace as STAGED */
+#define MAXK_BWD_EDGE_GATHER 6 /* as STAGED_EDGE, but the per-edge products are written in edge
+                                  (CSR) order -- one sequential stream -- and the segmented sum
+                                  gathers them per destination: csc_pos is then the CSC slot ->
+                                  CSR edge permutation (maxk_csc_perm_build); k a power of
+                                  two in [4, 256] */
 size_t maxk_backward_workspace_bytes(int algo, int64_t num_edges, int dim_k,
                                      int64_t csc_num_panels);
 int maxk_sspmm_backward(int algo, const int32_t *sched, int64_t num_panels,

@@ -29,6 +29,7 @@ MAXK_BWD_STAGED = 2
 MAXK_BWD_LOCAL = 3
 MAXK_BWD_TILE = 4
 MAXK_BWD_STAGED_EDGE = 5
+MAXK_BWD_EDGE_GATHER = 6
 MAXK_TOPK_ORDER_COLUMN = 0
 MAXK_TOPK_ORDER_VALUE = 1
 MAXK_TOPK_ORDER_LANE = 2
@@ -76,6 +77,7 @@ SIGNATURES = {
     "maxk_spgemm_forward_packed": (_I, [_P, _L, _P, _P, _P, _P, _I, _I, _I, _P, _P, _S, _P]),
     "maxk_csc_workspace_bytes": (_S, [_L, _I]),
     "maxk_csc_build": (_I, [_P, _L, _I, _P, _P, _P, _S, _P]),
+    "maxk_csc_perm_build": (_I, [_P, _L, _P, _P]),
     "maxk_local_plan_workspace_bytes": (_S, [_L, _I, _I]),
     "maxk_local_plan_build": (_I, [_P, _P, _P, _I, _I, _L, _P, _I, _I, _P, _P, _P, _P, _P, _P, _P,
                                    _S, _P]),

@@ -82,6 +82,13 @@ __global__ void scatter_rank_kernel(const int32_t *__restrict__ perm, int64_t n,
     if (i < n) pos[perm[i]] = (int32_t)i;
 }
 
+// inv[pos[i]] = i
+__global__ void invert_kernel(const int32_t *__restrict__ pos, int64_t n, int32_t *__restrict__ inv)
+{
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < n) inv[pos[i]] = (int32_t)i;
+}
+
 // out[c] = first i with sorted[i] >= c, c in [0, n_out)
 __global__ void lower_bounds_kernel(const int32_t *__restrict__ sorted, int64_t n,
                                     int32_t *__restrict__ out, int64_t n_out)
@@ -499,6 +506,15 @@ int maxk_csc_build(const int32_t *indices, int64_t num_edges, int num_cols, int3
     hipLaunchKernelGGL(lower_bounds_kernel, dim3((unsigned)blocks_for((int64_t)num_cols + 1)),
                        dim3(kThreads), 0, st, keys_sorted, num_edges, csc_indptr,
                        (int64_t)num_cols + 1);
+    return launch_status();
+}
+
+int maxk_csc_perm_build(const int32_t *csc_pos, int64_t num_edges, int32_t *csc_perm, void *stream)
+{
+    if (num_edges < 0 || (num_edges > 0 && (!csc_pos || !csc_perm))) return MAXK_E_ARG;
+    if (num_edges == 0) return MAXK_OK;
+    hipLaunchKernelGGL(invert_kernel, dim3((unsigned)blocks_for(num_edges)), dim3(kThreads), 0,
+                       static_cast<hipStream_t>(stream), csc_pos, num_edges, csc_perm);
     return launch_status();
 }
 

@@ -1137,7 +1137,9 @@ struct PRow {
     static constexpr int KP = K == 8 ? 16 : K;
 };
 
-template <int K, bool ESEL = false>
+// CSRP: P rows in edge (CSR) order -- P[e] -- written as one sequential stream
+// (unpadded; the EDGE_GATHER segmented sum gathers them per destination).
+template <int K, bool ESEL = false, bool CSRP = false>
 __device__ __forceinline__ void bwd_edges_stage_vec(int e0, int e1,
                                                     const int32_t *__restrict__ idx,
                                                     const float *__restrict__ val,
@@ -1145,7 +1147,7 @@ __device__ __forceinline__ void bwd_edges_stage_vec(int e0, int e1,
                                                     const uint8_t *__restrict__ sel,
                                                     const float *gs, float *__restrict__ P)
 {
-    constexpr int KP = PRow<K>::KP;
+    constexpr int KP = CSRP ? K : PRow<K>::KP;
     constexpr int LPE = KP / 4;
     constexpr int EPS = kWave / LPE;
     constexpr int STEPS = kWave / EPS;
@@ -1160,7 +1162,7 @@ __device__ __forceinline__ void bwd_edges_stage_vec(int e0, int e1,
         if (lane < n) {
             my_c = __builtin_nontemporal_load(idx + base + lane);
             my_v = __builtin_nontemporal_load(val + base + lane);
-            my_p = __builtin_nontemporal_load(csc_pos + base + lane);
+            my_p = CSRP ? base + lane : __builtin_nontemporal_load(csc_pos + base + lane);
         }
 #pragma unroll
         for (int s0 = 0; s0 < STEPS; s0 += U) {
@@ -1214,7 +1216,7 @@ __device__ __forceinline__ void bwd_edges_stage_scalar(int e0, int e1, int k,
 }
 
 // Panel-scheduled backward push (ATOMIC when P == nullptr, STAGED otherwise).
-template <int K, bool STAGED, bool ESEL = false>
+template <int K, bool STAGED, bool ESEL = false, bool CSRP = false>
 __global__ __launch_bounds__(kBlock) void bwd_panel_kernel(
     const int2 *__restrict__ sched, int64_t num_panels, const int32_t *__restrict__ indptr,
     const int32_t *__restrict__ idx, const float *__restrict__ val,
@@ -1238,7 +1240,7 @@ __global__ __launch_bounds__(kBlock) void bwd_panel_kernel(
         stage_row(gs, grad + (size_t)r * dim, dim);
         if constexpr (STAGED) {
             if constexpr (K > 0)
-                bwd_edges_stage_vec<K, ESEL>(eb, ee, idx, val, csc_pos, sel, gs, P);
+                bwd_edges_stage_vec<K, ESEL, CSRP>(eb, ee, idx, val, csc_pos, sel, gs, P);
             else
                 bwd_edges_stage_scalar(eb, ee, k, idx, val, csc_pos, sel, gs, P, ESEL);
         } else {
@@ -1253,32 +1255,40 @@ __global__ __launch_bounds__(kBlock) void bwd_panel_kernel(
 // STAGED phase 2: dxs[c, :] = sum of P rows [csc_indptr[c], csc_indptr[c+1]),
 // merge-path panels over the CSC ranges, register accumulation + cross-slot
 // reduction; split destinations go through the carry fixup.
-template <int K>
-__device__ __forceinline__ f4 seg_sum_vec(int q0, int q1, const float *__restrict__ P)
+// GATHER: CSC slot q's row is P[perm[q]] (P in edge order, unpadded) instead of P[q].
+template <int K, bool GATHER = false>
+__device__ __forceinline__ f4 seg_sum_vec(int q0, int q1, const float *__restrict__ P,
+                                          const int32_t *__restrict__ perm = nullptr)
 {
     constexpr int LPE = K / 4;
     constexpr int EPS = kWave / LPE;
     const int lane = lane_id();
     const int sub = lane % LPE;
     const int slot = lane / LPE;
-    constexpr int KP = PRow<K>::KP;  // P row stride
+    constexpr int KP = GATHER ? K : PRow<K>::KP;  // P row stride
     f4 s = f4{0.f, 0.f, 0.f, 0.f};
     constexpr int U = 4;
     int q = q0 + slot;
     for (; q + (U - 1) * EPS < q1; q += U * EPS) {
         f4 t[U];
+        size_t row[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u)
+            row[u] = GATHER ? (size_t)__builtin_nontemporal_load(perm + q + u * EPS)
+                            : (size_t)(q + u * EPS);
 #pragma unroll
         for (int u = 0; u < U; ++u)
             t[u] = __builtin_nontemporal_load(
-                reinterpret_cast<const f4 *>(P + (size_t)(q + u * EPS) * KP + sub * 4));
+                reinterpret_cast<const f4 *>(P + row[u] * KP + sub * 4));
 #pragma unroll
         for (int u = 0; u < U; ++u) {
             s.x += t[u].x; s.y += t[u].y; s.z += t[u].z; s.w += t[u].w;
         }
     }
     for (; q < q1; q += EPS) {
+        const size_t row = GATHER ? (size_t)perm[q] : (size_t)q;
         const f4 t = __builtin_nontemporal_load(
-            reinterpret_cast<const f4 *>(P + (size_t)q * KP + sub * 4));
+            reinterpret_cast<const f4 *>(P + row * KP + sub * 4));
         s.x += t.x; s.y += t.y; s.z += t.z; s.w += t.w;
     }
 #pragma unroll
@@ -1291,11 +1301,12 @@ __device__ __forceinline__ f4 seg_sum_vec(int q0, int q1, const float *__restric
     return s;  // every slot holds the total for its sub
 }
 
-template <int K>
+template <int K, bool GATHER = false>
 __global__ __launch_bounds__(kBlock) void bwd_segsum_kernel(
     const int2 *__restrict__ sched, int64_t num_panels, const int32_t *__restrict__ cptr,
     const float *__restrict__ P, int num_rows, int k, float *__restrict__ dxs,
-    float *__restrict__ carry, int32_t *__restrict__ carry_row)
+    float *__restrict__ carry, int32_t *__restrict__ carry_row,
+    const int32_t *__restrict__ perm = nullptr)
 {
     const int64_t w = (int64_t)blockIdx.x * kWavesPerBlock + threadIdx.x / kWave;
     if (w >= num_panels) return;
@@ -1309,7 +1320,7 @@ __global__ __launch_bounds__(kBlock) void bwd_segsum_kernel(
         const bool writer = lane < LPE;
         for (int c = i0; c < i1; ++c) {
             const int ce = cptr[c + 1];
-            const f4 s = seg_sum_vec<K>(e, ce, P);
+            const f4 s = seg_sum_vec<K, GATHER>(e, ce, P, perm);
             if (writer) reinterpret_cast<f4 *>(dxs + (size_t)c * K)[sub] = s;
             e = ce;
         }
@@ -1318,7 +1329,7 @@ __global__ __launch_bounds__(kBlock) void bwd_segsum_kernel(
         if (i1 < num_rows) {
             const int eb = e > cptr[i1] ? e : cptr[i1];
             if (eb < j1) {
-                s = seg_sum_vec<K>(eb, j1, P);
+                s = seg_sum_vec<K, GATHER>(eb, j1, P, perm);
                 has = 1;
             }
         }
@@ -2729,9 +2740,20 @@ struct BwdPanel {
     static int run(bool staged, const int32_t *sched, int64_t P, const int32_t *indptr,
                    const int32_t *idx, const float *val, const float *grad, const uint8_t *sel,
                    const int32_t *csc_pos, int V, int dim, int k, float *dxs, float *Pbuf,
-                   hipStream_t st, bool esel = false)
+                   hipStream_t st, bool esel = false, bool csrp = false)
     {
         const int64_t blocks = ceil_div(P, kWavesPerBlock);
+        if (csrp) {  // EDGE_GATHER phase 1 (edge selectors, P in edge order)
+            if constexpr (K == 0) {
+                return MAXK_E_DIM;
+            } else {
+                hipLaunchKernelGGL((bwd_panel_kernel<K, true, true, true>), dim3((unsigned)blocks),
+                                   dim3(kBlock), row_lds_bytes(), st,
+                                   reinterpret_cast<const int2 *>(sched), P, indptr, idx, val,
+                                   grad, sel, csc_pos, V, dim, k, dxs, Pbuf);
+                return launch_status();
+            }
+        }
         if (staged && esel)
             hipLaunchKernelGGL((bwd_panel_kernel<K, true, true>), dim3((unsigned)blocks),
                                dim3(kBlock), row_lds_bytes(), st,
@@ -2752,12 +2774,23 @@ struct BwdPanel {
 template <int K>
 struct BwdSegsum {
     static int run(const int32_t *csched, int64_t CP, const int32_t *cptr, const float *Pbuf,
-                   int V, int k, float *dxs, float *carry, int32_t *carry_row, hipStream_t st)
+                   int V, int k, float *dxs, float *carry, int32_t *carry_row, hipStream_t st,
+                   const int32_t *perm = nullptr)
     {
         const int64_t blocks = ceil_div(CP, kWavesPerBlock);
-        hipLaunchKernelGGL(bwd_segsum_kernel<K>, dim3((unsigned)blocks), dim3(kBlock), 0, st,
-                           reinterpret_cast<const int2 *>(csched), CP, cptr, Pbuf, V, k, dxs,
-                           carry, carry_row);
+        if (perm) {
+            if constexpr (K == 0) {
+                return MAXK_E_DIM;
+            } else {
+                hipLaunchKernelGGL((bwd_segsum_kernel<K, true>), dim3((unsigned)blocks),
+                                   dim3(kBlock), 0, st, reinterpret_cast<const int2 *>(csched), CP,
+                                   cptr, Pbuf, V, k, dxs, carry, carry_row, perm);
+            }
+        } else {
+            hipLaunchKernelGGL(bwd_segsum_kernel<K>, dim3((unsigned)blocks), dim3(kBlock), 0, st,
+                               reinterpret_cast<const int2 *>(csched), CP, cptr, Pbuf, V, k, dxs,
+                               carry, carry_row, (const int32_t *)nullptr);
+        }
         int rc = launch_status();
         if (rc) return rc;
         hipLaunchKernelGGL(carry_fixup_kernel, dim3((unsigned)blocks), dim3(kBlock), 0, st, CP,
@@ -3091,7 +3124,8 @@ size_t maxk_backward_workspace_bytes(int algo, int64_t num_edges, int dim_k,
                                      int64_t csc_num_panels)
 {
     if (algo == MAXK_BWD_ATOMIC) return 0;  // STAGED_EDGE: as STAGED
-    const int kp = dim_k == 8 ? 16 : dim_k;  // P rows padded to 64 B at k = 8 (PRow)
+    // P rows padded to 64 B at k = 8 (PRow) when scattered; EDGE_GATHER writes them in order
+    const int kp = dim_k == 8 && algo != MAXK_BWD_EDGE_GATHER ? 16 : dim_k;
     return align_up((size_t)num_edges * kp * sizeof(float), 256) +
            align_up((size_t)csc_num_panels * dim_k * sizeof(float), 256) +
            align_up((size_t)csc_num_panels * sizeof(int32_t), 256);
@@ -3117,7 +3151,11 @@ int maxk_sspmm_backward(int algo, const int32_t *sched, int64_t num_panels,
     const bool staged_ready = csc_pos && csc_sched && csc_indptr && csc_num_panels >= 1 &&
                               workspace;
     if (algo == MAXK_BWD_AUTO) algo = staged_ready ? MAXK_BWD_STAGED : MAXK_BWD_ATOMIC;
-    const bool esel = algo == MAXK_BWD_STAGED_EDGE;  // cbsr_sel = edge selectors uint8[E, k]
+    // STAGED_EDGE / EDGE_GATHER: cbsr_sel = edge selectors uint8[E, k];
+    // EDGE_GATHER: csc_pos = the CSC slot -> CSR edge permutation (maxk_csc_perm_build)
+    const bool gather = algo == MAXK_BWD_EDGE_GATHER;
+    const bool esel = algo == MAXK_BWD_STAGED_EDGE || gather;
+    const int ws_algo = algo;
     if (esel) algo = MAXK_BWD_STAGED;
     if (algo == MAXK_BWD_ATOMIC) {
         const int e = zero_floats(dxs, (size_t)num_cols * dim_k, st);
@@ -3128,9 +3166,9 @@ int maxk_sspmm_backward(int algo, const int32_t *sched, int64_t num_panels,
     }
     if (algo != MAXK_BWD_STAGED || !staged_ready) return MAXK_E_ARG;
     // workspace: [P rows (E*kp floats)] [carry (CP*k floats)] [carry_row (CP ints)]
-    if (workspace_bytes < maxk_backward_workspace_bytes(algo, num_edges, dim_k, csc_num_panels))
+    if (workspace_bytes < maxk_backward_workspace_bytes(ws_algo, num_edges, dim_k, csc_num_panels))
         return MAXK_E_WORKSPACE;
-    const int kp = dim_k == 8 ? 16 : dim_k;
+    const int kp = dim_k == 8 && !gather ? 16 : dim_k;
     const size_t pbytes = align_up((size_t)num_edges * kp * sizeof(float), 256);
     const size_t carry_bytes = align_up((size_t)csc_num_panels * dim_k * sizeof(float), 256);
     float *Pbuf = static_cast<float *>(workspace);
@@ -3139,10 +3177,11 @@ int maxk_sspmm_backward(int algo, const int32_t *sched, int64_t num_panels,
                                                      carry_bytes);
     int rc = dispatch_k<BwdPanel>(dim_k, true, sched, num_panels, indptr, indices, values, grad,
                                   cbsr_sel, csc_pos, num_rows, dim_origin, dim_k, dxs, Pbuf, st,
-                                  esel);
+                                  esel, gather);
     if (rc) return rc;
     return dispatch_k<BwdSegsum>(dim_k, csc_sched, csc_num_panels, csc_indptr, Pbuf, num_cols,
-                                 dim_k, dxs, carry, carry_row, st);
+                                 dim_k, dxs, carry, carry_row, st,
+                                 gather ? csc_pos : (const int32_t *)nullptr);
 }
 
 size_t maxk_backward_local_lds_bytes(int dmax, int dim_k)

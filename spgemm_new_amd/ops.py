@@ -124,6 +124,13 @@ def _validate_csr(indptr: torch.Tensor, indices: torch.Tensor, num_cols: int) ->
         raise RuntimeError(f"indices out of range: every column must be in [0, {num_cols})")
 
 
+_ESEL_ALGOS = (_lib.MAXK_BWD_STAGED_EDGE, _lib.MAXK_BWD_EDGE_GATHER)
+
+
+def _edge_gather_ok(k: int) -> bool:
+    return 4 <= k <= 256 and k & (k - 1) == 0
+
+
 def _min_ms(fn, reps: int | None = None) -> float:
     """fn's minimum time over a few calls (HIP events on the current stream),
     after one untimed call."""
@@ -234,6 +241,17 @@ class MaxKGraph:
             sched, P = _build_schedule(csc_indptr, C, E, self.csc_panel_cost, self.row_cost)
             self._csc = (csc_pos, csc_indptr, sched, P)
         return self._csc
+
+    def csc_perm(self) -> torch.Tensor:
+        """CSC slot -> CSR edge (the inverse of csc_pos; MAXK_BWD_EDGE_GATHER), once."""
+        if getattr(self, "_csc_perm", None) is None:
+            csc_pos = self.csc()[0]
+            perm = torch.empty(max(self.num_edges, 1), dtype=torch.int32, device=self.device)
+            _lib.check(_lib.load().maxk_csc_perm_build(csc_pos.data_ptr(), self.num_edges,
+                                                       perm.data_ptr(), _stream(perm)),
+                       "maxk_csc_perm_build")
+            self._csc_perm = perm
+        return self._csc_perm
 
     def local_plan(self, dim_k: int):
         """Plan of the LOCAL backward (maxk_sspmm_backward_local), or None when
@@ -448,14 +466,15 @@ class MaxKGraph:
             # forward writing the edge selectors only for STAGED_EDGE
             self.make_edge_selectors(sel)
             cands.append(_lib.MAXK_BWD_STAGED_EDGE)
+            if _edge_gather_ok(k):
+                cands.append(_lib.MAXK_BWD_EDGE_GATHER)
             dummy = self._workspace(("esel_data", k), self.num_cols * k * 4)
             dummy = dummy[: self.num_cols * k * 4].view(torch.float32).view(self.num_cols, k)
             yd = torch.empty((self.num_rows, grad.shape[1]), dtype=torch.float32,
                              device=self.device)
 
             def pair(a):
-                spgemm_forward(self, dummy, sel, grad.shape[1], out=yd,
-                               edge_sel=a == _lib.MAXK_BWD_STAGED_EDGE)
+                spgemm_forward(self, dummy, sel, grad.shape[1], out=yd, edge_sel=a in _ESEL_ALGOS)
                 sspmm_backward(self, grad, sel, out, values, a)
         best, best_ms, alt, alt_ms = None, float("inf"), None, float("inf")
         for a in cands:
@@ -463,13 +482,13 @@ class MaxKGraph:
                 ms = _min_ms(lambda: pair(a))
             else:
                 ms = _min_ms(lambda: sspmm_backward(self, grad, sel, out, values, a))
-            if a != _lib.MAXK_BWD_STAGED_EDGE and ms < alt_ms:
+            if a not in _ESEL_ALGOS and ms < alt_ms:
                 alt, alt_ms = a, ms
             if ms < best_ms:
                 best, best_ms = a, ms
         self._bwd_choice[key] = best
         self._bwd_alt[key] = alt
-        if best == _lib.MAXK_BWD_STAGED_EDGE:
+        if best in _ESEL_ALGOS:
             self._esel_on.add((k, grad.shape[1]))
         self.bwd_timings = getattr(self, "bwd_timings", {})
         self.bwd_timings[key] = best_ms
@@ -814,7 +833,7 @@ def sspmm_backward(g: MaxKGraph, grad, sel, out=None, values=None, algo: int = _
         _on_device(g, grad_input=out)
     if algo == _lib.MAXK_BWD_AUTO:
         algo = g.autotune_backward(grad, sel, out, values)
-        if algo == _lib.MAXK_BWD_STAGED_EDGE and g.edge_selectors(sel) is None:
+        if algo in _ESEL_ALGOS and g.edge_selectors(sel) is None:
             # this selector tensor went through no edge-selector forward: the best
             # of the others (never a second forward pass on the hot path)
             algo = g._bwd_alt.get((k, dim_origin, values is g.values), _lib.MAXK_BWD_STAGED)
@@ -853,14 +872,19 @@ def sspmm_backward(g: MaxKGraph, grad, sel, out=None, values=None, algo: int = _
     CP = 0
     ws = None
     sel_arg = sel
-    if algo == _lib.MAXK_BWD_STAGED_EDGE:
+    if algo == _lib.MAXK_BWD_EDGE_GATHER and not _edge_gather_ok(k):
+        raise RuntimeError("EDGE_GATHER backward needs k a power of two in [4, 256]")
+    if algo in _ESEL_ALGOS:
         sel_arg = g.make_edge_selectors(sel)   # written by this sel's forward (else made here)
-    if algo in (_lib.MAXK_BWD_STAGED, _lib.MAXK_BWD_STAGED_EDGE):
+    if algo in (_lib.MAXK_BWD_STAGED,) + _ESEL_ALGOS:
         csc_pos, csc_indptr, csc_sched, CP = g.csc()
+        if algo == _lib.MAXK_BWD_EDGE_GATHER:
+            csc_pos = g.csc_perm()
         nbytes = L.maxk_backward_workspace_bytes(algo, g.num_edges, k, CP)
         ws = g._workspace(("bwd", k), nbytes)
     g.last_bwd_algo = {_lib.MAXK_BWD_ATOMIC: "atomic", _lib.MAXK_BWD_STAGED: "staged",
-                       _lib.MAXK_BWD_STAGED_EDGE: "staged_edge"}[algo]
+                       _lib.MAXK_BWD_STAGED_EDGE: "staged_edge",
+                       _lib.MAXK_BWD_EDGE_GATHER: "edge_gather"}[algo]
     _lib.check(L.maxk_sspmm_backward(
         algo, g.bwd_sched.data_ptr(), g.bwd_num_panels, g.indptr.data_ptr(), g.indices.data_ptr(),
         values.data_ptr(), grad.data_ptr(), sel_arg.data_ptr(), g.num_rows, g.num_cols, g.num_edges,

@@ -932,8 +932,9 @@ def test_auto_under_capture_keeps_tile(dev, g_small):
 def test_edge_selector_forward_and_staged_edge(dev, oracle, g_small, k):
     """maxk_spgemm_forward_esel: the same Y as the plain forward (packed records
     at k = 4/8/16, generic k = 5) plus edge_sel[e] = sel[indices[e]]; the
-    STAGED_EDGE backward reading them equals STAGED bit for bit (same products
-    and sums, only the selector source differs) and the oracle."""
+    STAGED_EDGE and EDGE_GATHER backwards reading them equal STAGED bit for bit
+    (same products and sums, only where selectors and products are stored
+    differs) and the oracle."""
     indptr, indices, values = g_small
     v, h = len(indptr) - 1, 256
     data, sel = random_cbsr(v, k, h, seed=k + 1)
@@ -954,6 +955,10 @@ def test_edge_selector_forward_and_staged_edge(dev, oracle, g_small, k):
     assert torch.equal(a, b)
     ref = oracle.np_backward(indptr, indices, values, grad.cpu().numpy(), sel)
     assert oracle.parity_error(a.cpu().numpy(), ref) <= TOL
+    if k & (k - 1) == 0:
+        # EDGE_GATHER: the same products in edge order, summed in the same CSC order
+        c = g.backward(grad, s, algo=_lib.MAXK_BWD_EDGE_GATHER)
+        assert g.last_bwd_algo == "edge_gather" and torch.equal(c, b)
 
 
 def test_staged_edge_auto_flow(dev, g_small):

@@ -32,7 +32,8 @@ for k in [int(a) for a in sys.argv[2:]] or (8, 16, 32):
         fw.append(f"{f0:.3f}/{f1:.3f}")
     res = {}
     for name, a in (("atomic", _lib.MAXK_BWD_ATOMIC), ("staged", _lib.MAXK_BWD_STAGED),
-                    ("staged_edge", _lib.MAXK_BWD_STAGED_EDGE)):
+                    ("staged_edge", _lib.MAXK_BWD_STAGED_EDGE),
+                    ("edge_gather", _lib.MAXK_BWD_EDGE_GATHER)):
         res[name] = ops._min_ms(lambda: g.backward(G, sel, out=dx, algo=a), 5)
     print(f"{graph} k={k}: fwd plain/esel {' '.join(fw)} | " +
           " ".join(f"{n} {t:.3f}" for n, t in res.items()), flush=True)
