@@ -103,12 +103,13 @@ int oracle_spmm_forward(const int32_t *warp4, long long num_warps,
     return 0;
 }
 
-/* spmm_maxk_backward.cu:15-115 (intended math).  dxs must be pre-zeroed
+/* spmm_maxk_backward.cu:15-115 (intended math).  dxs (num_cols x dim_k: A may be a
+ * rectangular row block with halo columns) must be pre-zeroed
  * (cuda_kernel_bindings.cpp:128). */
 int oracle_spmm_backward(const int32_t *warp4, long long num_warps,
                          const int32_t *indices, const float *values,
                          const float *grad, const uint8_t *cbsr_sel,
-                         int num_rows, int dim_origin, int dim_k, float *dxs)
+                         int num_rows, int num_cols, int dim_origin, int dim_k, float *dxs)
 {
     for (long long w = 0; w < num_warps; ++w) {
         int row = warp4[4 * w + 0], loc = warp4[4 * w + 1], len = warp4[4 * w + 2];
@@ -116,6 +117,7 @@ int oracle_spmm_backward(const int32_t *warp4, long long num_warps,
         const float *g = grad + (size_t)row * dim_origin;       /* staged row, :52-57 */
         for (int i = 0; i < len; ++i) {                          /* :93-104 */
             int col = indices[loc + i];
+            if (col < 0 || col >= num_cols) return -4;
             float left = values[loc + i];
             const uint8_t *s = cbsr_sel + (size_t)col * dim_k;
             float *dx = dxs + (size_t)col * dim_k;
@@ -151,14 +153,15 @@ int oracle_spmm_forward_csr(const int32_t *indptr, const int32_t *indices,
 
 int oracle_spmm_backward_csr(const int32_t *indptr, const int32_t *indices,
                              const float *values, const float *grad,
-                             const uint8_t *cbsr_sel, int num_rows, int dim_origin,
-                             int dim_k, float *dxs)
+                             const uint8_t *cbsr_sel, int num_rows, int num_cols,
+                             int dim_origin, int dim_k, float *dxs)
 {
-    memset(dxs, 0, sizeof(float) * (size_t)num_rows * dim_k);
+    memset(dxs, 0, sizeof(float) * (size_t)num_cols * dim_k);
     for (int r = 0; r < num_rows; ++r) {
         const float *g = grad + (size_t)r * dim_origin;
         for (int e = indptr[r]; e < indptr[r + 1]; ++e) {
             int col = indices[e];
+            if (col < 0 || col >= num_cols) return -4;
             float left = values[e];
             const uint8_t *s = cbsr_sel + (size_t)col * dim_k;
             float *dx = dxs + (size_t)col * dim_k;

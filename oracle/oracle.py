@@ -49,15 +49,15 @@ def lib():
         L.oracle_warp4_count.argtypes = [P, ctypes.c_int, ctypes.c_int]
         L.oracle_warp4_fill.restype = ctypes.c_longlong
         L.oracle_warp4_fill.argtypes = [P, ctypes.c_int, ctypes.c_int, P]
-        for name in ("oracle_spmm_forward", "oracle_spmm_backward"):
-            f = getattr(L, name)
-            f.restype = ctypes.c_int
-            f.argtypes = [P, ctypes.c_longlong, P, P, P, P, ctypes.c_int, ctypes.c_int,
-                          ctypes.c_int, P]
-        for name in ("oracle_spmm_forward_csr", "oracle_spmm_backward_csr"):
-            f = getattr(L, name)
-            f.restype = ctypes.c_int
-            f.argtypes = [P, P, P, P, P, ctypes.c_int, ctypes.c_int, ctypes.c_int, P]
+        I = ctypes.c_int
+        L.oracle_spmm_forward.restype = I
+        L.oracle_spmm_forward.argtypes = [P, ctypes.c_longlong, P, P, P, P, I, I, I, P]
+        L.oracle_spmm_backward.restype = I   # rows, cols (a rectangular block), dim, k
+        L.oracle_spmm_backward.argtypes = [P, ctypes.c_longlong, P, P, P, P, I, I, I, I, P]
+        L.oracle_spmm_forward_csr.restype = I
+        L.oracle_spmm_forward_csr.argtypes = [P, P, P, P, P, I, I, I, P]
+        L.oracle_spmm_backward_csr.restype = I
+        L.oracle_spmm_backward_csr.argtypes = [P, P, P, P, P, I, I, I, I, P]
         L.oracle_main_inputs.restype = ctypes.c_int
         L.oracle_main_inputs.argtypes = [ctypes.c_int, ctypes.c_longlong, ctypes.c_int,
                                          P, P, P, P]
@@ -105,11 +105,11 @@ def c_backward(warp4, indices, values, grad, sel) -> np.ndarray:
     grad = np.ascontiguousarray(grad, dtype=np.float32)
     sel = np.ascontiguousarray(sel, dtype=np.uint8)
     v, h = grad.shape
-    k = sel.shape[1]
-    out = np.zeros((v, k), dtype=np.float32)
+    c, k = sel.shape          # dXs rows = A's columns (a rank's block has halo columns)
+    out = np.zeros((c, k), dtype=np.float32)
     rc = lib().oracle_spmm_backward(_p(warp4), len(warp4), _p(np.ascontiguousarray(indices, np.int32)),
                                     _p(np.ascontiguousarray(values, np.float32)), _p(grad), _p(sel),
-                                    v, h, k, _p(out))
+                                    v, c, h, k, _p(out))
     if rc != 0:
         raise ValueError(f"oracle_spmm_backward failed ({rc})")
     return out
@@ -131,12 +131,14 @@ def c_backward_csr(indptr, indices, values, grad, sel) -> np.ndarray:
     grad = np.ascontiguousarray(grad, dtype=np.float32)
     sel = np.ascontiguousarray(sel, dtype=np.uint8)
     v, h = grad.shape
-    k = sel.shape[1]
-    out = np.empty((v, k), dtype=np.float32)
-    lib().oracle_spmm_backward_csr(_p(np.ascontiguousarray(indptr, np.int32)),
-                                   _p(np.ascontiguousarray(indices, np.int32)),
-                                   _p(np.ascontiguousarray(values, np.float32)), _p(grad), _p(sel),
-                                   v, h, k, _p(out))
+    c, k = sel.shape          # dXs rows = A's columns
+    out = np.empty((c, k), dtype=np.float32)
+    rc = lib().oracle_spmm_backward_csr(_p(np.ascontiguousarray(indptr, np.int32)),
+                                        _p(np.ascontiguousarray(indices, np.int32)),
+                                        _p(np.ascontiguousarray(values, np.float32)), _p(grad),
+                                        _p(sel), v, c, h, k, _p(out))
+    if rc != 0:
+        raise ValueError(f"oracle_spmm_backward_csr failed ({rc})")
     return out
 
 

@@ -71,6 +71,10 @@ MIN_PANELS = int(os.environ.get("MAXK_MIN_PANELS", 16384))
 TILE_AUTO = os.environ.get("MAXK_TILE", "1") != "0"
 # STAGED_EDGE backward (edge selectors written by the forward) among the AUTO candidates
 ESEL_AUTO = os.environ.get("MAXK_ESEL", "1") != "0"
+# AUTO backward: "measure" (time the candidates once per graph and shape; the fastest
+# is kept) or "fixed" (a rule of the shape alone, no timing: the same algorithm -- and
+# so the same fp32 summation order -- on every run and machine)
+AUTO_MODE = os.environ.get("MAXK_AUTO", "measure")
 # edge-selector buffers kept per graph (one per live selector tensor: a forward
 # per layer before the backwards)
 ESEL_CACHE = int(os.environ.get("MAXK_ESEL_CACHE", 4))
@@ -423,6 +427,16 @@ class MaxKGraph:
             buf = self.edge_selectors(sel)
         return buf
 
+    def _fixed_choice(self, k: int, h: int, own: bool) -> int:
+        """MAXK_AUTO=fixed: TILE when its plan serves the shape and the graph's own
+        values; else LOCAL when the gradient fits a few source bands; else STAGED
+        (what measurement picks on the BASELINE shapes, minus the ties)."""
+        if own and TILE_AUTO and tile_shape_ok(k, h) and self.tile_plan(k) is not None:
+            return _lib.MAXK_BWD_TILE
+        if self.num_rows * h * 4 <= 8 * LOCAL_BAND_BYTES and self.local_plan(k) is not None:
+            return _lib.MAXK_BWD_LOCAL
+        return _lib.MAXK_BWD_STAGED
+
     def autotune_backward(self, grad, sel, out, values=None) -> int:
         """MAXK_BWD_AUTO: the fastest algorithm for this graph and k, measured once
         (each candidate run once, then timed AUTOTUNE_REPS times with HIP events on
@@ -443,6 +457,10 @@ class MaxKGraph:
         tile_ok = TILE_AUTO and tile_shape_ok(k, grad.shape[1])
         if self.num_edges == 0:
             return _lib.MAXK_BWD_STAGED
+        if AUTO_MODE == "fixed":
+            choice = self._fixed_choice(k, grad.shape[1], own)
+            self._bwd_choice[key] = choice
+            return choice
         if torch.cuda.is_current_stream_capturing():
             # nothing can be timed (or planned) while a graph is captured: the
             # choice measured for the same shape with the graph's own values,

@@ -985,3 +985,22 @@ def test_staged_edge_auto_flow(dev, g_small):
     assert torch.equal(a, ref)
     assert (b - ref).abs().max().item() <= 1e-4 * max(1.0, ref.abs().max().item())
     assert ops.ESEL_CACHE >= 1
+
+
+def test_auto_fixed_mode_is_deterministic(dev, g_small, monkeypatch):
+    """MAXK_AUTO=fixed: AUTO picks by the shape alone (no timing), the same
+    algorithm on every graph object, and the results are bitwise repeatable."""
+    from spgemm_new_amd import ops
+    monkeypatch.setattr(ops, "AUTO_MODE", "fixed")
+    monkeypatch.setattr(ops, "_min_ms", lambda *a, **k: (_ for _ in ()).throw(AssertionError("timed")))
+    indptr, indices, values = g_small
+    v, h = len(indptr) - 1, 256
+    outs, algos = [], []
+    for _ in range(2):
+        g = S.MaxKGraph(T(indptr, dev), T(indices, dev), T(values, dev))
+        data, sel = random_cbsr(v, 32, h, seed=3)
+        grad = T(np.random.default_rng(5).random((v, h), dtype=np.float32), dev)
+        outs.append(g.backward(grad, T(sel, dev)))
+        algos.append(g.last_bwd_algo)
+    assert algos[0] == algos[1] == "tile"
+    assert torch.equal(outs[0], outs[1])

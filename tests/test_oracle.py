@@ -96,3 +96,25 @@ def test_main_inputs_generator(oracle):
     v16 = oracle.c_main_inputs(v, e, 16)
     np.testing.assert_array_equal(v16[0], values)           # same edge values
     assert not np.array_equal(v16[2][:, :16], sel[:, :16])  # k=32 drawn after k=16
+
+
+def test_c_backward_rectangular_block(oracle):
+    """The C restatements size dXs by A's columns: a row block with halo
+    columns (num_cols > num_rows) agrees with the numpy oracle."""
+    from spgemm_new_amd.graphs import random_cbsr
+    rng = np.random.default_rng(3)
+    rows, cols, h, k = 150, 420, 64, 8
+    deg = rng.integers(0, 30, rows)
+    indptr = np.zeros(rows + 1, np.int32)
+    indptr[1:] = np.cumsum(deg)
+    indices = np.concatenate([np.sort(rng.choice(cols, d, replace=False)) for d in deg]).astype(np.int32)
+    values = rng.random(indices.size, dtype=np.float32)
+    _, sel = random_cbsr(cols, k, h, seed=4)
+    grad = rng.random((rows, h), dtype=np.float32)
+    ref = oracle.np_backward(indptr, indices, values, grad, sel)
+    assert ref.shape == (cols, k)
+    got = oracle.c_backward_csr(indptr, indices, values, grad, sel)
+    assert got.shape == (cols, k) and oracle.parity_error(got, ref) <= 1e-5
+    w4 = oracle.c_warp4(indptr)
+    got4 = oracle.c_backward(w4, indices, values, grad, sel)
+    assert got4.shape == (cols, k) and oracle.parity_error(got4, ref) <= 1e-5
