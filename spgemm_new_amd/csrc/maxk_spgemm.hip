@@ -2321,7 +2321,7 @@ __global__ __launch_bounds__(kTileWaves * kWave) void bwd_tile_kernel(
 #define TILE_PF_AHEAD 128  // dwords: the window starts 512 B past the chunk's records
 #endif
 #ifndef TILE_ABLATE
-#define TILE_ABLATE 0  // development timing ablations (results wrong): 1 / 2 above
+#define TILE_ABLATE 0  // development timing ablations (results wrong): bits 1 / 2 / 4 / 8 below
 #endif
     // the window must stay inside the record stream's padding: 512 records =
     // 1024 dwords after the last wave's stream (kTileRecPad in maxk_plan.hip)
@@ -2380,7 +2380,13 @@ __global__ __launch_bounds__(kTileWaves * kWave) void bwd_tile_kernel(
             gb[i] = pb[i];
         }
         tile_groups2(ga, n, m, lo, hi, selv, acc0, acc1);
+#if TILE_ABLATE & 8  // timing ablation: the first two record groups only
+        n = 0u;
+#endif
         tile_groups2(gb, n, m, lo, hi, selv, acc0, acc1);
+#if TILE_ABLATE & 4  // timing ablation: the four record groups loaded before the barrier only
+        n = 0u;
+#endif
         tile_group_loop(rb, ro + 128, n, m, lo, hi, selv, acc0, acc1);
         ro += 32 * gn;
     };
