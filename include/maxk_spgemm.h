@@ -47,6 +47,10 @@ extern "C" {
  * MAXK_DEFAULT_PANEL_COST. */
 #define MAXK_DEFAULT_PANEL_COST 2048
 #define MAXK_FWD_ACCUMULATE 1  /* forward flag: out += A . X^ instead of out = A . X^ */
+/* forward flag: gather the CBSR data rows with cacheable loads (default:
+ * non-temporal).  For a column-blocked call, whose block-major edge order
+ * re-reads each source block from L2 (see maxk_rows_sum). */
+#define MAXK_FWD_CACHED_GATHER 2
 #define MAXK_DEFAULT_ROW_COST 16
 
 /* Library build identification (string, host memory, static). */
@@ -90,6 +94,16 @@ int maxk_spgemm_forward_ex(const int32_t *sched, int64_t num_panels, const int32
                            const uint8_t *cbsr_sel, int num_rows, int dim_origin, int dim_k,
                            int flags, float *out, void *workspace, size_t workspace_bytes,
                            void *stream);
+/* Column-blocked forward (no reference counterpart; same result up to fp32
+ * summation order): the caller restacks the CSR block-major -- row b*V + r
+ * holds row r's edges whose sources lie in column block b of NB -- runs
+ * maxk_spgemm_forward_ex(..., MAXK_FWD_CACHED_GATHER, ...) on it into
+ * partial fp32[NB][V][dim_origin], and sums the parts with maxk_rows_sum
+ * (spgemm_new_amd/ops.py, MaxKGraph.blocked_plan).  Pays 2 x NB partial rows
+ * per output row; wins where rows are long (Reddit: 3.29 -> 2.9 ms).
+ * out[i] = parts[0][i] + ... + parts[num_parts-1][i] (that order), n floats
+ * per part. */
+int maxk_rows_sum(const float *parts, int num_parts, int64_t n, float *out, void *stream);
 
 /* ---------------------------------------------------------------------------
  * Packed CBSR forward (k = 4, 8, 16).  maxk_cbsr_pack writes one record per

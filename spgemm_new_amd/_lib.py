@@ -34,6 +34,7 @@ MAXK_TOPK_ORDER_COLUMN = 0
 MAXK_TOPK_ORDER_VALUE = 1
 MAXK_TOPK_ORDER_LANE = 2
 MAXK_FWD_ACCUMULATE = 1
+MAXK_FWD_CACHED_GATHER = 2
 DEFAULT_PANEL_COST = 2048
 DEFAULT_ROW_COST = 16
 
@@ -64,6 +65,7 @@ SIGNATURES = {
     "maxk_sspmm_backward_tile": (_I, [_P, _P, _P, _P, _P, _I, _I, _I, _P, _P, _P, _I, _I, _I, _I,
                                       _P, _P, _P]),
     "maxk_tile_format": (_I, [ctypes.POINTER(_I), ctypes.POINTER(_I)]),
+    "maxk_rows_sum": (_I, [_P, _I, _L, _P, _P]),
     "maxk_tile_plan_shape": (_I, [_I, _I, _I, ctypes.POINTER(_I), ctypes.POINTER(_I),
                                   ctypes.POINTER(_I)]),
     "maxk_tile_plan_workspace_bytes": (_S, [_L, _I]),

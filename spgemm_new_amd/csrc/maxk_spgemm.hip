@@ -237,7 +237,7 @@ __device__ __forceinline__ uint32_t dpp_xor2(uint32_t v)
     return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x4E, 0xF, 0xF, false);
 }
 
-template <int K, int RS = 0, bool ESEL = false>
+template <int K, int RS = 0, bool ESEL = false, bool NTD = true>
 __device__ __forceinline__ void fwd_edges_vec(int e0, int e1, const int32_t *__restrict__ idx,
                                               const float *__restrict__ val,
                                               const float *__restrict__ data,
@@ -281,7 +281,12 @@ __device__ __forceinline__ void fwd_edges_vec(int e0, int e1, const int32_t *__r
                         const size_t off = (size_t)c * K + sub * VEC;
                         // data rows non-temporal (measured 3.45 -> 3.18 ms on Reddit k=32);
                         // selector words plain (nt 4-B loads measured slower)
-                        d[u] = __builtin_nontemporal_load(reinterpret_cast<const D *>(data + off));
+                        // (NTD false: cacheable, for the column-blocked forward whose
+                        // block-major sweep re-reads a block's rows from L2)
+                        if constexpr (NTD)
+                            d[u] = __builtin_nontemporal_load(reinterpret_cast<const D *>(data + off));
+                        else
+                            d[u] = *reinterpret_cast<const D *>(data + off);
                         sb[u] = *reinterpret_cast<const SB *>(sel + off);
                     } else {  // data = record base, sel = record base + 4K bytes
                         const size_t rec = (size_t)c * RS;
@@ -367,7 +372,7 @@ __device__ __forceinline__ void fwd_edges_scalar(int e0, int e1, int k,
     }
 }
 
-template <int K, int RS = 0, bool ESEL = false>
+template <int K, int RS = 0, bool ESEL = false, bool NTD = true>
 __device__ __forceinline__ void fwd_edges(int e0, int e1, int k, const int32_t *__restrict__ idx,
                                           const float *__restrict__ val,
                                           const float *__restrict__ data,
@@ -375,7 +380,7 @@ __device__ __forceinline__ void fwd_edges(int e0, int e1, int k, const int32_t *
                                           uint8_t *__restrict__ esel = nullptr)
 {
     if constexpr (K > 0)
-        fwd_edges_vec<K, RS, ESEL>(e0, e1, idx, val, data, sel, acc, esel);
+        fwd_edges_vec<K, RS, ESEL, NTD>(e0, e1, idx, val, data, sel, acc, esel);
     else
         fwd_edges_scalar(e0, e1, k, idx, val, data, sel, acc, ESEL ? esel : nullptr);
 }
@@ -435,7 +440,7 @@ __device__ __forceinline__ void zero_lds(float *acc, int n)
 
 // Panel-scheduled forward.  Rows [i0, i1) are finished and owned by this
 // wave (plain store); row i1 is in progress at the panel end -> carry.
-template <int K, int RS = 0, bool ACC = false, bool ESEL = false>
+template <int K, int RS = 0, bool ACC = false, bool ESEL = false, bool NTD = true>
 __global__ __launch_bounds__(kBlock) void fwd_panel_kernel(
     const int2 *__restrict__ sched, int64_t num_panels, const int32_t *__restrict__ indptr,
     const int32_t *__restrict__ idx, const float *__restrict__ val,
@@ -460,7 +465,7 @@ __global__ __launch_bounds__(kBlock) void fwd_panel_kernel(
     const bool split_first = i0 < i1 && j0 > indptr[i0];
     for (int r = i0; r < i1; ++r) {
         const int re = indptr[r + 1];
-        if (e < re) fwd_edges<K, RS, ESEL>(e, re, k, idx, val, data, sel, acc, esel);
+        if (e < re) fwd_edges<K, RS, ESEL, NTD>(e, re, k, idx, val, data, sel, acc, esel);
         if (r == i0 && split_first)
             flush_row<kStore>(acc, copies, owner + (size_t)w * dimp, dim);
         else
@@ -471,7 +476,7 @@ __global__ __launch_bounds__(kBlock) void fwd_panel_kernel(
     if (i1 < num_rows) {
         const int eb = e > indptr[i1] ? e : indptr[i1];
         if (eb < j1) {
-            fwd_edges<K, RS, ESEL>(eb, j1, k, idx, val, data, sel, acc, esel);
+            fwd_edges<K, RS, ESEL, NTD>(eb, j1, k, idx, val, data, sel, acc, esel);
             has_carry = 1;
         }
     }
@@ -2419,6 +2424,30 @@ __global__ __launch_bounds__(kBlock) void tile_combine_kernel(float *__restrict_
     }
 }
 
+// out = parts[0] + parts[1] + ... (in part order: deterministic), n floats
+// per part -- the column-blocked forward's partial outputs (maxk_rows_sum)
+template <bool VEC>
+__global__ __launch_bounds__(kBlock) void rows_sum_kernel(const float *__restrict__ parts,
+                                                          int nparts, int64_t n,
+                                                          float *__restrict__ out)
+{
+    const int64_t items = VEC ? n / 4 : n;
+    for (int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x; i < items;
+         i += (int64_t)gridDim.x * kBlock) {
+        if constexpr (VEC) {
+            const f4 *p = reinterpret_cast<const f4 *>(parts);
+            f4 a = __builtin_nontemporal_load(p + i);
+            for (int q = 1; q < nparts; ++q)
+                a += __builtin_nontemporal_load(p + (int64_t)q * (n / 4) + i);
+            __builtin_nontemporal_store(a, reinterpret_cast<f4 *>(out) + i);
+        } else {
+            float a = parts[i];
+            for (int q = 1; q < nparts; ++q) a += parts[(int64_t)q * n + i];
+            out[i] = a;
+        }
+    }
+}
+
 template <int K>
 __global__ __launch_bounds__(kBlock) void cbsr_pack_kernel(const float *__restrict__ data,
                                                            const uint8_t *__restrict__ sel,
@@ -2581,11 +2610,13 @@ struct FwdPanel {
     static int run(const int32_t *sched, int64_t P, const int32_t *indptr, const int32_t *idx,
                    const float *val, const float *data, const uint8_t *sel, int V, int dim, int k,
                    float *out, float *carry, int32_t *carry_row, float *owner, bool acc,
-                   hipStream_t st, uint8_t *esel = nullptr)
+                   hipStream_t st, uint8_t *esel = nullptr, bool cached = false)
     {
         const int64_t blocks = ceil_div(P, kWavesPerBlock);
         auto kern = esel ? fwd_panel_kernel<K, 0, false, true>
-                         : acc ? fwd_panel_kernel<K, 0, true> : fwd_panel_kernel<K, 0, false>;
+                    : cached ? (acc ? fwd_panel_kernel<K, 0, true, false, false>
+                                    : fwd_panel_kernel<K, 0, false, false, false>)
+                    : acc ? fwd_panel_kernel<K, 0, true> : fwd_panel_kernel<K, 0, false>;
         hipLaunchKernelGGL(kern, dim3((unsigned)blocks), dim3(kBlock), fwd_lds_bytes<K>(k), st,
                            reinterpret_cast<const int2 *>(sched), P, indptr, idx, val, data, sel,
                            V, dim, k, out, carry, carry_row, owner, esel);
@@ -2922,7 +2953,7 @@ int maxk_spgemm_forward_ex(const int32_t *sched, int64_t num_panels, const int32
                            int flags, float *out, void *workspace, size_t workspace_bytes,
                            void *stream)
 {
-    if (flags & ~MAXK_FWD_ACCUMULATE) return MAXK_E_ARG;
+    if (flags & ~(MAXK_FWD_ACCUMULATE | MAXK_FWD_CACHED_GATHER)) return MAXK_E_ARG;
     if (!sched || !indptr || !out || num_panels < 1 || num_rows < 0) return MAXK_E_ARG;
     if (!dims_ok(dim_origin, dim_k)) return MAXK_E_DIM;
     if (num_rows == 0) return MAXK_OK;
@@ -2936,7 +2967,26 @@ int maxk_spgemm_forward_ex(const int32_t *sched, int64_t num_panels, const int32
     return dispatch_k<FwdPanel>(dim_k, sched, num_panels, indptr, indices, values, cbsr_data,
                                 cbsr_sel, num_rows, dim_origin, dim_k, out, carry, carry_row,
                                 fwd_owner_slots(workspace, num_panels, dim_origin),
-                                (flags & MAXK_FWD_ACCUMULATE) != 0, as_stream(stream));
+                                (flags & MAXK_FWD_ACCUMULATE) != 0, as_stream(stream),
+                                (uint8_t *)nullptr, (flags & MAXK_FWD_CACHED_GATHER) != 0);
+}
+
+int maxk_rows_sum(const float *parts, int num_parts, int64_t n, float *out, void *stream)
+{
+    if (num_parts < 1 || n < 0 || (n > 0 && (!parts || !out))) return MAXK_E_ARG;
+    if (n == 0) return MAXK_OK;
+    hipStream_t st = as_stream(stream);
+    const bool vec = (n % 4) == 0 && ((uintptr_t)parts % 16) == 0 && ((uintptr_t)out % 16) == 0;
+    const int64_t items = vec ? n / 4 : n;
+    int64_t blocks = ceil_div(items, kBlock);
+    blocks = blocks < 65536 ? blocks : 65536;
+    if (vec)
+        hipLaunchKernelGGL(rows_sum_kernel<true>, dim3((unsigned)blocks), dim3(kBlock), 0, st, parts,
+                           num_parts, n, out);
+    else
+        hipLaunchKernelGGL(rows_sum_kernel<false>, dim3((unsigned)blocks), dim3(kBlock), 0, st,
+                           parts, num_parts, n, out);
+    return launch_status();
 }
 
 int maxk_spmm_dense_forward(const int32_t *sched, int64_t num_panels, const int32_t *indptr,

@@ -84,6 +84,12 @@ def tile_shape_ok(dim_k: int, dim_origin: int) -> bool:
     return dim_k in (32, 64) and dim_origin == 256
 # forward at k in {4, 8, 16}: pack CBSR into one record per node (MAXK_FWD_PACKED=0 disables)
 FWD_PACKED = os.environ.get("MAXK_FWD_PACKED", "1") != "0"
+# column-blocked forward (k >= 32): MAXK_FWD_BLOCKS = -1 (default) measures it against
+# the plain forward once per (k, h) on graphs whose mean degree reaches
+# FWD_BLOCKED_MIN_DEGREE; 0 never; n > 0 always, with n column blocks
+FWD_BLOCKS = int(os.environ.get("MAXK_FWD_BLOCKS", "-1"))
+FWD_BLOCKED_MIN_DEGREE = 128
+FWD_BLOCKED_CANDIDATES = (8,)
 # fused multi-relation forward: reorder CBSR entries against LDS store conflicts
 MULTI_BANK_ORDER = os.environ.get("MAXK_MULTI_BANK_ORDER", "1") != "0"
 
@@ -219,6 +225,8 @@ class MaxKGraph:
         self._esel_on = set()     # (k, h): forwards write edge selectors (AUTO chose STAGED_EDGE)
         self._esel = []           # [(sel key, sel, uint8 buffer[E * k])], most recent last
         self.last_bwd_algo = None
+        self._blocked = {}        # column-blocked forward plans, per block count
+        self._fwd_blocks = {}     # (k, h) -> block count chosen (0: plain forward)
 
     # ------------------------------------------------------------------ utils
     def _workspace(self, key, nbytes: int) -> torch.Tensor:
@@ -227,6 +235,46 @@ class MaxKGraph:
             t = torch.empty(max(nbytes, 1), dtype=torch.uint8, device=self.device)
             self._ws[key] = t
         return t
+
+    def blocked_plan(self, num_blocks: int) -> dict:
+        """The CSR restacked block-major for the column-blocked forward: row
+        b * V + r holds row r's edges whose source column lies in block b of
+        num_blocks (equal column ranges), in CSR order; built once.  The sweep
+        then reads one block's CBSR rows at a time, from L2 (include/maxk_spgemm.h,
+        maxk_rows_sum)."""
+        plan = self._blocked.get(num_blocks)
+        if plan is None:
+            V, C, nb = self.num_rows, self.num_cols, num_blocks
+            rows = torch.repeat_interleave(torch.arange(V, device=self.device),
+                                           (self.indptr[1:] - self.indptr[:-1]).long())
+            key = (self.indices.long() * nb) // C * V + rows
+            key, order = torch.sort(key, stable=True)
+            indptr = torch.zeros(nb * V + 1, dtype=torch.int32, device=self.device)
+            indptr[1:] = torch.cumsum(torch.bincount(key, minlength=nb * V), 0).to(torch.int32)
+            del key, rows
+            sched, P = _build_schedule(indptr, nb * V, self.num_edges, self.panel_cost,
+                                       self.row_cost)
+            plan = {"num_blocks": nb, "order": order, "indptr": indptr,
+                    "indices": self.indices[order].contiguous(), "sched": sched,
+                    "num_panels": P, "values": None, "values_key": None}
+            self._blocked[num_blocks] = plan
+        return plan
+
+    def _blocked_values(self, plan: dict, values: torch.Tensor) -> torch.Tensor:
+        """values in the plan's edge order: kept for the graph's own values
+        (refreshed when they change in place), gathered per call for others."""
+        if values is not self.values:
+            return values[plan["order"]]
+        key = _tensor_key(values)
+        if plan["values"] is None or plan["values_key"] != key:
+            if torch.cuda.is_current_stream_capturing() and plan["values"] is not None:
+                torch.index_select(values, 0, plan["order"], out=plan["values"])
+            else:
+                plan["values"] = values[plan["order"]].contiguous()
+            plan["values_key"] = key
+        elif torch.cuda.is_current_stream_capturing():
+            torch.index_select(values, 0, plan["order"], out=plan["values"])
+        return plan["values"]
 
     def csc(self):
         """(csc_pos, csc_indptr, csc_sched, csc_num_panels), built once on the
@@ -727,6 +775,10 @@ def spgemm_forward(g: MaxKGraph, data, sel, dim_origin: int = 256, out=None, val
             values.data_ptr(), rec.data_ptr(), g.num_rows, dim_origin, k, out.data_ptr(),
             ws.data_ptr(), ws.numel(), _stream(out)), "maxk_spgemm_forward_packed")
         return out
+    if not accumulate and k >= 32 and g.num_edges > 0:
+        nb = _fwd_blocks(g, data, sel, dim_origin, out, values)
+        if nb:
+            return _forward_blocked(g, nb, data, sel, dim_origin, out, values)
     flags = _lib.MAXK_FWD_ACCUMULATE if accumulate else 0
     _lib.check(L.maxk_spgemm_forward_ex(g.sched.data_ptr(), g.num_panels, g.indptr.data_ptr(),
                                         g.indices.data_ptr(), values.data_ptr(), data.data_ptr(),
@@ -734,6 +786,65 @@ def spgemm_forward(g: MaxKGraph, data, sel, dim_origin: int = 256, out=None, val
                                         out.data_ptr(), ws.data_ptr(), ws.numel(), _stream(out)),
                "maxk_spgemm_forward")
     return out
+
+
+def _forward_blocked(g: MaxKGraph, nb: int, data, sel, dim_origin: int, out, values):
+    """Column-blocked forward: the restacked CSR's forward into nb partial
+    outputs (cacheable gathers), then their sum in block order."""
+    L = _lib.load()
+    plan = g.blocked_plan(nb)
+    vals = g._blocked_values(plan, values)
+    P = plan["num_panels"]
+    ws = g._workspace(("fwd_blocked", nb, dim_origin), L.maxk_forward_workspace_bytes(P, dim_origin))
+    n = g.num_rows * dim_origin
+    parts = g._workspace(("fwd_parts", nb, dim_origin), 4 * nb * n)
+    _lib.check(L.maxk_spgemm_forward_ex(plan["sched"].data_ptr(), P, plan["indptr"].data_ptr(),
+                                        plan["indices"].data_ptr(), vals.data_ptr(), data.data_ptr(),
+                                        sel.data_ptr(), nb * g.num_rows, dim_origin, data.shape[1],
+                                        _lib.MAXK_FWD_CACHED_GATHER, parts.data_ptr(),
+                                        ws.data_ptr(), ws.numel(), _stream(out)),
+               "maxk_spgemm_forward (column-blocked)")
+    _lib.check(L.maxk_rows_sum(parts.data_ptr(), nb, n, out.data_ptr(), _stream(out)),
+               "maxk_rows_sum")
+    return out
+
+
+def _fwd_blocks(g: MaxKGraph, data, sel, dim_origin: int, out, values) -> int:
+    """Column blocks for this (k, h): MAXK_FWD_BLOCKS, or measured once
+    against the plain forward (graphs with long rows only; never under capture)."""
+    if FWD_BLOCKS >= 0:
+        return FWD_BLOCKS
+    key = (data.shape[1], dim_origin)
+    nb = g._fwd_blocks.get(key)
+    if nb is not None:
+        return nb
+    if g.num_edges < FWD_BLOCKED_MIN_DEGREE * g.num_rows or AUTO_MODE == "fixed":
+        g._fwd_blocks[key] = 0
+        return 0
+    if torch.cuda.is_current_stream_capturing():
+        return 0
+    L = _lib.load()
+    ws = g._workspace(("fwd", dim_origin), L.maxk_forward_workspace_bytes(g.num_panels, dim_origin))
+
+    def plain():
+        _lib.check(L.maxk_spgemm_forward_ex(g.sched.data_ptr(), g.num_panels, g.indptr.data_ptr(),
+                                            g.indices.data_ptr(), values.data_ptr(),
+                                            data.data_ptr(), sel.data_ptr(), g.num_rows,
+                                            dim_origin, data.shape[1], 0, out.data_ptr(),
+                                            ws.data_ptr(), ws.numel(), _stream(out)),
+                   "maxk_spgemm_forward")
+    best, best_ms = 0, _min_ms(plain)
+    for cand in FWD_BLOCKED_CANDIDATES:
+        ms = _min_ms(lambda: _forward_blocked(g, cand, data, sel, dim_origin, out, values))
+        if ms < best_ms:
+            best, best_ms = cand, ms
+    if best == 0:  # free what the losing candidates built
+        g._blocked.clear()
+        for c in FWD_BLOCKED_CANDIDATES:
+            g._ws.pop(("fwd_parts", c, dim_origin), None)
+            g._ws.pop(("fwd_blocked", c, dim_origin), None)
+    g._fwd_blocks[key] = best
+    return best
 
 
 def cbsr_gather_records(data: torch.Tensor, sel: torch.Tensor, rows: torch.Tensor | None = None,

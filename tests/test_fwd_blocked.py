@@ -1,0 +1,137 @@
+"""Column-blocked forward (ops._forward_blocked, maxk_rows_sum, the
+MAXK_FWD_CACHED_GATHER flag) against the CPU oracle: every block count, lanes
+and shapes the plain forward covers, rectangular blocks, values that change
+in place or arrive per call, hipGraph capture, and AUTO's choice.  Same
+tolerance as test_gpu_parity (the blocks change the fp32 summation order)."""
+import numpy as np
+import pytest
+import torch
+
+import spgemm_new_amd as S
+from spgemm_new_amd import _lib, ops
+from spgemm_new_amd.graphs import random_cbsr, small_csr
+
+pytestmark = pytest.mark.gpu
+TOL = 1e-4
+
+
+def T(a, dev):
+    return torch.from_numpy(np.ascontiguousarray(a)).to(dev)
+
+
+def _dense_graph(V, C, deg, seed):
+    rng = np.random.default_rng(seed)
+    d = rng.poisson(deg, V)
+    d[:3] = [0, C, 1]                                  # an empty row, a full row, a single edge
+    indptr = np.zeros(V + 1, np.int64)
+    indptr[1:] = np.cumsum(d)
+    idx = np.concatenate([np.sort(rng.choice(C, size=x, replace=False)) for x in d])
+    vals = rng.uniform(-1, 1, idx.size).astype(np.float32)
+    return indptr.astype(np.int32), idx.astype(np.int32), vals
+
+
+@pytest.mark.parametrize("nb", [1, 2, 3, 8, 16])
+@pytest.mark.parametrize("k", [32, 64])
+def test_blocked_forward_matches_oracle(dev, oracle, nb, k):
+    indptr, idx, vals = _dense_graph(2000, 2000, 150, seed=nb + k)
+    data, sel = random_cbsr(2000, k, 256, seed=k)
+    g = S.MaxKGraph(T(indptr, dev), T(idx, dev), T(vals, dev))
+    out = torch.full((2000, 256), float("nan"), device=dev)
+    ops._forward_blocked(g, nb, T(data, dev), T(sel, dev), 256, out, g.values)
+    ref = oracle.np_forward(indptr, idx, vals, data, sel, 256)
+    assert oracle.parity_error(out.cpu().numpy(), ref) <= TOL
+
+
+def test_blocked_forward_small_graph_and_narrow_rows(dev, oracle):
+    """The degree-mix graph of the parity tests (degrees 0 .. 3000) and h < 256."""
+    indptr, idx = small_csr(3000, seed=21)
+    vals = np.random.default_rng(2).random(len(idx), dtype=np.float32)
+    g = S.MaxKGraph(T(indptr, dev), T(idx, dev), T(vals, dev), panel_cost=300)
+    for k, h in [(32, 256), (48, 100), (64, 64)]:
+        data, sel = random_cbsr(3000, k, h, seed=k + h)
+        out = torch.empty((3000, h), device=dev)
+        ops._forward_blocked(g, 8, T(data, dev), T(sel, dev), h, out, g.values)
+        ref = oracle.np_forward(indptr, idx, vals, data, sel, h)
+        assert oracle.parity_error(out.cpu().numpy(), ref) <= TOL
+
+
+def test_blocked_forward_rectangular(dev, oracle):
+    """A rank's block: more columns than rows."""
+    indptr, idx, vals = _dense_graph(700, 2500, 200, seed=4)
+    data, sel = random_cbsr(2500, 32, 256, seed=9)
+    g = S.MaxKGraph(T(indptr, dev), T(idx, dev), T(vals, dev), num_cols=2500)
+    out = torch.empty((700, 256), device=dev)
+    ops._forward_blocked(g, 8, T(data, dev), T(sel, dev), 256, out, g.values)
+    ref = oracle.np_forward(indptr, idx, vals, data, sel, 256)
+    assert oracle.parity_error(out.cpu().numpy(), ref) <= TOL
+
+
+def test_blocked_forward_values_in_place_and_per_call(dev, oracle):
+    indptr, idx, vals = _dense_graph(1500, 1500, 160, seed=5)
+    data, sel = random_cbsr(1500, 32, 256, seed=2)
+    g = S.MaxKGraph(T(indptr, dev), T(idx, dev), T(vals, dev))
+    D, Sl = T(data, dev), T(sel, dev)
+    out = torch.empty((1500, 256), device=dev)
+    ops._forward_blocked(g, 4, D, Sl, 256, out, g.values)
+    g.values.mul_(-2.0)                                # in place: the plan's copy must follow
+    ops._forward_blocked(g, 4, D, Sl, 256, out, g.values)
+    ref = oracle.np_forward(indptr, idx, -2.0 * vals, data, sel, 256)
+    assert oracle.parity_error(out.cpu().numpy(), ref) <= TOL
+    w = np.random.default_rng(3).random(len(idx), dtype=np.float32)
+    ops._forward_blocked(g, 4, D, Sl, 256, out, T(w, dev))
+    ref = oracle.np_forward(indptr, idx, w, data, sel, 256)
+    assert oracle.parity_error(out.cpu().numpy(), ref) <= TOL
+
+
+def test_blocked_forward_under_hipgraph(dev, oracle):
+    indptr, idx, vals = _dense_graph(1500, 1500, 160, seed=6)
+    data, sel = random_cbsr(1500, 32, 256, seed=3)
+    g = S.MaxKGraph(T(indptr, dev), T(idx, dev), T(vals, dev))
+    D, Sl = T(data, dev), T(sel, dev)
+    out = torch.empty((1500, 256), device=dev)
+    ops._forward_blocked(g, 8, D, Sl, 256, out, g.values)      # plan and buffers first
+    s = torch.cuda.Stream()
+    s.wait_stream(torch.cuda.current_stream())
+    graph = torch.cuda.CUDAGraph()
+    with torch.cuda.stream(s), torch.cuda.graph(graph, stream=s):
+        ops._forward_blocked(g, 8, D, Sl, 256, out, g.values)
+    torch.cuda.current_stream().wait_stream(s)
+    g.values.mul_(0.5)
+    out.zero_()
+    graph.replay()
+    torch.cuda.synchronize()
+    ref = oracle.np_forward(indptr, idx, 0.5 * vals, data, sel, 256)
+    assert oracle.parity_error(out.cpu().numpy(), ref) <= TOL
+
+
+def test_rows_sum_order_and_tail(dev):
+    L = _lib.load()
+    for n in (1, 7, 1024, 4099):
+        parts = torch.randn(5, n, device=dev)
+        out = torch.empty(n, device=dev)
+        _lib.check(L.maxk_rows_sum(parts.data_ptr(), 5, n, out.data_ptr(), None), "rows_sum")
+        ref = parts[0].clone()
+        for q in range(1, 5):
+            ref += parts[q]
+        torch.cuda.synchronize()
+        assert torch.equal(out, ref)
+    assert L.maxk_rows_sum(None, 0, 4, None, None) == _lib.MAXK_E_ARG
+
+
+def test_auto_chooses_and_stays_correct(dev, oracle, monkeypatch):
+    """AUTO (MAXK_FWD_BLOCKS=-1) measures the blocked forward against the plain
+    one on a long-row graph, keeps its choice per (k, h), and is right either way;
+    short-row graphs never try it."""
+    monkeypatch.setattr(ops, "FWD_BLOCKS", -1)
+    indptr, idx, vals = _dense_graph(2000, 2000, 300, seed=8)
+    data, sel = random_cbsr(2000, 32, 256, seed=4)
+    g = S.MaxKGraph(T(indptr, dev), T(idx, dev), T(vals, dev))
+    y = g.forward(T(data, dev), T(sel, dev), 256)
+    assert (32, 256) in g._fwd_blocks
+    ref = oracle.np_forward(indptr, idx, vals, data, sel, 256)
+    assert oracle.parity_error(y.cpu().numpy(), ref) <= TOL
+    indptr2, idx2 = small_csr(3000, seed=21)           # mean degree < 128
+    g2 = S.MaxKGraph(T(indptr2, dev), T(idx2, dev))
+    g2.forward(T(random_cbsr(3000, 32, 256, seed=1)[0], dev),
+               T(random_cbsr(3000, 32, 256, seed=1)[1], dev), 256)
+    assert g2._fwd_blocks[(32, 256)] == 0 and not g2._blocked
