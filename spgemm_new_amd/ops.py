@@ -89,7 +89,7 @@ FWD_PACKED = os.environ.get("MAXK_FWD_PACKED", "1") != "0"
 # FWD_BLOCKED_MIN_DEGREE; 0 never; n > 0 always, with n column blocks
 FWD_BLOCKS = int(os.environ.get("MAXK_FWD_BLOCKS", "-1"))
 FWD_BLOCKED_MIN_DEGREE = 128
-FWD_BLOCKED_CANDIDATES = (8,)
+FWD_BLOCKED_CANDIDATES = (3, 4, 6, 8)  # Reddit: 4 best at k = 32 and 64
 # fused multi-relation forward: reorder CBSR entries against LDS store conflicts
 MULTI_BANK_ORDER = os.environ.get("MAXK_MULTI_BANK_ORDER", "1") != "0"
 
@@ -833,16 +833,19 @@ def _fwd_blocks(g: MaxKGraph, data, sel, dim_origin: int, out, values) -> int:
                                             dim_origin, data.shape[1], 0, out.data_ptr(),
                                             ws.data_ptr(), ws.numel(), _stream(out)),
                    "maxk_spgemm_forward")
+    def drop(c):  # what a losing candidate built
+        g._blocked.pop(c, None)
+        g._ws.pop(("fwd_parts", c, dim_origin), None)
+        g._ws.pop(("fwd_blocked", c, dim_origin), None)
     best, best_ms = 0, _min_ms(plain)
     for cand in FWD_BLOCKED_CANDIDATES:
         ms = _min_ms(lambda: _forward_blocked(g, cand, data, sel, dim_origin, out, values))
         if ms < best_ms:
+            if best:
+                drop(best)
             best, best_ms = cand, ms
-    if best == 0:  # free what the losing candidates built
-        g._blocked.clear()
-        for c in FWD_BLOCKED_CANDIDATES:
-            g._ws.pop(("fwd_parts", c, dim_origin), None)
-            g._ws.pop(("fwd_blocked", c, dim_origin), None)
+        else:
+            drop(cand)
     g._fwd_blocks[key] = best
     return best
 
