@@ -1909,10 +1909,10 @@ __device__ __forceinline__ void tile_groups2(const uint32_t (&g)[16], uint32_t &
     uint32_t t0, t1, t2, t3, t4, t5, t6, t7;
     uint64_t ex;
     asm volatile(
+        "s_waitcnt lgkmcnt(0)\n\t"
         "s_cmp_eq_u32 %[n], 0\n\t"
         "s_cbranch_scc1 .Ltp_done%=\n\t"
         "s_mov_b64 %[ex], exec\n\t"
-        "s_waitcnt lgkmcnt(0)\n\t"
         "s_cmp_lt_i32 %[m], 0\n\t"
         "s_cselect_b64 exec, %[lo], %[hi]\n\t"
         "s_lshr_b32 s80, %[g0], 2\n\t"
@@ -2378,6 +2378,12 @@ __global__ __launch_bounds__(kTileWaves * kWave) void bwd_tile_kernel(
         n = 0u;
         m = 0u;
 #endif
+        // the record groups must have landed before anything reads (or copies)
+        // their SGPRs -- also when this chunk has no records: a skipped wait let
+        // the next step's s_loads into the same SGPRs race with these (SMEM
+        // returns out of order), i.e. stale records, on graphs with empty
+        // wave-chunks (products k=32: runs differed in the last bits)
+        asm volatile("s_waitcnt lgkmcnt(0)" : "+s"(pa), "+s"(pb)::"memory");
         uint32_t ga[16], gb[16];
 #pragma unroll
         for (int i = 0; i < 16; ++i) {
