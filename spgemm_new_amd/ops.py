@@ -838,7 +838,11 @@ def _fwd_blocks(g: MaxKGraph, data, sel, dim_origin: int, out, values) -> int:
         g._ws.pop(("fwd_parts", c, dim_origin), None)
         g._ws.pop(("fwd_blocked", c, dim_origin), None)
     best, best_ms = 0, _min_ms(plain)
+    free, _ = torch.cuda.mem_get_info(g.device)
     for cand in FWD_BLOCKED_CANDIDATES:
+        # partial outputs + restacked indices / values / order: keep within a quarter of what is free
+        if 4 * cand * g.num_rows * dim_origin + 16 * g.num_edges > free // 4:
+            continue
         ms = _min_ms(lambda: _forward_blocked(g, cand, data, sel, dim_origin, out, values))
         if ms < best_ms:
             if best:
