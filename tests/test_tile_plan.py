@@ -295,3 +295,25 @@ def test_tile_one_range_is_sequential_fma(dev, k):
         prod = np.float64(vals[e]) * grad[rows[e], sel[c].astype(np.int64)].astype(np.float64)
         acc[c] = (prod + acc[c].astype(np.float64)).astype(np.float32)
     assert np.array_equal(got, acc)
+
+
+@pytest.mark.gpu
+def test_tile_repeat_calls_with_empty_wave_chunks(dev, oracle):
+    """A sparse graph (most wave-chunks hold no records): every step must wait for
+    its record loads even when it has nothing to do, or the next step's loads race
+    into the same registers (stale records; seen on products k=32).  Ten repeat
+    calls must be bit-identical and right."""
+    import spgemm_new_amd as S
+    from spgemm_new_amd import _lib
+    V, C = 20000, 20000
+    indptr, idx, vals = _graph(V, C, 3, seed=77)
+    grad, sel = _inputs(V, C, seed=78, k=32)
+    g = S.MaxKGraph(torch.from_numpy(indptr).to(dev), torch.from_numpy(idx).to(dev),
+                    torch.from_numpy(vals).to(dev))
+    assert g.tile_plan(32) is not None
+    G, sl = torch.from_numpy(grad).to(dev), torch.from_numpy(sel).to(dev)
+    first = g.backward(G, sl, algo=_lib.MAXK_BWD_TILE)
+    for _ in range(10):
+        assert torch.equal(first, g.backward(G, sl, algo=_lib.MAXK_BWD_TILE))
+    ref = oracle.np_backward(indptr, idx, vals, grad, sel)
+    assert oracle.parity_error(first.cpu().numpy(), ref) < TOL
