@@ -104,6 +104,22 @@ int maxk_spgemm_forward_ex(const int32_t *sched, int64_t num_panels, const int32
  * out[i] = parts[0][i] + ... + parts[num_parts-1][i] (that order), n floats
  * per part. */
 int maxk_rows_sum(const float *parts, int num_parts, int64_t n, float *out, void *stream);
+/* The column-blocked forward's restacked CSR, built on the device: row b*V + r
+ * of out_indptr (int32[num_blocks*V + 1]) holds row r's edges whose source c
+ * has c*num_blocks/num_cols == b, in CSR order; out_indices / out_values
+ * (int32 / fp32[E]; out_values may be NULL) are indices / values permuted by
+ * out_order (int32[E], the CSR edge of each restacked edge).  Needs
+ * num_blocks * V < 2^31 and maxk_blocked_plan_workspace_bytes() of device
+ * workspace.  Values that change later: maxk_permute_f32(values, out_order, E,
+ * out_values, stream). */
+size_t maxk_blocked_plan_workspace_bytes(int64_t num_edges, int num_rows, int num_blocks);
+int maxk_blocked_plan_build(const int32_t *indptr, const int32_t *indices, const float *values,
+                            int num_rows, int num_cols, int64_t num_edges, int num_blocks,
+                            int32_t *out_indptr, int32_t *out_indices, float *out_values,
+                            int32_t *out_order, void *workspace, size_t workspace_bytes,
+                            void *stream);
+/* dst[i] = src[perm[i]], n fp32 words. */
+int maxk_permute_f32(const float *src, const int32_t *perm, int64_t n, float *dst, void *stream);
 
 /* ---------------------------------------------------------------------------
  * Packed CBSR forward (k = 4, 8, 16).  maxk_cbsr_pack writes one record per

@@ -65,6 +65,9 @@ SIGNATURES = {
     "maxk_sspmm_backward_tile": (_I, [_P, _P, _P, _P, _P, _I, _I, _I, _P, _P, _P, _I, _I, _I, _I,
                                       _P, _P, _P]),
     "maxk_tile_format": (_I, [ctypes.POINTER(_I), ctypes.POINTER(_I)]),
+    "maxk_blocked_plan_workspace_bytes": (_S, [_L, _I, _I]),
+    "maxk_blocked_plan_build": (_I, [_P, _P, _P, _I, _I, _L, _I, _P, _P, _P, _P, _P, _S, _P]),
+    "maxk_permute_f32": (_I, [_P, _P, _L, _P, _P]),
     "maxk_rows_sum": (_I, [_P, _I, _L, _P, _P]),
     "maxk_tile_plan_shape": (_I, [_I, _I, _I, ctypes.POINTER(_I), ctypes.POINTER(_I),
                                   ctypes.POINTER(_I)]),

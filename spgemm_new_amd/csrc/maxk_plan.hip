@@ -97,6 +97,32 @@ __global__ void lower_bounds_kernel(const int32_t *__restrict__ sorted, int64_t 
     if (c < n_out) out[c] = (int32_t)lower_bound(sorted, n, c);
 }
 
+// ------------------------------------------------------ column-blocked forward
+// key of edge e = (column block of its source) * V + (its row): the restacked
+// CSR's row.  The row comes from a binary search of e in indptr.
+__global__ void blocked_keys_kernel(const int32_t *__restrict__ indptr, int num_rows,
+                                    const int32_t *__restrict__ indices, int64_t num_edges,
+                                    int num_cols, int num_blocks, int32_t *__restrict__ key)
+{
+    const int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (e >= num_edges) return;
+    int lo = 0, hi = num_rows;  // last row r with indptr[r] <= e
+    while (hi - lo > 1) {
+        const int mid = (lo + hi) >> 1;
+        if (indptr[mid] <= e) lo = mid; else hi = mid;
+    }
+    const int b = (int)(((int64_t)indices[e] * num_blocks) / num_cols);
+    key[e] = b * num_rows + lo;
+}
+
+// dst[i] = src[perm[i]] (32-bit words)
+__global__ void permute32_kernel(const uint32_t *__restrict__ src, const int32_t *__restrict__ perm,
+                                 int64_t n, uint32_t *__restrict__ dst)
+{
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < n) dst[i] = src[perm[i]];
+}
+
 // ---------------------------------------------------------------- LOCAL
 // cut[w] = first destination i with csc_indptr[i] >= w * E / T (exact integer
 // form of the balanced split), cut[0] = 0, cut[T] = V
@@ -506,6 +532,68 @@ int maxk_csc_build(const int32_t *indices, int64_t num_edges, int num_cols, int3
     hipLaunchKernelGGL(lower_bounds_kernel, dim3((unsigned)blocks_for((int64_t)num_cols + 1)),
                        dim3(kThreads), 0, st, keys_sorted, num_edges, csc_indptr,
                        (int64_t)num_cols + 1);
+    return launch_status();
+}
+
+size_t maxk_blocked_plan_workspace_bytes(int64_t num_edges, int num_rows, int num_blocks)
+{
+    if (num_edges < 0 || num_rows < 1 || num_blocks < 1 ||
+        (int64_t)num_rows * num_blocks >= INT32_MAX)
+        return 0;
+    return align_up((size_t)num_edges * 4, 256) * 2 +
+           align_up(sort_temp_bytes(num_edges, bits_for((int64_t)num_rows * num_blocks)), 256) + 256;
+}
+
+int maxk_blocked_plan_build(const int32_t *indptr, const int32_t *indices, const float *values,
+                            int num_rows, int num_cols, int64_t num_edges, int num_blocks,
+                            int32_t *out_indptr, int32_t *out_indices, float *out_values,
+                            int32_t *out_order, void *workspace, size_t workspace_bytes,
+                            void *stream)
+{
+    if (num_rows < 1 || num_cols < 1 || num_blocks < 1 || num_edges < 0 || num_edges > INT32_MAX ||
+        (int64_t)num_rows * num_blocks >= INT32_MAX || !indptr || !out_indptr)
+        return MAXK_E_ARG;
+    if (num_edges > 0 && (!indices || !out_indices || !out_order)) return MAXK_E_ARG;
+    hipStream_t st = static_cast<hipStream_t>(stream);
+    const int64_t R = (int64_t)num_rows * num_blocks;
+    if (num_edges == 0)
+        return (int)hipMemsetAsync(out_indptr, 0, sizeof(int32_t) * ((size_t)R + 1), st);
+    if (!workspace ||
+        workspace_bytes < maxk_blocked_plan_workspace_bytes(num_edges, num_rows, num_blocks))
+        return MAXK_E_WORKSPACE;
+    char *p = static_cast<char *>(workspace);
+    int32_t *key = carve<int32_t>(p, num_edges);
+    int32_t *key_sorted = carve<int32_t>(p, num_edges);
+    const unsigned bits = bits_for(R);
+    size_t tb = sort_temp_bytes(num_edges, bits);
+    hipLaunchKernelGGL(blocked_keys_kernel, dim3((unsigned)blocks_for(num_edges)), dim3(kThreads),
+                       0, st, indptr, num_rows, indices, num_edges, num_cols, num_blocks, key);
+    int rc = launch_status();
+    if (rc) return rc;
+    // LSD radix sort: stable, so a restacked row keeps its edges in CSR order
+    rocprim::counting_iterator<int32_t> iota(0);
+    hipError_t e = rocprim::radix_sort_pairs(p, tb, key, key_sorted, iota, out_order,
+                                             (size_t)num_edges, 0u, bits, st);
+    if (e != hipSuccess) return (int)e;
+    hipLaunchKernelGGL(lower_bounds_kernel, dim3((unsigned)blocks_for(R + 1)), dim3(kThreads), 0, st,
+                       key_sorted, num_edges, out_indptr, R + 1);
+    if ((rc = launch_status())) return rc;
+    hipLaunchKernelGGL(permute32_kernel, dim3((unsigned)blocks_for(num_edges)), dim3(kThreads), 0,
+                       st, reinterpret_cast<const uint32_t *>(indices), out_order, num_edges,
+                       reinterpret_cast<uint32_t *>(out_indices));
+    if ((rc = launch_status())) return rc;
+    if (values && out_values)
+        return maxk_permute_f32(values, out_order, num_edges, out_values, stream);
+    return MAXK_OK;
+}
+
+int maxk_permute_f32(const float *src, const int32_t *perm, int64_t n, float *dst, void *stream)
+{
+    if (n < 0 || (n > 0 && (!src || !perm || !dst))) return MAXK_E_ARG;
+    if (n == 0) return MAXK_OK;
+    hipLaunchKernelGGL(permute32_kernel, dim3((unsigned)blocks_for(n)), dim3(kThreads), 0,
+                       static_cast<hipStream_t>(stream), reinterpret_cast<const uint32_t *>(src),
+                       perm, n, reinterpret_cast<uint32_t *>(dst));
     return launch_status();
 }
 

@@ -244,36 +244,45 @@ class MaxKGraph:
         maxk_rows_sum)."""
         plan = self._blocked.get(num_blocks)
         if plan is None:
-            V, C, nb = self.num_rows, self.num_cols, num_blocks
-            rows = torch.repeat_interleave(torch.arange(V, device=self.device),
-                                           (self.indptr[1:] - self.indptr[:-1]).long())
-            key = (self.indices.long() * nb) // C * V + rows
-            key, order = torch.sort(key, stable=True)
-            indptr = torch.zeros(nb * V + 1, dtype=torch.int32, device=self.device)
-            indptr[1:] = torch.cumsum(torch.bincount(key, minlength=nb * V), 0).to(torch.int32)
-            del key, rows
-            sched, P = _build_schedule(indptr, nb * V, self.num_edges, self.panel_cost,
-                                       self.row_cost)
-            plan = {"num_blocks": nb, "order": order, "indptr": indptr,
-                    "indices": self.indices[order].contiguous(), "sched": sched,
-                    "num_panels": P, "values": None, "values_key": None}
+            V, C, nb, E = self.num_rows, self.num_cols, num_blocks, self.num_edges
+            L = _lib.load()
+            indptr = torch.empty(nb * V + 1, dtype=torch.int32, device=self.device)
+            indices = torch.empty(E, dtype=torch.int32, device=self.device)
+            order = torch.empty(E, dtype=torch.int32, device=self.device)
+            ws = torch.empty(max(1, L.maxk_blocked_plan_workspace_bytes(E, V, nb)), dtype=torch.uint8,
+                             device=self.device)
+            _lib.check(L.maxk_blocked_plan_build(self.indptr.data_ptr(), self.indices.data_ptr(), None,
+                                                 V, C, E, nb, indptr.data_ptr(), indices.data_ptr(),
+                                                 None, order.data_ptr(), ws.data_ptr(), ws.numel(),
+                                                 _stream(indptr)), "maxk_blocked_plan_build")
+            del ws
+            sched, P = _build_schedule(indptr, nb * V, E, self.panel_cost, self.row_cost)
+            plan = {"num_blocks": nb, "order": order, "indptr": indptr, "indices": indices,
+                    "sched": sched, "num_panels": P, "values": None, "values_key": None}
             self._blocked[num_blocks] = plan
         return plan
 
     def _blocked_values(self, plan: dict, values: torch.Tensor) -> torch.Tensor:
-        """values in the plan's edge order: kept for the graph's own values
-        (refreshed when they change in place), gathered per call for others."""
+        """values in the plan's edge order (maxk_permute_f32): kept for the
+        graph's own values (refreshed when they change in place; always re-gathered
+        under hipGraph capture), gathered per call for others."""
+        L = _lib.load()
+
+        def permute(dst):
+            _lib.check(L.maxk_permute_f32(values.data_ptr(), plan["order"].data_ptr(),
+                                          self.num_edges, dst.data_ptr(), _stream(dst)),
+                       "maxk_permute_f32")
+            return dst
         if values is not self.values:
-            return values[plan["order"]]
+            return permute(torch.empty(self.num_edges, dtype=torch.float32, device=self.device))
         key = _tensor_key(values)
-        if plan["values"] is None or plan["values_key"] != key:
-            if torch.cuda.is_current_stream_capturing() and plan["values"] is not None:
-                torch.index_select(values, 0, plan["order"], out=plan["values"])
-            else:
-                plan["values"] = values[plan["order"]].contiguous()
+        capturing = torch.cuda.is_current_stream_capturing()
+        if plan["values"] is None:
+            plan["values"] = torch.empty(self.num_edges, dtype=torch.float32, device=self.device)
+            plan["values_key"] = None
+        if capturing or plan["values_key"] != key:
+            permute(plan["values"])
             plan["values_key"] = key
-        elif torch.cuda.is_current_stream_capturing():
-            torch.index_select(values, 0, plan["order"], out=plan["values"])
         return plan["values"]
 
     def csc(self):

@@ -135,3 +135,22 @@ def test_auto_chooses_and_stays_correct(dev, oracle, monkeypatch):
     g2.forward(T(random_cbsr(3000, 32, 256, seed=1)[0], dev),
                T(random_cbsr(3000, 32, 256, seed=1)[1], dev), 256)
     assert g2._fwd_blocks[(32, 256)] == 0 and not g2._blocked
+
+
+@pytest.mark.parametrize("nb", [1, 3, 8])
+def test_blocked_plan_builder_matches_torch_reference(dev, nb):
+    """maxk_blocked_plan_build (device radix sort) == a stable torch sort of the
+    (column block, row) keys; values permuted by the same order."""
+    indptr, idx, vals = _dense_graph(1200, 3100, 40, seed=nb)
+    g = S.MaxKGraph(T(indptr, dev), T(idx, dev), T(vals, dev), num_cols=3100)
+    plan = g.blocked_plan(nb)
+    V, C = 1200, 3100
+    rows = torch.repeat_interleave(torch.arange(V, device=dev), (g.indptr[1:] - g.indptr[:-1]).long())
+    key = (g.indices.long() * nb) // C * V + rows
+    key, order = torch.sort(key, stable=True)
+    ip = torch.zeros(nb * V + 1, dtype=torch.int32, device=dev)
+    ip[1:] = torch.cumsum(torch.bincount(key, minlength=nb * V), 0).to(torch.int32)
+    assert torch.equal(plan["indptr"], ip)
+    assert torch.equal(plan["order"].long(), order)
+    assert torch.equal(plan["indices"], g.indices[order])
+    assert torch.equal(g._blocked_values(plan, g.values), g.values[order])
