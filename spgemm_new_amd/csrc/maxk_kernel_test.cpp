@@ -176,6 +176,31 @@ void test_graph(const std::string &dir, const std::string &graph, int idx, int c
     hipDeviceProp_t prop;
     HIPCHECK(hipGetDeviceProperties(&prop, 0));
 
+    // column-blocked forward (include/maxk_spgemm.h, maxk_rows_sum): the CSR
+    // restacked into kBlocks column blocks, its schedule and workspaces
+    constexpr int kBlocks = 4;
+    int32_t *b_indptr = dev_alloc<int32_t>((size_t)kBlocks * V + 1);
+    int32_t *b_indices = dev_alloc<int32_t>(E > 0 ? E : 1), *b_order = dev_alloc<int32_t>(E > 0 ? E : 1);
+    float *b_val = dev_alloc<float>(E > 0 ? E : 1);
+    {
+        const size_t b = maxk_blocked_plan_workspace_bytes(E, V, kBlocks);
+        void *ws = dev_alloc<char>(b);
+        MAXKCHECK(maxk_blocked_plan_build(indptr, indices, val, V, V, E, kBlocks, b_indptr, b_indices,
+                                          b_val, b_order, ws, b, st));
+        HIPCHECK(hipStreamSynchronize(st));
+        HIPCHECK(hipFree(ws));
+    }
+    int64_t BP = 0;
+    MAXKCHECK(maxk_schedule_num_panels((int64_t)kBlocks * V, E, MAXK_DEFAULT_PANEL_COST,
+                                       MAXK_DEFAULT_ROW_COST, &BP));
+    int32_t *b_sched = dev_alloc<int32_t>(2 * (size_t)(BP + 1));
+    MAXKCHECK(maxk_schedule_build(b_indptr, kBlocks * V, MAXK_DEFAULT_PANEL_COST,
+                                  MAXK_DEFAULT_ROW_COST, b_sched, BP, st));
+    const size_t bws_b = maxk_forward_workspace_bytes(BP, kDimOrigin);
+    void *bws = dev_alloc<char>(bws_b);
+    float *parts = dev_alloc<float>((size_t)kBlocks * V * kDimOrigin);
+    float *y_blk = dev_alloc<float>((size_t)V * kDimOrigin);
+
     std::printf("num graph dim_origin dim_k kernel time(ms)\n");
     for (size_t n = 0; n < sizeof(kDimKList) / sizeof(int); ++n) {
         const int k = kDimKList[n];
@@ -220,6 +245,29 @@ void test_graph(const std::string &dir, const std::string &graph, int idx, int c
             for (size_t i = 0; i < a.size(); ++i) err_sum += std::fabs((double)a[i] - b[i]);
             std::printf("err sum = %g  %s\n", err_sum,
                         err_sum / a.size() < 0.001 ? "validation pass!" : "validation fail!");
+        }
+
+        if (k >= 32) {  // the column-blocked forward: same Y up to the fp32 regrouping by block
+            auto fwd_blk = [&] {
+                MAXKCHECK(maxk_spgemm_forward_ex(b_sched, BP, b_indptr, b_indices, b_val, data, sel,
+                                                 kBlocks * V, kDimOrigin, k, MAXK_FWD_CACHED_GATHER,
+                                                 parts, bws, bws_b, st));
+                MAXKCHECK(maxk_rows_sum(parts, kBlocks, (int64_t)V * kDimOrigin, y_blk, st));
+            };
+            std::printf("%s maxk_blocked%d %g\n", out.c_str(), kBlocks, time_ms(fwd_blk));
+            if (check) {
+                fwd();
+                fwd_blk();
+                HIPCHECK(hipDeviceSynchronize());
+                std::vector<float> a((size_t)V * kDimOrigin), b(a.size());
+                HIPCHECK(hipMemcpy(a.data(), y_blk, a.size() * 4, hipMemcpyDeviceToHost));
+                HIPCHECK(hipMemcpy(b.data(), y, b.size() * 4, hipMemcpyDeviceToHost));
+                double worst = 0;
+                for (size_t i = 0; i < a.size(); ++i)
+                    worst = std::max(worst, std::fabs((double)a[i] - b[i]) / std::max(1.0, std::fabs((double)b[i])));
+                std::printf("forward blocked%d vs plain: max rel diff %g  %s\n", kBlocks, worst,
+                            worst <= 1e-4 ? "validation pass!" : "validation fail!");
+            }
         }
 
         // backward: every algorithm, then the fastest as maxk_backward; with

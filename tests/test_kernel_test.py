@@ -43,12 +43,15 @@ def test_harness_runs_and_validates(tmp_path):
                      "maxk_backward_local"]
             if k in (32, 64):
                 algos.append("maxk_backward_tile")   # the TILE plan through the C ABI
-            for kern in ["maxk", "maxk_backward"] + algos:
+            fwds = ["maxk"] + (["maxk_blocked4"] if k >= 32 else [])   # column-blocked forward
+            for kern in fwds + ["maxk_backward"] + algos:
                 assert times[(g, k, kern)] > 0, (g, k, kern)
             assert times[(g, k, "maxk_backward")] == min(times[(g, k, a)] for a in algos)
     checks = [ln for ln in lines if "validation" in ln]
-    # per graph: k=16 fwd + staged + staged_edge + local; k=32 and k=64 also tile
-    assert len(checks) == 2 * (4 + 5 + 5), checks
+    # per graph: k=16 fwd + staged + staged_edge + local; k=32 and k=64 also tile and
+    # the blocked forward
+    assert len(checks) == 2 * (4 + 6 + 6), checks
     assert all("validation pass!" in ln for ln in checks), checks
     assert sum("backward tile vs atomic" in ln for ln in checks) == 4
+    assert sum("forward blocked4 vs plain" in ln for ln in checks) == 4
     assert np.isfinite(list(times.values())).all()
