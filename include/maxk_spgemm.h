@@ -104,6 +104,18 @@ int maxk_spgemm_forward_ex(const int32_t *sched, int64_t num_panels, const int32
  * out[i] = parts[0][i] + ... + parts[num_parts-1][i] (that order), n floats
  * per part. */
 int maxk_rows_sum(const float *parts, int num_parts, int64_t n, float *out, void *stream);
+/* The column-blocked forward's last block with the sum fused into its row
+ * flush: out[r] = ((parts[0][r] + parts[1][r]) + ... + parts[num_parts-1][r])
+ * + (A . X^)[r], parts fp32[num_parts][num_rows][dim_origin] -- bitwise the
+ * result of maxk_rows_sum over num_parts + 1 parts, without writing and
+ * re-reading the last part or a separate pass.  flags: 0 or
+ * MAXK_FWD_CACHED_GATHER; num_parts = 0 is maxk_spgemm_forward_ex. */
+int maxk_spgemm_forward_sum_parts(const int32_t *sched, int64_t num_panels, const int32_t *indptr,
+                                  const int32_t *indices, const float *values,
+                                  const float *cbsr_data, const uint8_t *cbsr_sel, int num_rows,
+                                  int dim_origin, int dim_k, int flags, const float *parts,
+                                  int num_parts, float *out, void *workspace,
+                                  size_t workspace_bytes, void *stream);
 /* The column-blocked forward's restacked CSR, built on the device: row b*V + r
  * of out_indptr (int32[num_blocks*V + 1]) holds row r's edges whose source c
  * has c*num_blocks/num_cols == b, in CSR order; out_indices / out_values

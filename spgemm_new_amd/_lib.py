@@ -69,6 +69,7 @@ SIGNATURES = {
     "maxk_blocked_plan_build": (_I, [_P, _P, _P, _I, _I, _L, _I, _P, _P, _P, _P, _P, _S, _P]),
     "maxk_permute_f32": (_I, [_P, _P, _L, _P, _P]),
     "maxk_rows_sum": (_I, [_P, _I, _L, _P, _P]),
+    "maxk_spgemm_forward_sum_parts": (_I, [_P, _L, _P, _P, _P, _P, _P, _I, _I, _I, _I, _P, _I, _P, _P, _S, _P]),
     "maxk_tile_plan_shape": (_I, [_I, _I, _I, ctypes.POINTER(_I), ctypes.POINTER(_I),
                                   ctypes.POINTER(_I)]),
     "maxk_tile_plan_workspace_bytes": (_S, [_L, _I]),

@@ -395,8 +395,14 @@ enum FlushOp { kStore = 0, kAtomic = 1, kAdd = 2 };
 #define FWD_PACKED_NT 0
 #endif
 
+// SUMP (sp != nullptr, kStore only): the row is stored as
+// ((sp[0] + sp[ss]) + ... + sp[(nsp-1)*ss]) + row -- the column-blocked
+// forward's last block adding the earlier blocks' partial rows, in block
+// order: bitwise what maxk_rows_sum gives over all nb parts.
 template <int OP>
-__device__ __forceinline__ void flush_row(float *acc, int copies, float *__restrict__ dst, int dim)
+__device__ __forceinline__ void flush_row(float *acc, int copies, float *__restrict__ dst, int dim,
+                                          const float *__restrict__ sp = nullptr, int nsp = 0,
+                                          size_t ss = 0)
 {
     const int lane = lane_id();
     wave_sync_lds();
@@ -410,6 +416,12 @@ __device__ __forceinline__ void flush_row(float *acc, int copies, float *__restr
                 *q = f4{0.f, 0.f, 0.f, 0.f};
             }
             if (OP == kAdd) a += reinterpret_cast<const f4 *>(dst)[c4];  // row owned by this wave
+            if (OP == kStore && sp) {
+                f4 s = __builtin_nontemporal_load(reinterpret_cast<const f4 *>(sp) + c4);
+                for (int q = 1; q < nsp; ++q)
+                    s += __builtin_nontemporal_load(reinterpret_cast<const f4 *>(sp + q * ss) + c4);
+                a = s + a;
+            }
 #if FWD_NT_OUT
             __builtin_nontemporal_store(a, reinterpret_cast<f4 *>(dst) + c4);
 #else
@@ -423,6 +435,11 @@ __device__ __forceinline__ void flush_row(float *acc, int copies, float *__restr
             for (int cp = 1; cp < copies; ++cp) {
                 a += acc[cp * kMaxDim + c];
                 acc[cp * kMaxDim + c] = 0.f;
+            }
+            if (OP == kStore && sp) {
+                float t = sp[c];
+                for (int q = 1; q < nsp; ++q) t += sp[q * ss + c];
+                a = t + a;
             }
             if (OP == kStore) dst[c] = a;
             else if (OP == kAtomic) gbl_add(dst + c, a);
@@ -446,7 +463,8 @@ __global__ __launch_bounds__(kBlock) void fwd_panel_kernel(
     const int32_t *__restrict__ idx, const float *__restrict__ val,
     const float *__restrict__ data, const uint8_t *__restrict__ sel, int num_rows, int dim,
     int k, float *__restrict__ out, float *__restrict__ carry, int32_t *__restrict__ carry_row,
-    float *__restrict__ owner, uint8_t *__restrict__ esel)
+    float *__restrict__ owner, uint8_t *__restrict__ esel, const float *__restrict__ sump,
+    int nsump)
 {
     extern __shared__ __attribute__((aligned(16))) float lds[];
     const int dimp = (dim + 3) & ~3;
@@ -468,6 +486,9 @@ __global__ __launch_bounds__(kBlock) void fwd_panel_kernel(
         if (e < re) fwd_edges<K, RS, ESEL, NTD>(e, re, k, idx, val, data, sel, acc, esel);
         if (r == i0 && split_first)
             flush_row<kStore>(acc, copies, owner + (size_t)w * dimp, dim);
+        else if (!ACC && sump)
+            flush_row<kStore>(acc, copies, out + (size_t)r * dim, dim, sump + (size_t)r * dim, nsump,
+                              (size_t)num_rows * dim);
         else
             flush_row<ACC ? kAdd : kStore>(acc, copies, out + (size_t)r * dim, dim);
         e = re;
@@ -527,7 +548,8 @@ template <bool ACC>
 __global__ __launch_bounds__(kBlock) void carry_fixup_owner_kernel(
     const int2 *__restrict__ sched, int64_t num_panels, const float *__restrict__ carry,
     const float *__restrict__ owner, const int32_t *__restrict__ carry_row,
-    float *__restrict__ out, int dim, int dimp)
+    float *__restrict__ out, int dim, int dimp, int num_rows, const float *__restrict__ sump,
+    int nsump)
 {
     const int64_t w = (int64_t)blockIdx.x * kWavesPerBlock + threadIdx.x / kWave;
     if (w >= num_panels) return;
@@ -543,12 +565,23 @@ __global__ __launch_bounds__(kBlock) void carry_fixup_owner_kernel(
             f4 a = reinterpret_cast<const f4 *>(owner + (size_t)own * dimp)[c4];
             for (int64_t v = w; v < w_end; ++v) a += reinterpret_cast<const f4 *>(carry + (size_t)v * dimp)[c4];
             if (ACC) a += reinterpret_cast<const f4 *>(dst)[c4];
+            if (!ACC && sump) {  // earlier blocks' partial rows first (flush_row's SUMP order)
+                const f4 *sp = reinterpret_cast<const f4 *>(sump + (size_t)r * dim) + c4;
+                f4 t = sp[0];
+                for (int q = 1; q < nsump; ++q) t += sp[(size_t)q * num_rows * (dim >> 2)];
+                a = t + a;
+            }
             __builtin_nontemporal_store(a, reinterpret_cast<f4 *>(dst) + c4);
         }
     } else {
         for (int c = lane_id(); c < dim; c += kWave) {
             float a = owner[(size_t)own * dimp + c];
             for (int64_t v = w; v < w_end; ++v) a += carry[(size_t)v * dimp + c];
+            if (!ACC && sump) {
+                float t = sump[(size_t)r * dim + c];
+                for (int q = 1; q < nsump; ++q) t += sump[((size_t)q * num_rows + r) * dim + c];
+                a = t + a;
+            }
             dst[c] = ACC ? dst[c] + a : a;
         }
     }
@@ -2597,17 +2630,19 @@ template <int K>
 size_t fwd_lds_bytes(int k) { return (size_t)kWavesPerBlock * fwd_copies<K>(k) * kMaxDim * sizeof(float); }
 
 inline int fwd_fixup(const int32_t *sched, int64_t P, const float *carry, const float *owner,
-                     const int32_t *carry_row, float *out, int dim, bool acc, hipStream_t st)
+                     const int32_t *carry_row, float *out, int dim, bool acc, hipStream_t st,
+                     int num_rows = 0, const float *sump = nullptr, int nsump = 0)
 {
     const int64_t blocks = ceil_div(P, kWavesPerBlock);
     const int dimp = (dim + 3) & ~3;
     const int2 *sc = reinterpret_cast<const int2 *>(sched);
     if (acc)
         hipLaunchKernelGGL(carry_fixup_owner_kernel<true>, dim3((unsigned)blocks), dim3(kBlock), 0,
-                           st, sc, P, carry, owner, carry_row, out, dim, dimp);
+                           st, sc, P, carry, owner, carry_row, out, dim, dimp, num_rows,
+                           (const float *)nullptr, 0);
     else
         hipLaunchKernelGGL(carry_fixup_owner_kernel<false>, dim3((unsigned)blocks), dim3(kBlock), 0,
-                           st, sc, P, carry, owner, carry_row, out, dim, dimp);
+                           st, sc, P, carry, owner, carry_row, out, dim, dimp, num_rows, sump, nsump);
     return launch_status();
 }
 
@@ -2616,7 +2651,8 @@ struct FwdPanel {
     static int run(const int32_t *sched, int64_t P, const int32_t *indptr, const int32_t *idx,
                    const float *val, const float *data, const uint8_t *sel, int V, int dim, int k,
                    float *out, float *carry, int32_t *carry_row, float *owner, bool acc,
-                   hipStream_t st, uint8_t *esel = nullptr, bool cached = false)
+                   hipStream_t st, uint8_t *esel = nullptr, bool cached = false,
+                   const float *sump = nullptr, int nsump = 0)
     {
         const int64_t blocks = ceil_div(P, kWavesPerBlock);
         auto kern = esel ? fwd_panel_kernel<K, 0, false, true>
@@ -2625,10 +2661,10 @@ struct FwdPanel {
                     : acc ? fwd_panel_kernel<K, 0, true> : fwd_panel_kernel<K, 0, false>;
         hipLaunchKernelGGL(kern, dim3((unsigned)blocks), dim3(kBlock), fwd_lds_bytes<K>(k), st,
                            reinterpret_cast<const int2 *>(sched), P, indptr, idx, val, data, sel,
-                           V, dim, k, out, carry, carry_row, owner, esel);
+                           V, dim, k, out, carry, carry_row, owner, esel, sump, nsump);
         int rc = launch_status();
         if (rc) return rc;
-        return fwd_fixup(sched, P, carry, owner, carry_row, out, dim, acc, st);
+        return fwd_fixup(sched, P, carry, owner, carry_row, out, dim, acc, st, V, sump, nsump);
     }
 };
 
@@ -2648,7 +2684,8 @@ struct FwdPanelPacked {
             hipLaunchKernelGGL(kern, dim3((unsigned)blocks), dim3(kBlock),
                                fwd_lds_bytes<K>(k), st, reinterpret_cast<const int2 *>(sched), P,
                                indptr, idx, val, reinterpret_cast<const float *>(rec),
-                               rec + 4 * K, V, dim, k, out, carry, carry_row, owner, esel);
+                               rec + 4 * K, V, dim, k, out, carry, carry_row, owner, esel,
+                               (const float *)nullptr, 0);
             int rc = launch_status();
             if (rc) return rc;
             return fwd_fixup(sched, P, carry, owner, carry_row, out, dim, false, st);
@@ -2671,7 +2708,7 @@ struct FwdRecords {
             hipLaunchKernelGGL(kern, dim3((unsigned)blocks), dim3(kBlock), fwd_lds_bytes<K>(k), st,
                                reinterpret_cast<const int2 *>(sched), P, indptr, idx, val,
                                reinterpret_cast<const float *>(rec), rec + 4 * K, V, dim, k, out,
-                               carry, carry_row, owner, (uint8_t *)nullptr);
+                               carry, carry_row, owner, (uint8_t *)nullptr, (const float *)nullptr, 0);
             int rc = launch_status();
             if (rc) return rc;
             return fwd_fixup(sched, P, carry, owner, carry_row, out, dim, acc, st);
@@ -2975,6 +3012,33 @@ int maxk_spgemm_forward_ex(const int32_t *sched, int64_t num_panels, const int32
                                 fwd_owner_slots(workspace, num_panels, dim_origin),
                                 (flags & MAXK_FWD_ACCUMULATE) != 0, as_stream(stream),
                                 (uint8_t *)nullptr, (flags & MAXK_FWD_CACHED_GATHER) != 0);
+}
+
+int maxk_spgemm_forward_sum_parts(const int32_t *sched, int64_t num_panels, const int32_t *indptr,
+                                  const int32_t *indices, const float *values,
+                                  const float *cbsr_data, const uint8_t *cbsr_sel, int num_rows,
+                                  int dim_origin, int dim_k, int flags, const float *parts,
+                                  int num_parts, float *out, void *workspace,
+                                  size_t workspace_bytes, void *stream)
+{
+    if (flags & ~MAXK_FWD_CACHED_GATHER) return MAXK_E_ARG;
+    if (num_parts < 0 || (num_parts > 0 && !parts)) return MAXK_E_ARG;
+    if (!sched || !indptr || !out || num_panels < 1 || num_rows < 0) return MAXK_E_ARG;
+    if (!dims_ok(dim_origin, dim_k)) return MAXK_E_DIM;
+    if (num_rows == 0) return MAXK_OK;
+    if (!indices || !values || !cbsr_data || !cbsr_sel) return MAXK_E_ARG;
+    if (!workspace || workspace_bytes < maxk_forward_workspace_bytes(num_panels, dim_origin))
+        return MAXK_E_WORKSPACE;
+    const size_t dimp = (size_t)((dim_origin + 3) & ~3);
+    float *carry = static_cast<float *>(workspace);
+    int32_t *carry_row = reinterpret_cast<int32_t *>(
+        static_cast<char *>(workspace) + align_up((size_t)num_panels * dimp * sizeof(float), 256));
+    return dispatch_k<FwdPanel>(dim_k, sched, num_panels, indptr, indices, values, cbsr_data,
+                                cbsr_sel, num_rows, dim_origin, dim_k, out, carry, carry_row,
+                                fwd_owner_slots(workspace, num_panels, dim_origin), false,
+                                as_stream(stream), (uint8_t *)nullptr,
+                                (flags & MAXK_FWD_CACHED_GATHER) != 0,
+                                num_parts > 0 ? parts : (const float *)nullptr, num_parts);
 }
 
 int maxk_rows_sum(const float *parts, int num_parts, int64_t n, float *out, void *stream)

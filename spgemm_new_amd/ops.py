@@ -259,6 +259,7 @@ class MaxKGraph:
             sched, P = _build_schedule(indptr, nb * V, E, self.panel_cost, self.row_cost)
             plan = {"num_blocks": nb, "order": order, "indptr": indptr, "indices": indices,
                     "sched": sched, "num_panels": P, "values": None, "values_key": None}
+            _blocked_split(self, plan)
             self._blocked[num_blocks] = plan
         return plan
 
@@ -797,24 +798,56 @@ def spgemm_forward(g: MaxKGraph, data, sel, dim_origin: int = 256, out=None, val
     return out
 
 
+def _blocked_split(g: MaxKGraph, plan: dict) -> dict:
+    """Schedules of the column-blocked forward's two launches, built once: the
+    first nb-1 blocks (rows [0, (nb-1)V) of the restacked CSR, into partial
+    outputs) and the last block (rows [(nb-1)V, nb V), whose row flush adds the
+    partials: maxk_spgemm_forward_sum_parts)."""
+    sp = plan.get("split")
+    if sp is None:
+        nb, V = plan["num_blocks"], g.num_rows
+        ip = plan["indptr"]
+        h = (nb - 1) * V
+        e_head = int(ip[h].item())
+        sp = {"head_rows": h, "last_indptr": ip[h:]}
+        if h > 0:
+            sp["head_sched"], sp["head_P"] = _build_schedule(ip[:h + 1], h, e_head, g.panel_cost,
+                                                             g.row_cost)
+        sp["last_sched"], sp["last_P"] = _build_schedule(sp["last_indptr"], V, g.num_edges - e_head,
+                                                         g.panel_cost, g.row_cost)
+        plan["split"] = sp
+    return sp
+
+
 def _forward_blocked(g: MaxKGraph, nb: int, data, sel, dim_origin: int, out, values):
-    """Column-blocked forward: the restacked CSR's forward into nb partial
-    outputs (cacheable gathers), then their sum in block order."""
+    """Column-blocked forward: the restacked CSR's first nb-1 blocks into
+    partial outputs (cacheable gathers), then the last block, whose row flush
+    adds the partials in block order (bitwise the sum maxk_rows_sum gives over
+    all nb parts, one partial write + read and one pass fewer)."""
     L = _lib.load()
     plan = g.blocked_plan(nb)
     vals = g._blocked_values(plan, values)
-    P = plan["num_panels"]
+    sp = _blocked_split(g, plan)
+    P = max(sp["last_P"], sp.get("head_P", 1))
     ws = g._workspace(("fwd_blocked", nb, dim_origin), L.maxk_forward_workspace_bytes(P, dim_origin))
     n = g.num_rows * dim_origin
-    parts = g._workspace(("fwd_parts", nb, dim_origin), 4 * nb * n)
-    _lib.check(L.maxk_spgemm_forward_ex(plan["sched"].data_ptr(), P, plan["indptr"].data_ptr(),
-                                        plan["indices"].data_ptr(), vals.data_ptr(), data.data_ptr(),
-                                        sel.data_ptr(), nb * g.num_rows, dim_origin, data.shape[1],
-                                        _lib.MAXK_FWD_CACHED_GATHER, parts.data_ptr(),
-                                        ws.data_ptr(), ws.numel(), _stream(out)),
-               "maxk_spgemm_forward (column-blocked)")
-    _lib.check(L.maxk_rows_sum(parts.data_ptr(), nb, n, out.data_ptr(), _stream(out)),
-               "maxk_rows_sum")
+    k = data.shape[1]
+    parts = None
+    if nb > 1:
+        parts = g._workspace(("fwd_parts", nb, dim_origin), 4 * (nb - 1) * n)
+        _lib.check(L.maxk_spgemm_forward_ex(sp["head_sched"].data_ptr(), sp["head_P"],
+                                            plan["indptr"].data_ptr(), plan["indices"].data_ptr(),
+                                            vals.data_ptr(), data.data_ptr(), sel.data_ptr(),
+                                            sp["head_rows"], dim_origin, k,
+                                            _lib.MAXK_FWD_CACHED_GATHER, parts.data_ptr(),
+                                            ws.data_ptr(), ws.numel(), _stream(out)),
+                   "maxk_spgemm_forward (column-blocked, blocks 0..nb-2)")
+    _lib.check(L.maxk_spgemm_forward_sum_parts(
+        sp["last_sched"].data_ptr(), sp["last_P"], sp["last_indptr"].data_ptr(),
+        plan["indices"].data_ptr(), vals.data_ptr(), data.data_ptr(), sel.data_ptr(), g.num_rows,
+        dim_origin, k, _lib.MAXK_FWD_CACHED_GATHER, parts.data_ptr() if parts is not None else None,
+        nb - 1, out.data_ptr(), ws.data_ptr(), ws.numel(), _stream(out)),
+        "maxk_spgemm_forward_sum_parts (column-blocked, last block)")
     return out
 
 

@@ -154,3 +154,58 @@ def test_blocked_plan_builder_matches_torch_reference(dev, nb):
     assert torch.equal(plan["order"].long(), order)
     assert torch.equal(plan["indices"], g.indices[order])
     assert torch.equal(g._blocked_values(plan, g.values), g.values[order])
+
+
+def _blocked_all_parts_then_sum(g, nb, data, sel, h, L):
+    """The earlier form on the same panels: every block into its own partial
+    (blocks 0..nb-2 on the head schedule, the last block on its own), then
+    maxk_rows_sum over the nb parts."""
+    plan = g.blocked_plan(nb)
+    vals = g._blocked_values(plan, g.values)
+    sp = ops._blocked_split(g, plan)
+    V, k = g.num_rows, data.shape[1]
+    P = max(sp["last_P"], sp.get("head_P", 1))
+    ws = torch.empty(L.maxk_forward_workspace_bytes(P, h), dtype=torch.uint8, device=data.device)
+    parts = torch.empty((nb, V, h), device=data.device)
+    launches = [(sp["last_sched"], sp["last_P"], sp["last_indptr"], V, parts[nb - 1])]
+    if nb > 1:
+        launches.append((sp["head_sched"], sp["head_P"], plan["indptr"], sp["head_rows"], parts))
+    for sched, np_, ip, rows, dst in launches:
+        _lib.check(L.maxk_spgemm_forward_ex(sched.data_ptr(), np_, ip.data_ptr(),
+                                            plan["indices"].data_ptr(), vals.data_ptr(),
+                                            data.data_ptr(), sel.data_ptr(), rows, h, k,
+                                            _lib.MAXK_FWD_CACHED_GATHER, dst.data_ptr(),
+                                            ws.data_ptr(), ws.numel(), None), "fwd")
+    out = torch.empty((V, h), device=data.device)
+    _lib.check(L.maxk_rows_sum(parts.data_ptr(), nb, V * h, out.data_ptr(), None), "sum")
+    return out
+
+
+@pytest.mark.parametrize("nb", [1, 2, 4, 8])
+def test_fused_last_block_sum_bitwise_equals_rows_sum(dev, nb):
+    """maxk_spgemm_forward_sum_parts (the last block adds the partials in its
+    row flush and in the split-row fixup) is bitwise the all-parts + rows_sum
+    form: rows split over panels (panel_cost 300, degrees up to 3000), empty
+    rows, h a multiple of 4 and not."""
+    L = _lib.load()
+    indptr, idx = small_csr(3000, seed=5)
+    vals = np.random.default_rng(3).random(len(idx), dtype=np.float32)
+    g = S.MaxKGraph(T(indptr, dev), T(idx, dev), T(vals, dev), panel_cost=300)
+    for k, h in [(32, 256), (32, 98), (64, 256)]:
+        data, sel = random_cbsr(3000, k, h, seed=k + h + nb)
+        data, sel = T(data, dev), T(sel, dev)
+        out = torch.full((3000, h), float("nan"), device=dev)
+        ops._forward_blocked(g, nb, data, sel, h, out, g.values)
+        ref = _blocked_all_parts_then_sum(g, nb, data, sel, h, L)
+        assert torch.equal(out, ref), (nb, k, h)
+
+
+def test_sum_parts_entry_arguments(dev):
+    L = _lib.load()
+    assert L.maxk_spgemm_forward_sum_parts(None, 1, None, None, None, None, None, 1, 256, 32, 0,
+                                           None, 0, None, None, 0, None) == _lib.MAXK_E_ARG
+    # accumulate is not a flag of this entry
+    x = torch.zeros(16, device=dev)
+    assert L.maxk_spgemm_forward_sum_parts(x.data_ptr(), 1, x.data_ptr(), None, None, None, None, 1,
+                                           256, 32, _lib.MAXK_FWD_ACCUMULATE, None, 0, x.data_ptr(),
+                                           None, 0, None) == _lib.MAXK_E_ARG
