@@ -42,6 +42,32 @@ elif mode == "addr":
         body = body.replace('[%s] "=&v"(%s), ' % (o, o), "")
     body = body.replace("uint32_t o0, o1, o2, o3, a0, a1, a2, a3;", "uint32_t a0, a1, a2, a3;")
     body = body.replace('"memory", "scc", ', '"memory", "scc", "s81", "s84", "s87", "s90", ')
+elif mode in ("alate", "anop"):
+    # "addr", then either the VALU row-address shifts moved after the group's
+    # s_set_gpr_idx_off (no gpr-index toggle between their write and the read),
+    # or kept in place with s_nop 7 before each SRC0 s_set_gpr_idx_on
+    om = {"o0": "s81", "o1": "s84", "o2": "s87", "o3": "s90"}
+    for o, sg in om.items():
+        body = re.sub(r'"v_lshlrev_b32 %%\[%s\], 3, ([^\\]+)\\n\\t"' % o, r'"s_lshl_b32 %s, \1, 3\\n\\t"' % sg, body)
+        body = body.replace(", v48, %%[%s], 8" % o, ", v48, %s, 8" % sg)
+        body = body.replace('[%s] "=&v"(%s), ' % (o, o), "")
+    body = body.replace("uint32_t o0, o1, o2, o3, a0, a1, a2, a3;", "uint32_t a0, a1, a2, a3;")
+    body = body.replace('"memory", "scc", ', '"memory", "scc", "s81", "s84", "s87", "s90", ')
+    if mode == "anop":
+        body = body.replace('"s_set_gpr_idx_on s80, gpr_idx(SRC0)\\n\\t"',
+                            '"s_nop 7\\n\\ts_set_gpr_idx_on s80, gpr_idx(SRC0)\\n\\t"')
+    else:
+        out, pend = [], []
+        for line in body.split("\n"):
+            if re.match(r'\s*"v_lshrrev_b32 %\[a\d\], 14, ', line):
+                pend.append(line)
+                continue
+            out.append(line)
+            if '"s_set_gpr_idx_off\\n\\t"' in line and pend:
+                out.extend(pend)
+                pend = []
+        assert not pend
+        body = "\n".join(out)
 else:
-    sys.exit("mode: movbfe | addr")
+    sys.exit("mode: movbfe | addr | alate | anop")
 open(dst, "w").write(s[:a] + body + s[b:])
