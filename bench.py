@@ -27,6 +27,8 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md, chip-level parameters)
+# committed per-workload PMC results (tools/summarize_profile.py writes it)
+PMC_INDEX = os.path.join(ROOT, "profiles", "pmc_traffic.json")
 
 
 def parse():
@@ -43,7 +45,9 @@ def parse():
     p.add_argument("--panel-cost", type=int, default=None)
     p.add_argument("--row-cost", type=int, default=None)
     p.add_argument("--no-cpu-baseline", action="store_true")
-    p.add_argument("--cpu-seconds", type=float, default=15.0)
+    p.add_argument("--cpu-seconds", type=float, default=40.0,
+                   help="CPU-baseline budget: the whole graph when 4 runs of it fit, else "
+                        "the rows holding half of E")
     p.add_argument("--partitioned", action="store_true",
                    help="use the multi-GPU (row partition + halo exchange) path even at N=1")
     p.add_argument("--verbose", action="store_true")
@@ -54,6 +58,11 @@ def parse():
     p.add_argument("--relations", type=int, default=1,
                    help="R > 1: BASELINE config 5, the fused R-relation forward "
                         "(use with --graph proteins) vs R single-relation forwards")
+    p.add_argument("--no-configs", action="store_true",
+                   help="skip the BASELINE config 3 / 5 sweep appended to the N=1 line "
+                        "(products k in {8,16,32,64}, proteins R=8)")
+    p.add_argument("--configs-only", default=None,
+                   help="comma list of sweep entries to run (products_k8,...,proteins_r8)")
     return p.parse_args()
 
 
@@ -75,28 +84,46 @@ def log(*a):
     print(*a, file=sys.stderr, flush=True)
 
 
+def _median(xs):
+    xs = sorted(xs)
+    n = len(xs)
+    return 0.5 * (xs[(n - 1) // 2] + xs[n // 2]) if n else float("nan")
+
+
 def cpu_threads():
-    """Host threads for the CPU baseline: every core this process may run on
-    (sched_getaffinity), capped by OMP_NUM_THREADS when the launcher sets it
-    (the GPU box sets it to its per-GPU CPU share)."""
-    visible = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else \
-        (os.cpu_count() or 1)
+    """Thread counts for the CPU baseline: os.cpu_count(), the
+    cores this process may run on (sched_getaffinity) and the OMP_NUM_THREADS
+    cap the launcher sets (the GPU box: its per-GPU CPU share)."""
+    count = os.cpu_count() or 1
+    visible = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else count
     cap = os.environ.get("OMP_NUM_THREADS")
-    threads = min(visible, int(cap)) if cap and cap.isdigit() and int(cap) > 0 else visible
-    return threads, visible, cap
+    capped = min(visible, int(cap)) if cap and cap.isdigit() and int(cap) > 0 else visible
+    return count, visible, cap, capped
+
+
+def _cgroup_cpu_quota():
+    """The cgroup v2 CPU quota in cores (None when unlimited or unknown)."""
+    try:
+        q, p = open("/sys/fs/cgroup/cpu.max").read().split()[:2]
+        return None if q == "max" else round(int(q) / int(p), 2)
+    except (OSError, ValueError):
+        return None
 
 
 def cpu_baseline(indptr, indices, values, x_masked, grad, mask, k, h, budget_s):
     """The reference's CPU aggregation path (utils/models.py:281-287:
     torch.sparse.mm(adj, x) and its mean form torch.sparse.mm(adj, x) /
-    (adj.sum(1) + 1e-6)), forward and backward (A^T G * mask), on a bounded
-    row sample of the same graph, timed on the host cores.  `value` is the
-    sum form's fwd + bwd rate on the sample (same byte formula as the GPU
-    line); the full-graph time is the sample's time scaled by E / e_sample."""
+    (adj.sum(1) + 1e-6)), forward and backward (A^T G * mask), timed on the
+    host cores.  Threads: os.cpu_count() as SURVEY.md §8d asks; when the
+    launcher caps OMP_NUM_THREADS below it (the GPU box: its per-GPU share),
+    both counts are probed on a small sample and the faster one times the main
+    sample (both probes are in the line).  The main sample is the rows holding
+    at least half of E -- the whole graph when the projected time fits the
+    budget -- timed 1 warm-up + 3 runs (median), the reference's protocol
+    (SURVEY.md §8d).  `value` is the sum form's fwd + bwd rate on that sample
+    (same byte formula as the GPU line)."""
     import numpy as np
-    threads, visible, cap = cpu_threads()
-    torch.set_num_threads(threads)
-    log(f"[bench] CPU baseline on {threads} threads ({visible} visible, OMP_NUM_THREADS={cap})")
+    count, visible, cap, capped = cpu_threads()
     ip = indptr.cpu().numpy().astype(np.int64)
     V = len(ip) - 1
     E = int(ip[-1])
@@ -121,12 +148,22 @@ def cpu_baseline(indptr, indices, values, x_masked, grad, mask, k, h, budget_s):
         del y, dx, ym
         return e, t1 - t0, t2 - t1, t3 - t2
 
-    rows = max(1, min(V, V // 200))
-    e, tf, tb, _ = run(rows)
-    per_edge = (tf + tb) / max(e, 1)
-    target_e = min(E, int(budget_s / 3 / max(per_edge, 1e-12)))
-    rows = int(np.searchsorted(ip, target_e))
-    rows = max(1, min(V, rows))
+    # thread probe: a small sample (~2 % of E) per candidate count
+    probe_rows = max(1, min(V, int(np.searchsorted(ip, E // 50))))
+    probes = {}
+    for t in sorted({count, capped}):
+        torch.set_num_threads(t)
+        run(probe_rows)
+        e_p, tf, tb, _ = run(probe_rows)
+        probes[t] = (tf + tb) / max(e_p, 1)
+    threads = min(probes, key=probes.get)
+    torch.set_num_threads(threads)
+    log(f"[bench] CPU baseline on {threads} threads (os.cpu_count() {count}, affinity {visible}, "
+        f"OMP_NUM_THREADS={cap}; probe s/edge {probes})")
+    per_edge = probes[threads]
+    # at least half of E; the whole graph when 4 runs of it fit the budget
+    target_e = max(E // 2, min(E, int(budget_s / 4.6 / max(per_edge, 1e-12))))
+    rows = max(1, min(V, int(np.searchsorted(ip, target_e))))
     run(rows)  # warm-up
     res = [run(rows) for _ in range(3)]
     e = res[0][0]
@@ -135,17 +172,24 @@ def cpu_baseline(indptr, indices, values, x_masked, grad, mask, k, h, budget_s):
     scale = E / max(e, 1)
     return {
         "value": round(nbytes / (tf + tb) / 1e9, 3), "unit": "GB/s", "cores": threads,
-        "cores_visible": visible, "kind": "reference",
+        "os_cpu_count": count, "cores_affinity": visible, "omp_num_threads": cap,
+        "cgroup_cpu_quota_cores": _cgroup_cpu_quota(),
+        "thread_probe_us_per_kedge": {str(t): round(v * 1e9, 2) for t, v in probes.items()},
+        "kind": "reference",
+        "rows_sampled": rows, "edges_sampled": e, "edge_fraction": round(e / E, 4),
         "ms_per_step_sample": round((tf + tb) * 1e3, 2),
         "fwd_ms_sample": round(tf * 1e3, 2), "bwd_ms_sample": round(tb * 1e3, 2),
         "mean_form_fwd_ms_sample": round(tm * 1e3, 2),
         "mean_form_GBs": round((nbytes / 2) / tm / 1e9, 3),
-        "ms_per_step_full_graph_extrapolated": round((tf + tb) * scale * 1e3, 1),
-        "sample": (f"rows [0,{rows}) of the same graph ({e} edges, {e / E:.1%} of E; full-graph "
-                   f"time extrapolated x{scale:.2f} by edges): torch.sparse.mm(A,X*mask) + "
-                   "torch.sparse.mm(A^T,G)*mask on CPU fp32 (sum form = value), plus the mean "
-                   "form /(rowsum+1e-6), median of 3 after 1 warm-up (reference CPU path "
-                   f"utils/models.py:281-287), {threads} threads"),
+        "ms_per_step_full_graph": round((tf + tb) * scale * 1e3, 1),
+        "sample": (f"rows [0,{rows}) of the same graph ({e} edges, {e / E:.1%} of E"
+                   + ("" if e == E else f"; full-graph time scaled x{scale:.3f} by edges")
+                   + "): torch.sparse.mm(A,X*mask) + torch.sparse.mm(A^T,G)*mask on CPU fp32 "
+                   "(sum form = value; the backward's A^T coalesce is inside its time, as in "
+                   "torch's autograd of the reference op), plus the mean form /(rowsum+1e-6); "
+                   "median of 3 after 1 warm-up (reference CPU path utils/models.py:281-287), "
+                   f"{threads} threads (the faster of os.cpu_count()={count} and the "
+                   f"OMP_NUM_THREADS cap {capped} on a 2 %-of-E probe)"),
         "cpu_model": _cpu_model(),
     }
 
@@ -176,19 +220,43 @@ def workload_key(args, bwd_algo):
     return f"{args.graph}_h{args.h}_k{args.k}_{bwd_algo}"
 
 
+KERNEL_SOURCES = ("spgemm_new_amd/csrc/maxk_spgemm.hip", "spgemm_new_amd/csrc/maxk_plan.hip",
+                  "spgemm_new_amd/csrc/tile_format.h")
+
+
+def kernel_source_sha(root=ROOT) -> str:
+    """sha256 (16 hex) of the kernel and plan-builder sources: the key that ties a
+    committed PMC profile to the code it measured (tools/summarize_profile.py
+    stores it; bench.py refuses a profile whose key differs)."""
+    import hashlib
+    h = hashlib.sha256()
+    for rel in KERNEL_SOURCES:
+        with open(os.path.join(root, rel), "rb") as fh:
+            h.update(fh.read())
+    return h.hexdigest()[:16]
+
+
 def pmc_traffic(key, call, algo=None, bands=1):
     """HBM bytes of one hot-path call (`spgemm_forward` / `sspmm_backward`)
     measured by rocprofv3 PMC passes (FETCH_SIZE x2 + WRITE_SIZE,
     MI355X_MICROARCH.md §HBM) for this exact workload, from the committed
     profile summary (tools/profile.sh + tools/summarize_profile.py): per-kernel
     bytes per launch times the launches the call makes (the LOCAL backward
-    launches once per source band).  None when no such profile exists."""
-    path = os.path.join(ROOT, "profiles", "pmc_traffic.json")
+    launches once per source band).  Returns (bytes, source, stale): bytes is
+    None when no profile exists for the workload or when the profile was taken
+    on other kernel sources than these (its `source_sha` differs from
+    kernel_source_sha(): a stale profile is reported, never used)."""
     try:
-        ent = json.load(open(path))[key]
+        ent = json.load(open(PMC_INDEX))[key]
         k = ent["kernels"]
     except (OSError, KeyError, ValueError, TypeError):
-        return None, None
+        return None, None, None
+    src = f"profiles/{ent['profile']}_summary.json"
+    sha = ent.get("source_sha")
+    if sha != kernel_source_sha():
+        return None, src, {"profile": ent["profile"], "profiled_source_sha": sha,
+                           "current_source_sha": kernel_source_sha(),
+                           "reason": "kernel sources changed since this profile: not used"}
     fix = k.get("carry_fixup_kernel", 0.0)
     if call == "spgemm_forward":
         parts = [k.get("fwd_panel_kernel"), k.get("carry_fixup_owner_kernel", fix)]
@@ -201,8 +269,45 @@ def pmc_traffic(key, call, algo=None, bands=1):
     else:
         parts = [k.get("bwd_panel_kernel")]
     if any(p is None for p in parts):
-        return None, None
-    return int(sum(parts)), f"profiles/{ent['profile']}_summary.json"
+        return None, src, None
+    return int(sum(parts)), src, None
+
+
+# issue capacity per CU and cycle (MI355X_MICROARCH.md): one scalar instruction,
+# two wave64 vector instructions (4 SIMD-32, 2 cycles each), LDS-array cycles by
+# the instruction's width (ds_read_b32: 2 cycles per wave-instruction)
+ISSUE_PEAK_PER_CU_CYCLE = {"SQ_INSTS_SALU": 1.0, "SQ_INSTS_VALU": 2.0, "SQ_INSTS_SMEM": 1.0}
+
+
+def issue_bound(key, kernel, launch_ms, cus):
+    """Issue-rate roofline of one kernel from the committed SQ counters of its
+    profile (same source key as pmc_traffic): instructions of each class per
+    CU-cycle against that class's peak issue rate, cycles = GRBM_GUI_ACTIVE / 8
+    (the counter sums the 8 XCDs, MI355X_MICROARCH.md 'DVFS give-back'); LDS
+    busy = SQ_LDS_IDX_ACTIVE (LDS-array cycles, summed over CUs) per CU-cycle.
+    None without such counters."""
+    try:
+        ent = json.load(open(PMC_INDEX))[key]
+        c = ent["issue"][kernel]
+    except (OSError, KeyError, ValueError, TypeError):
+        return None
+    if ent.get("source_sha") != kernel_source_sha() or not c.get("GRBM_GUI_ACTIVE"):
+        return None
+    cycles = c["GRBM_GUI_ACTIVE"] / 8.0
+    out = {"profile": ent["profile"], "kernel": kernel, "cycles": int(cycles),
+           "clock_GHz": round(cycles / (c.get("avg_ms", launch_ms) * 1e6), 3) if c.get("avg_ms")
+           else None}
+    fr = {}
+    for name, peak in ISSUE_PEAK_PER_CU_CYCLE.items():
+        if name in c:
+            fr[name] = round(c[name] / (cus * cycles * peak), 4)
+    if "SQ_LDS_IDX_ACTIVE" in c:
+        fr["SQ_LDS_IDX_ACTIVE"] = round(c["SQ_LDS_IDX_ACTIVE"] / (cus * cycles), 4)
+    out["busy_frac"] = fr
+    if fr:
+        out["bound"] = max(fr, key=fr.get)
+        out["frac"] = fr[out["bound"]]
+    return out
 
 
 def vendor_baseline(g, indptr, indices, values, X, sel, y, fwd_ms, ev_ms):
@@ -292,6 +397,157 @@ def bench_multi_partitioned(args, indptr, indices, vals, data, sel, V, E, h, k, 
     }
     if rank == 0:
         print(json.dumps(result), flush=True)
+
+
+def _timed_calls(calls, steps, warmup):
+    """Per-call HIP-event times (ms) of a step made of `calls` (functions run in
+    order), on the current stream: `warmup` untimed steps, then `steps` timed
+    ones; returns one list per call."""
+    st = torch.cuda.current_stream()
+    for _ in range(warmup):
+        for fn in calls:
+            fn()
+    out = [[] for _ in calls]
+    for _ in range(steps):
+        ev = [torch.cuda.Event(enable_timing=True) for _ in range(len(calls) + 1)]
+        ev[0].record(st)
+        for i, fn in enumerate(calls):
+            fn()
+            ev[i + 1].record(st)
+        ev[-1].synchronize()
+        for i in range(len(calls)):
+            out[i].append(ev[i].elapsed_time(ev[i + 1]))
+    return out
+
+
+def _ms_stats(xs):
+    return {"mean": round(sum(xs) / len(xs), 4), "median": round(_median(xs), 4),
+            "min": round(min(xs), 4)}
+
+
+SWEEP_ENTRIES = ("products_k8", "products_k16", "products_k32", "products_k64", "proteins_r8")
+
+
+def config_sweep(args, dev, only=None):
+    """BASELINE configs 3 and 5 on this GPU, appended to the N=1 line (VERDICT r2
+    item 2): ogbn-products-shaped h=256 with k in {8, 16, 32, 64} -- the k sweep of
+    the reference harness (kernels/main.cu:111-116) -- and ogbn-proteins-shaped
+    h=256 k=32 with R=8 relations (fused forward + multi-relation backward).
+    Per entry: >= 5 warm-up steps then `steps` (>= 20) timed steps of forward +
+    backward, HIP events per call; mean and median ms; fraction of the 8 TB/s
+    roofline on the algorithmic bytes; the algorithms AUTO
+    chose; the timed dx checked against STAGED and the exact adjoint identity."""
+    import spgemm_new_amd as S
+    from spgemm_new_amd import _lib
+    from spgemm_new_amd.graphs import (CONFIGS, synthetic_columns, synthetic_indptr,
+                                       synthetic_values)
+    from spgemm_new_amd.ops import topk_cbsr
+    steps, warmup = max(args.steps, 20), max(args.warmup, 5)
+    h = 256
+    out = {"protocol": f"{warmup} warm-up + {steps} timed steps, HIP events per call, "
+                       "AUTO algorithms, same synthetic generator as the headline (seed 123)"}
+    want = set(only) if only else set(SWEEP_ENTRIES)
+    t_all = time.time()
+    ks = [k for k in (8, 16, 32, 64) if f"products_k{k}" in want]
+    if ks:
+        V, E = CONFIGS["products"]
+        t0 = time.time()
+        indptr = synthetic_indptr(V, E, seed=args.seed, device=dev)
+        indices = synthetic_columns(indptr, seed=args.seed)
+        values = synthetic_values(args.seed, 0, E, device=dev)
+        g = S.MaxKGraph(indptr, indices, values)
+        gen = torch.Generator(device=dev)
+        gen.manual_seed(args.seed + 1)
+        X = torch.rand((V, h), generator=gen, device=dev)
+        G = torch.rand((V, h), generator=gen, device=dev)
+        y = torch.empty((V, h), device=dev)
+        log(f"[bench] sweep: products V={V} E={E} built in {time.time() - t0:.1f}s")
+        for k in ks:
+            t0 = time.time()
+            data, sel = topk_cbsr(X, k)
+            dx = torch.empty((V, k), device=dev)
+            g.backward(G, sel, out=dx)        # AUTO choice, plans, workspaces
+            fw, bw = _timed_calls([lambda: g.forward(data, sel, h, out=y, edge_sel="auto"),
+                                   lambda: g.backward(G, sel, out=dx)], steps, warmup)
+            algo = g.last_bwd_algo
+            nb = g._fwd_blocks.get((k, h), 0)
+            b = g.nbytes_fwd(k, h)
+            torch.cuda.synchronize()
+            dx_ref = g.backward(G, sel, algo=_lib.MAXK_BWD_STAGED)
+            lhs = float((y.double() * G.double()).sum())
+            rhs = float((data.double() * dx.double()).sum())
+            fs, bs = _ms_stats(fw), _ms_stats(bw)
+            st = [a + c for a, c in zip(fw, bw)]
+            out[f"products_k{k}"] = {
+                "graph": "products", "num_nodes": V, "num_edges": E, "hidden": h, "k": k,
+                "fwd_ms": fs, "bwd_ms": bs, "ms_per_step": _ms_stats(st),
+                "algorithmic_bytes_per_call": b,
+                "fwd_frac": round(b / (fs["mean"] / 1e3) / 1e9 / HBM_PEAK_GBS, 4),
+                "bwd_frac": round(b / (bs["mean"] / 1e3) / 1e9 / HBM_PEAK_GBS, 4),
+                "step_GBs": round(2 * b / (sum(st) / len(st) / 1e3) / 1e9, 1),
+                "bwd_algo": algo, "fwd_form": (f"column-blocked nb={nb}" if nb else
+                                               "packed CBSR records" if k <= 16 else "plain"),
+                "bwd_check": {"vs": "staged",
+                              "max_rel_diff": float(((dx - dx_ref).abs()
+                                                     / dx_ref.abs().clamp_min(1)).max()),
+                              "adjoint_rel_err": abs(lhs - rhs) / max(abs(lhs), 1e-30)},
+                "wall_s": round(time.time() - t0, 1)}
+            log(f"[bench] sweep products k={k}: fwd {fs['mean']:.3f} bwd {bs['mean']:.3f} ms "
+                f"({algo}) in {time.time() - t0:.1f}s")
+            del data, sel, dx, dx_ref
+            # drop the per-k plans and buffers before the next k
+            g._ws.clear()
+            g._esel.clear()
+            g._tile.clear()
+            g._local.clear()
+            g._blocked.clear()
+            torch.cuda.empty_cache()
+        del g, X, G, y, indptr, indices, values
+        torch.cuda.empty_cache()
+    if "proteins_r8" in want:
+        t0 = time.time()
+        V, E = CONFIGS["proteins"]
+        R, k = 8, 32
+        indptr = synthetic_indptr(V, E, seed=args.seed, device=dev)
+        indices = synthetic_columns(indptr, seed=args.seed)
+        vals = torch.stack([synthetic_values(args.seed + 7 + q, 0, E, device=dev)
+                            for q in range(R)], dim=1).contiguous()
+        g = S.MaxKGraph(indptr, indices, vals[:, 0].contiguous())
+        gen = torch.Generator(device=dev)
+        gen.manual_seed(args.seed + 1)
+        X = torch.rand((V, h), generator=gen, device=dev)
+        G = torch.rand((R, V, h), generator=gen, device=dev)
+        data, sel = topk_cbsr(X, k)
+        y = torch.empty((R, V, h), device=dev)
+        dx = torch.empty((V, k), device=dev)
+        g.forward_multi(data, sel, vals, h, out=y)
+        g.backward_multi(G, sel, vals, out=dx)      # AUTO choice
+        fw, bw = _timed_calls([lambda: g.forward_multi(data, sel, vals, h, out=y),
+                               lambda: g.backward_multi(G, sel, vals, out=dx)], steps, warmup)
+        torch.cuda.synchronize()
+        y0 = g.forward(data, sel, h, values=vals[:, 0].contiguous())
+        fwd_err = float(((y[0] - y0).abs() / y0.abs().clamp_min(1)).max())
+        lhs = float((y.double() * G.double()).sum())
+        rhs = float((data.double() * dx.double()).sum())
+        b = E * (4 + 4 * R + 5 * k) + R * 4 * h * V
+        fs, bs = _ms_stats(fw), _ms_stats(bw)
+        out["proteins_r8"] = {
+            "graph": "proteins", "num_nodes": V, "num_edges": E, "hidden": h, "k": k,
+            "relations": R, "fwd_ms": fs, "bwd_ms": bs,
+            "algorithmic_bytes_per_call": b,
+            "bytes_formula": "E*(4 + 4R + 5k) + R*4hV (SURVEY.md §8d, fused)",
+            "fwd_frac": round(b / (fs["mean"] / 1e3) / 1e9 / HBM_PEAK_GBS, 4),
+            "bwd_frac": round(b / (bs["mean"] / 1e3) / 1e9 / HBM_PEAK_GBS, 4),
+            "bwd_algo": g.last_bwd_algo,
+            "check": {"fwd_rel0_vs_single_max_rel_diff": fwd_err,
+                      "adjoint_rel_err": abs(lhs - rhs) / max(abs(lhs), 1e-30)},
+            "wall_s": round(time.time() - t0, 1)}
+        log(f"[bench] sweep proteins R=8: fwd {fs['mean']:.3f} bwd {bs['mean']:.3f} ms "
+            f"in {time.time() - t0:.1f}s")
+        del g, X, G, y, y0, dx, data, sel, vals, indptr, indices
+        torch.cuda.empty_cache()
+    out["wall_s"] = round(time.time() - t_all, 1)
+    return out
 
 
 def _cpu_model():
@@ -475,8 +731,8 @@ def main():
         dx = torch.empty((V, k), device=dev)
         g.backward(G, sel, out=dx, algo=algo)  # builds CSC/workspaces once
 
-        def fwd_call():
-            g.forward(data, sel, h, out=y)
+        def fwd_call():   # a training forward: its backward follows with this sel
+            g.forward(data, sel, h, out=y, edge_sel="auto")
 
         def bwd_call():
             g.backward(G, sel, out=dx, algo=algo)
@@ -543,6 +799,13 @@ def main():
         if dist:
             dist.all_reduce(t, op=dist.ReduceOp.MAX)
         fms, bms, b_max = float(t[0]), float(t[1]), float(t[2])
+        med = torch.tensor([_median([a + b for a, b in zip(fw, bw)]), _median(fw), _median(bw)],
+                           device=dev, dtype=torch.float64)
+        if dist:
+            dist.all_reduce(med, op=dist.ReduceOp.MAX)
+        result["ms_per_step_median"] = round(float(med[0]), 4)
+        result["fwd_ms_median"] = round(float(med[1]), 4)
+        result["bwd_ms_median"] = round(float(med[2]), 4)
         dom = ("sspmm_backward", bms) if bms >= fms else ("spgemm_forward", fms)
         ach = b_max / (dom[1] / 1e3) / 1e9
         result["roofline"] = {"bound": "hbm", "achieved": round(ach, 1), "peak": HBM_PEAK_GBS,
@@ -572,8 +835,8 @@ def main():
         bands = 1
         if g.last_bwd_algo == "local":
             bands = g.local_bands(g.local_plan(k), h)[1]
-        traffic, tsrc = pmc_traffic(workload_key(args, g.last_bwd_algo), dom[0],
-                                    g.last_bwd_algo, bands)
+        wkey = workload_key(args, g.last_bwd_algo)
+        traffic, tsrc, stale = pmc_traffic(wkey, dom[0], g.last_bwd_algo, bands)
         result["roofline"] = {"bound": "hbm", "achieved": round(ach, 1), "peak": HBM_PEAK_GBS,
                               "unit": "GB/s", "frac": round(ach / HBM_PEAK_GBS, 4),
                               "traffic": traffic, "traffic_source": tsrc, "kernel": dom[0],
@@ -585,8 +848,25 @@ def main():
         rf["algorithmic_bytes_per_call"] = b_call
         rf["algorithmic_bytes_per_launch"] = b_call // rf["launches_per_call"]
         rf["launch_avg_ms"] = round(dom[1] / rf["launches_per_call"], 4)
+        rf["source_sha"] = kernel_source_sha()
+        if stale is not None:
+            rf["traffic_stale"] = stale
         if traffic is not None:
             rf["traffic_per_launch"] = traffic // rf["launches_per_call"]
+            # what the counters say the kernel really moves: fabric bytes / time / peak
+            rf["traffic_GBs"] = round(traffic / (dom[1] / 1e3) / 1e9, 1)
+            rf["traffic_frac"] = round(rf["traffic_GBs"] / HBM_PEAK_GBS, 4)
+        main_kernel = {"tile": "bwd_tile_kernel", "local": "bwd_local_kernel"}.get(
+            g.last_bwd_algo, "bwd_panel_kernel") if dom[0] == "sspmm_backward" else "fwd_panel_kernel"
+        cus = torch.cuda.get_device_properties(dev).multi_processor_count
+        iss = issue_bound(wkey, main_kernel, rf["launch_avg_ms"], cus)
+        if iss is not None:
+            rf["issue"] = iss
+        steps_ms = sorted(a + b for a, b in zip(fw, bw))
+        result["ms_per_step_median"] = round(_median(steps_ms), 4)
+        result["ms_per_step_events_mean"] = round(sum(steps_ms) / len(steps_ms), 4)
+        result["fwd_ms_median"] = round(_median(fw), 4)
+        result["bwd_ms_median"] = round(_median(bw), 4)
         result["config"]["bwd_algo"] = g.last_bwd_algo
         # untimed parity check of the timed outputs: dx of the timed algorithm vs
         # STAGED (an independent algorithm), and the exact adjoint identity
@@ -641,6 +921,9 @@ def main():
         if not args.no_vendor and rank == 0:
             result["vendor_baseline"] = vendor_baseline(g, indptr, indices, values, X, sel, y, fms,
                                                         ev_ms)
+        if not args.no_configs and args.graph == "reddit" and rank == 0:
+            only = args.configs_only.split(",") if args.configs_only else None
+            result["configs"] = config_sweep(args, dev, only)
         if not args.no_cpu_baseline and rank == 0:
             mask = torch.zeros((V, h), device=dev)
             mask.scatter_(1, sel.long(), 1.0)

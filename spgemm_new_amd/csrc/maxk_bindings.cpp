@@ -95,34 +95,42 @@ torch::Tensor spmm_maxk_backward(torch::Tensor warp4_metadata, torch::Tensor ind
     return grad_input;
 }
 
-// exact top-k by the library's CBSR producer in torch.topk's order (replaces
-// the reference's uint8-quantised kernel, cuda_kernel_bindings.cpp:203-238)
-std::vector<torch::Tensor> cuda_topk_maxk_float(torch::Tensor input, int k)
+std::tuple<torch::Tensor, torch::Tensor> cuda_topk_maxk(torch::Tensor input, int k)
 {
-    TORCH_CHECK(input.is_cuda(), "Input must be CUDA tensor");
+    TORCH_CHECK(input.is_cuda(), "Input must be on CUDA");
+    TORCH_CHECK(input.dim() == 2, "Input must be 2D tensor");
+    TORCH_CHECK(input.dtype() == torch::kUInt8, "Input must be uint8 tensor");
+    TORCH_CHECK(k > 0 && k <= input.size(1), "Invalid k value");
+    auto r = torch::topk(input.to(torch::kInt32), k, 1);
+    return std::make_tuple(std::get<0>(r).to(torch::kUInt8), std::get<1>(r).to(torch::kUInt8));
+}
+
+// cuda_kernel_bindings.cpp:203-238's contract: float32 in -> (float32 values,
+// int32 indices); uint8 in -> (uint8 values, int32 indices) through the uint8
+// path.  The float32 top-k is exact (the library's CBSR producer in torch.topk's
+// order) instead of the reference's uint8-quantised one.
+std::tuple<torch::Tensor, torch::Tensor> cuda_topk_maxk_float(torch::Tensor input, int k)
+{
+    TORCH_CHECK(input.is_cuda(), "Input must be on CUDA");
     TORCH_CHECK(input.dim() == 2, "Input must be 2D tensor");
     TORCH_CHECK(k > 0 && k <= input.size(1), "Invalid k value");
-    auto x = input.to(torch::kFloat32).contiguous();
+    if (input.dtype() == torch::kUInt8) {
+        auto r = cuda_topk_maxk(input, k);
+        return std::make_tuple(std::get<0>(r), std::get<1>(r).to(torch::kInt32));
+    }
+    TORCH_CHECK(input.dtype() == torch::kFloat32, "Input must be float32 or uint8");
+    auto x = input.contiguous();
     const int V = (int)x.size(0), h = (int)x.size(1);
+    TORCH_CHECK(h <= kFullDim, "Input rows must have at most 256 columns");
     auto vals = torch::empty({V, k}, x.options());
     auto sel = torch::empty({V, k}, x.options().dtype(torch::kUInt8));
     check_rc(maxk_topk_cbsr(x.data_ptr<float>(), V, h, h, k, MAXK_TOPK_ORDER_VALUE,
                             vals.data_ptr<float>(), sel.data_ptr<uint8_t>(), nullptr, cur_stream()),
              "maxk_topk_cbsr");
-    return {vals, sel.to(torch::kInt32)};
+    return std::make_tuple(vals, sel.to(torch::kInt32));
 }
 
-std::vector<torch::Tensor> cuda_topk_maxk(torch::Tensor input, int k)
-{
-    TORCH_CHECK(input.is_cuda(), "Input must be CUDA tensor");
-    TORCH_CHECK(input.dtype() == torch::kUInt8, "Input must be uint8");
-    TORCH_CHECK(input.dim() == 2, "Input must be 2D tensor");
-    TORCH_CHECK(k > 0 && k <= input.size(1), "Invalid k value");
-    auto r = torch::topk(input.to(torch::kInt32), k, 1);
-    return {std::get<0>(r).to(torch::kUInt8), std::get<1>(r).to(torch::kUInt8)};
-}
-
-std::vector<torch::Tensor> prepare_cbsr_format_maxk(torch::Tensor features, int maxk)
+std::tuple<torch::Tensor, torch::Tensor> prepare_cbsr_format_maxk(torch::Tensor features, int maxk)
 {
     return cuda_topk_maxk_float(features, maxk);
 }

@@ -54,6 +54,28 @@ def a2a(out: torch.Tensor, inp: torch.Tensor, out_split=None, in_split=None,
     return out
 
 
+def ag(out: torch.Tensor, inp: torch.Tensor, async_op: bool = False):
+    """all_gather_into_tensor (every rank's equal-sized chunk, in rank order);
+    with gloo the device tensors are staged through host memory and the call
+    completes before it returns (tests on one GPU)."""
+    if out.is_cuda and dist.get_backend() == "gloo":
+        world = dist.get_world_size()
+        chunks = [torch.empty_like(inp, device="cpu") for _ in range(world)]
+        dist.all_gather(chunks, inp.cpu())
+        out.copy_(torch.cat(chunks))
+        return _Done() if async_op else out
+    if async_op:
+        return dist.all_gather_into_tensor(out, inp, async_op=True)
+    dist.all_gather_into_tensor(out, inp)
+    return out
+
+
+# all-gather the CBSR instead of the all-to-all-v of halo records when some
+# rank's halo covers more than this fraction of V (SURVEY.md §8e: "when the halo
+# is close to the full vertex set"; then both move about (N-1)/N of the table)
+HALO_ALLGATHER_FRAC = 0.75
+
+
 def row_partition(indptr: torch.Tensor, world: int, row_cost: int = 16) -> list[int]:
     """Contiguous row bounds [b_0=0, ..., b_world=V] balancing edges + row_cost*rows."""
     V = indptr.numel() - 1
@@ -141,11 +163,28 @@ class PartitionedMaxK:
 
     def __init__(self, indptr, indices, values, rank: int, world: int, device,
                  engine=None, row_cost: int = 16, overlap: bool = True, records: bool = True,
-                 local_block: bool = False, overlap_backward: bool | None = None, **engine_kw):
+                 local_block: bool = False, overlap_backward: bool | None = None,
+                 bwd_algo: int | None = None, halo_mode: str = "auto", **engine_kw):
         """indptr: the GLOBAL row pointer (V + 1 entries, cheap); indices /
         values: the global arrays, or with ``local_block=True`` only this rank's
         edges (rows [bounds[rank], bounds[rank + 1]) of ``row_partition(indptr,
-        world, row_cost)``), so no rank materialises the whole graph."""
+        world, row_cost)``), so no rank materialises the whole graph.
+
+        ``bwd_algo`` pins the local backward algorithm (a ``_lib.MAXK_BWD_*``
+        code) of every part; None keeps the engine's AUTO, which tunes the
+        single block and the own / halo parts separately and may pick
+        different algorithms (so different fp32 summation orders) for them.
+
+        ``halo_mode``: "records" -- the forward's all-to-all-v
+        of exactly the halo rows; "allgather" -- every rank all-gathers the
+        whole CBSR as records (5k B per node, its own rows one chunk; no
+        per-peer packing) and the halo part reads the halo rows in place from
+        that table; "auto" -- allgather when some rank's halo exceeds
+        HALO_ALLGATHER_FRAC of V (products at N = 8: 87 %),
+        decided once with an all-reduce so every rank calls the same collective.
+        The halo part computes on the same edges in the same order either way,
+        so Y is bitwise the same; the backward's reverse exchange is the
+        all-to-all-v of halo partial sums in both modes."""
         self.rank, self.world, self.device = rank, world, torch.device(device)
         self.bounds = row_partition(indptr, world, row_cost)
         self.plan = HaloPlan(indptr, indices, self.bounds, rank, world, self.device,
@@ -170,12 +209,15 @@ class PartitionedMaxK:
         seg_off[1:] = torch.cumsum(counts, 0)
         self._ret = (order.contiguous(), seg_off, nodes.to(torch.int64).contiguous())
         self.records = records
-        # overlap (forward): the block is also split by column into own | halo
-        # parts, so the own part computes while the halo CBSR is in flight.  The
-        # backward keeps the single block: split, each part's LOCAL sweep visits
-        # every source band and the pair cost +0.05 ms (N=8) to +0.31 ms (N=2)
-        # more than the block, more than the exchange they would hide
-        # (tools/exp_rank_local.py).
+        # overlap: the block is also split by column into own | halo parts.  The
+        # forward computes the own part while the halo CBSR is in flight; the
+        # backward (overlap_backward, on for N > 1) computes the halo columns
+        # first and their partial sums travel while the own columns are computed.
+        # The column sets are disjoint, so with the same local algorithm on every
+        # part (bwd_algo pinned) dXs is bitwise the single block's; the forward
+        # adds each row's own-column edges before its halo-column edges, a
+        # different fp32 order than the single block's edge order.
+        self.bwd_algo = bwd_algo
         self.overlap = overlap and p.num_halo > 0
         if self.overlap:
             li = p.local_indices.long()
@@ -191,6 +233,14 @@ class PartitionedMaxK:
                             lv[mask].contiguous(), ncols, **engine_kw)
             self.local_own = part(is_own, 0, p.num_own)
             self.local_halo = part(~is_own, p.num_own, p.num_halo)
+            hm = ~is_own
+            ip_h = torch.zeros(p.num_own + 1, dtype=torch.int32, device=self.device)
+            ip_h[1:] = torch.cumsum(torch.bincount(rows[hm], minlength=p.num_own), 0)
+            # the halo part's CSR, kept to build its all-gather-table form on demand
+            self._halo_csr = (ip_h, (li[hm] - p.num_own).contiguous(), lv[hm].contiguous())
+        self._make, self._engine_kw = make, engine_kw
+        self.halo_mode = self._pick_halo_mode(halo_mode)
+        self._halo_tab = None
         self.local = make(p.local_indptr, p.local_indices, lv, p.num_own + p.num_halo,
                           **engine_kw)
         # backward overlap: the halo columns' dXs first, their reverse exchange in
@@ -203,6 +253,38 @@ class PartitionedMaxK:
         self._halo_part = None   # its halo selectors: [num_halo, k] (view of records or rows)
 
     # --------------------------------------------------------------- helpers
+    def _pick_halo_mode(self, mode: str) -> str:
+        if mode not in ("auto", "records", "allgather"):
+            raise RuntimeError("halo_mode must be 'auto', 'records' or 'allgather'")
+        if mode != "auto" or self.world == 1:
+            return "records" if mode == "auto" else mode
+        p = self.plan
+        V = self.bounds[-1]
+        frac = torch.tensor([p.num_halo / max(1, V)], dtype=torch.float64)
+        if dist.get_backend() != "gloo":
+            frac = frac.to(self.device)
+        dist.all_reduce(frac, op=dist.ReduceOp.MAX)
+        return "allgather" if float(frac) > HALO_ALLGATHER_FRAC else "records"
+
+    def _allgather_ok(self, k: int) -> bool:
+        return (self.halo_mode == "allgather" and self.overlap and self.world > 1
+                and self._use_records(k, self.local_halo))
+
+    def _table(self):
+        """(max_own, halo table rows, halo-part engine over table rows): row r of
+        rank q sits at q * max_own + (r - bounds[q]) of the all-gathered table."""
+        if self._halo_tab is None:
+            p = self.plan
+            b = torch.tensor(self.bounds, device=self.device)
+            max_own = max(self.bounds[i + 1] - self.bounds[i] for i in range(self.world))
+            owner = torch.searchsorted(b, p.halo_global, right=True) - 1
+            pos = (owner * max_own + (p.halo_global - b[owner])).to(torch.int32).contiguous()
+            ip_h, cols_h, vals_h = self._halo_csr
+            eng = self._make(ip_h, pos[cols_h.long()].contiguous(), vals_h, self.world * max_own,
+                             **self._engine_kw)
+            self._halo_tab = (max_own, pos, eng)
+        return self._halo_tab
+
     def local_rows(self, t: torch.Tensor) -> torch.Tensor:
         """Slice of a global per-node tensor owned by this rank."""
         r0, r1 = self.bounds[self.rank], self.bounds[self.rank + 1]
@@ -275,6 +357,8 @@ class PartitionedMaxK:
             return self.local.forward(data, sel, dim_origin)
         if not self._use_records(k, self.local_halo):
             return self._forward_overlap_rows(data_own, sel_own, dim_origin)
+        if self._allgather_ok(k):
+            return self._forward_allgather(data_own, sel_own, dim_origin)
         recv = self._buf(("recv", k), (p.num_halo, 5 * k), torch.uint8)
         work = a2a(recv, self._pack(data_own, sel_own), p.recv_counts, p.send_counts,
                    async_op=True)
@@ -284,6 +368,41 @@ class PartitionedMaxK:
         self.local_halo.forward_records(recv, k, dim_origin, out=y, accumulate=True)
         self._fwd_sel, self._halo_part = sel_own, recv[:, 4 * k:]
         return y
+
+    def _forward_allgather(self, data_own, sel_own, dim_origin):
+        """halo_mode "allgather": every rank's own rows as one records chunk,
+        all-gathered (padded to the largest block); the own part computes while
+        it is in flight; the halo part then reads its rows in place from the
+        table (same edges and order as the records path: bitwise the same Y)."""
+        from .ops import cbsr_gather_records
+        p = self.plan
+        k = data_own.shape[1]
+        max_own, pos, eng = self._table()
+        mine = self._bufs.get(("ag_send", k))
+        if mine is None:   # rows past this rank's block are padding: zeros, never read
+            mine = self._bufs[("ag_send", k)] = torch.zeros((max_own, 5 * k), dtype=torch.uint8,
+                                                           device=self.device)
+        if data_own.is_cuda:
+            cbsr_gather_records(data_own, sel_own, out=mine[: p.num_own])
+        else:
+            mine[: p.num_own, : 4 * k] = data_own.contiguous().view(torch.uint8).reshape(-1, 4 * k)
+            mine[: p.num_own, 4 * k:] = sel_own
+        table = self._buf(("ag_table", k), (self.world * max_own, 5 * k), torch.uint8)
+        work = ag(table, mine, async_op=True)
+        y = self.local_own.forward(data_own, sel_own, dim_origin)   # overlaps the all-gather
+        work.wait()
+        eng.forward_records(table, k, dim_origin, out=y, accumulate=True)
+        self._fwd_sel = sel_own
+        self._halo_part = torch.index_select(table[:, 4 * k:], 0, pos.long())
+        return y
+
+    def halo_bytes(self, k: int) -> dict:
+        """Bytes this rank receives per step in each exchange, both halo modes."""
+        p = self.plan
+        max_own = max(self.bounds[i + 1] - self.bounds[i] for i in range(self.world))
+        return {"records_fwd": p.num_halo * 5 * k,
+                "allgather_fwd": (self.world - 1) * max_own * 5 * k,
+                "reverse_bwd": p.num_halo * 4 * k}
 
     def _forward_overlap_rows(self, data_own, sel_own, dim_origin):
         p = self.plan
@@ -358,15 +477,20 @@ class PartitionedMaxK:
         travel while the own columns are computed."""
         sel = self._block_sel(sel_own, halo_sel)
         if not self.overlap_backward:
-            return self._return_halo(self.local.backward(grad_own, sel))
+            return self._return_halo(self._local_bwd(self.local, grad_own, sel))
         p = self.plan
         k = sel.shape[1]
-        dh = self.local_halo.backward(grad_own, sel[p.num_own:])
+        dh = self._local_bwd(self.local_halo, grad_own, sel[p.num_own:])
         back = self._buf(("back", k), (sum(p.send_counts), k), torch.float32)
         work = a2a(back, dh, p.send_counts, p.recv_counts, async_op=True)
-        own = self.local_own.backward(grad_own, sel[: p.num_own])   # overlaps the exchange
+        own = self._local_bwd(self.local_own, grad_own, sel[: p.num_own])   # overlaps the exchange
         work.wait()
         return self._add_returns(back, own)
+
+    def _local_bwd(self, eng, grad, sel):
+        if self.bwd_algo is None:
+            return eng.backward(grad, sel)
+        return eng.backward(grad, sel, algo=self.bwd_algo)
 
     # ------------------------------------------------- multi-relation (config 5)
     def forward_multi(self, data_own: torch.Tensor, sel_own: torch.Tensor,

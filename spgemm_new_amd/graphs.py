@@ -154,6 +154,15 @@ def synthetic_values(seed: int, e0: int, e1: int, device="cuda") -> torch.Tensor
     return bits.to(torch.float32) * (1.0 / (1 << 24))
 
 
+def synthetic_features(seed: int, r0: int, r1: int, dim: int, device="cuda") -> torch.Tensor:
+    """fp32 U(0,1) node features (or gradient rows) of rows [r0, r1), dim wide:
+    entry (r, c) is a hash of (seed, r * dim + c), so a rank of the row partition
+    generates exactly its rows of the whole matrix."""
+    pos = torch.arange(r0 * dim, r1 * dim, device=device, dtype=torch.int64)
+    bits = (_mix64(pos ^ _key(seed, 202)) >> 40) & ((1 << 24) - 1)
+    return (bits.to(torch.float32) * (1.0 / (1 << 24))).view(r1 - r0, dim)
+
+
 def synthetic_csr_gpu(num_rows: int, num_edges: int, seed: int = 123, device="cuda",
                       alpha: float = 2.2, self_loops: bool = False):
     """(indptr int32[V+1], indices int32[E]) on `device`; columns uniform in

@@ -187,13 +187,19 @@ def validate_spmm_maxk(warp4_metadata, indices, values, input_data, sparse_selec
 
 # --------------------------------------------------------------------- top-k
 def cuda_topk_maxk_float(input, k: int):
-    """Exact top-k -> (fp32 values[V,k], int32 indices[V,k]).  Replaces the lossy
-    uint8-quantised kernel (cuda_kernel_bindings.cpp:203-238)."""
+    """Top-k with the contract of cuda_kernel_bindings.cpp:203-238: float32 in ->
+    (fp32 values[V,k], int32 indices[V,k]), exact (the HIP CBSR producer in
+    torch.topk's order, not the lossy uint8-quantised kernel, SURVEY §2.4-5);
+    uint8 in -> (uint8 values, int32 indices) through the uint8 path."""
     check_tensor(input, "Input", dim=2)
     if not (0 < k <= input.size(1)):
         raise RuntimeError("Invalid k value")
-    x = input.float() if input.dtype != torch.float32 else input
-    vals, idx = topk_cbsr(x.contiguous(), k, order="value")  # HIP producer (dim <= 256)
+    if input.dtype == torch.uint8:
+        vals, idx = cuda_topk_maxk(input, k)
+        return vals, idx.to(torch.int32)
+    if input.dtype != torch.float32:
+        raise RuntimeError("Input must be float32 or uint8")
+    vals, idx = topk_cbsr(input.contiguous(), k, order="value")  # HIP producer (dim <= 256)
     return vals, idx.to(torch.int32)
 
 

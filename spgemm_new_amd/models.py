@@ -56,7 +56,9 @@ class SpGEMMFunction(Function):
         x = features.contiguous()
         data, sel = topk_cbsr(x, maxk, order="column")
         g = graph_for(indptr.contiguous(), indices.contiguous(), values.contiguous())
-        out = g.forward(data, sel, dim_origin=x.size(1))
+        # edge selectors only when this forward's backward will run
+        out = g.forward(data, sel, dim_origin=x.size(1),
+                        edge_sel="auto" if ctx.needs_input_grad[0] else False)
         ctx.graph = g
         ctx.sparse_selector = sel
         ctx.maxk = maxk

@@ -223,7 +223,7 @@ class MaxKGraph:
         self._bwd_choice = {}
         self._bwd_alt = {}        # AUTO's best algorithm other than STAGED_EDGE, per key
         self._esel_on = set()     # (k, h): forwards write edge selectors (AUTO chose STAGED_EDGE)
-        self._esel = []           # [(sel key, sel, uint8 buffer[E * k])], most recent last
+        self._esel = []           # [(sel key, sel, uint8 buffer[E * k], pinned)], most recent last
         self.last_bwd_algo = None
         self._blocked = {}        # column-blocked forward plans, per block count
         self._fwd_blocks = {}     # (k, h) -> block count chosen (0: plain forward)
@@ -323,7 +323,10 @@ class MaxKGraph:
         host read of the range count)."""
         if dim_k in self._local:
             plan = self._local[dim_k]
-            if plan is not None and plan["values_key"] != _tensor_key(self.values):
+            # under capture the gather is always recorded: replays see the graph's
+            # values as they are then, also after an in-place change
+            if plan is not None and (plan["values_key"] != _tensor_key(self.values)
+                                     or torch.cuda.is_current_stream_capturing()):
                 plan["edge_val"] = self.values[: self.num_edges][plan["perm"].long()].contiguous()
                 plan["values_key"] = _tensor_key(self.values)
             return plan
@@ -425,10 +428,17 @@ class MaxKGraph:
         in place or not, or per-call ones): one scatter of E values into the
         records (maxk_tile_plan_set_values) when they hold anything else.  While
         a hipGraph is captured the scatter is always recorded, so replays pick
-        up values changed between them."""
+        up values changed between them; once a capture has recorded it, every
+        eager call rewrites the records as well (a replay may have rewritten
+        them with other values than the ones the Python state names)."""
         key = _tensor_key(values)
-        if plan["values_key"] != key or plan["values_ref"] is not values or \
-                torch.cuda.is_current_stream_capturing():
+        capturing = torch.cuda.is_current_stream_capturing()
+        if capturing:
+            # a replay rewrites the records behind the Python state's back: from
+            # now on every eager call rewrites them too (ADVICE r2)
+            plan["captured_values"] = True
+        if plan["values_key"] != key or plan["values_ref"] is not values or capturing or \
+                plan.get("captured_values"):
             from . import tile
             tile.set_values(plan, values[: self.num_edges])
             plan["values_key"], plan["values_ref"] = key, values
@@ -448,27 +458,32 @@ class MaxKGraph:
         """The edge selectors of ``sel`` (uint8[E * k], CSR edge order) when a
         forward wrote them for this selector tensor (MAXK_BWD_STAGED_EDGE), else None."""
         key = _tensor_key(sel)
-        for k_, s_, buf in reversed(self._esel):
+        for k_, s_, buf, _ in reversed(self._esel):
             if k_ == key and s_ is sel:
                 return buf
         return None
 
     def _esel_slot(self, sel: torch.Tensor) -> torch.Tensor:
         """A buffer for the edge selectors of ``sel`` (recycles the oldest entry);
-        the entry holds ``sel`` so its address is not reused while cached."""
+        the entry holds ``sel`` so its address is not reused while cached.  A
+        buffer written under hipGraph capture is pinned: a replay rewrites it, so
+        no other selector tensor may ever be given it."""
         n = max(1, self.num_edges * sel.shape[1])
         key = _tensor_key(sel)
-        for i, (k_, s_, buf) in enumerate(self._esel):
+        pinned = torch.cuda.is_current_stream_capturing()
+        for i, (k_, s_, buf, pin) in enumerate(self._esel):
             if s_ is sel:
                 del self._esel[i]
+                pinned = pinned or pin
                 break
         else:
             buf = None
-            if len(self._esel) >= max(1, ESEL_CACHE):
-                _, _, buf = self._esel.pop(0)
+            free = [i for i, e in enumerate(self._esel) if not e[3]]
+            if not pinned and len(free) >= max(1, ESEL_CACHE):
+                _, _, buf, _ = self._esel.pop(free[0])
             if buf is None or buf.numel() < n:
                 buf = torch.empty(n, dtype=torch.uint8, device=self.device)
-        self._esel.append((key, sel, buf))
+        self._esel.append((key, sel, buf, pinned))
         return buf
 
     def make_edge_selectors(self, sel: torch.Tensor) -> torch.Tensor:
@@ -579,10 +594,13 @@ class MaxKGraph:
     # ---------------------------------------------------------------- compute
     def forward(self, cbsr_data: torch.Tensor, cbsr_sel: torch.Tensor, dim_origin: int = 256,
                 out: torch.Tensor | None = None, values: torch.Tensor | None = None,
-                accumulate: bool = False, edge_sel: bool | None = None) -> torch.Tensor:
+                accumulate: bool = False, edge_sel: bool | str = False) -> torch.Tensor:
         """Y = A . scatter(CBSR)  (spmm_maxk.cu:17-106).  Returns fp32[V, dim_origin];
         accumulate=True adds into out instead.  edge_sel: also write the edge
-        selectors for the STAGED_EDGE backward (None: when AUTO chose it)."""
+        selectors for a STAGED_EDGE / EDGE_GATHER backward of this same selector
+        tensor -- "auto": when AUTO chose such a backward for (k, h); only a
+        caller that runs that backward next should ask (the autograd Function
+        does when the input needs a gradient), else the E*k bytes are wasted."""
         return spgemm_forward(self, cbsr_data, cbsr_sel, dim_origin, out, values, accumulate,
                               edge_sel)
 
@@ -744,9 +762,10 @@ def _check_cbsr(g: MaxKGraph, data, sel):
 
 
 def spgemm_forward(g: MaxKGraph, data, sel, dim_origin: int = 256, out=None, values=None,
-                   accumulate: bool = False, edge_sel: bool | None = None):
+                   accumulate: bool = False, edge_sel: bool | str = False):
     """edge_sel: also write the edge selectors of sel (kept by the graph for the
-    STAGED_EDGE backward); None = when AUTO chose that backward for (k, h)."""
+    STAGED_EDGE / EDGE_GATHER backward); "auto" = when AUTO chose such a backward
+    for (k, h)."""
     _check_cbsr(g, data, sel)
     k = data.shape[1]
     values = _check_values(g, values)
@@ -762,7 +781,7 @@ def spgemm_forward(g: MaxKGraph, data, sel, dim_origin: int = 256, out=None, val
     L = _lib.load()
     nbytes = L.maxk_forward_workspace_bytes(g.num_panels, dim_origin)
     ws = g._workspace(("fwd", dim_origin), nbytes)
-    if edge_sel is None:
+    if edge_sel == "auto":
         edge_sel = (k, dim_origin) in g._esel_on
     edge_sel = edge_sel and not accumulate and g.num_edges > 0
     rs = L.maxk_cbsr_packed_row_bytes(k) if FWD_PACKED and not accumulate else 0

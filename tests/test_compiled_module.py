@@ -63,6 +63,13 @@ def test_compiled_module_matches_oracle(dev, oracle, k):
     vals, idx = m.cuda_topk_maxk_float(x, k)
     ref = torch.topk(x, k, dim=1)
     assert torch.equal(vals, ref.values) and torch.equal(idx.long(), ref.indices)
+    assert isinstance(m.cuda_topk_maxk_float(x, k), tuple)
+    # uint8 input keeps uint8 values, int32 indices (cuda_kernel_bindings.cpp:226-233)
+    xu = (x * 255).round().to(torch.uint8)
+    for mod in (m, py_mod):
+        vu, iu = mod.cuda_topk_maxk_float(xu, k)
+        assert vu.dtype == torch.uint8 and iu.dtype == torch.int32
+        assert torch.equal(vu, torch.topk(xu.int(), k, dim=1).values.to(torch.uint8))
     t = m.CudaTimer()
     t.start()
     assert t.stop() >= 0.0

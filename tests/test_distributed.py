@@ -488,3 +488,66 @@ def test_partitioned_full_size_two_ranks_one_gpu(graph, R):
     lhs, rhs, halo = q.get(timeout=5)
     assert halo > 0
     assert abs(lhs - rhs) / abs(lhs) <= 1e-6, (lhs, rhs)
+
+
+def _allgather_worker(rank, world, port, q, k):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from spgemm_new_amd.distributed import PartitionedMaxK
+        indptr, indices = small_csr(900, seed=4)
+        v, h = len(indptr) - 1, 64
+        values = np.random.default_rng(1).random(len(indices), dtype=np.float32)
+        data, sel = random_cbsr(v, k, h, seed=2)
+        grad = np.random.default_rng(3).random((v, h), dtype=np.float32)
+        args = (torch.from_numpy(indptr), torch.from_numpy(indices), torch.from_numpy(values),
+                rank, world, "cpu")
+        m_rec = PartitionedMaxK(*args, engine=OracleEngine, halo_mode="records")
+        m_ag = PartitionedMaxK(*args, engine=OracleEngine, halo_mode="allgather")
+        m_auto = PartitionedMaxK(*args, engine=OracleEngine)
+        d_l, s_l = m_rec.local_rows(torch.from_numpy(data)), m_rec.local_rows(torch.from_numpy(sel))
+        g_l = m_rec.local_rows(torch.from_numpy(grad))
+        y_r, y_a = m_rec.forward(d_l, s_l, h), m_ag.forward(d_l, s_l, h)
+        dx_r, dx_a = m_rec.backward(g_l, s_l), m_ag.backward(g_l, s_l)
+        same = torch.equal(y_r, y_a) and torch.equal(dx_r, dx_a) and \
+            torch.equal(m_rec.last_halo_selectors(), m_ag.last_halo_selectors())
+        ys, dxs = [None] * world, [None] * world
+        dist.all_gather_object(ys, y_a.numpy())
+        dist.all_gather_object(dxs, dx_a.numpy())
+        flags = [None] * world
+        dist.all_gather_object(flags, (same, m_auto.halo_mode, m_ag.halo_bytes(k)))
+        if rank == 0:
+            from oracle import oracle as O
+            ey = O.parity_error(np.concatenate(ys), O.np_forward(indptr, indices, values, data, sel, h))
+            ed = O.parity_error(np.concatenate(dxs),
+                                O.np_backward(indptr, indices, values, grad, sel))
+            q.put((ey, ed, flags))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [2, 3, 8])
+def test_allgather_halo_mode_bitwise_equals_records(world):
+    """SURVEY.md §8e's all-gather fallback: the forward all-gathers the whole CBSR
+    (records) instead of the halo all-to-all-v and the halo part reads it in
+    place -- Y, dXs and the saved halo selectors bitwise equal to the records
+    path, and both equal the oracle; "auto" picks it when a halo covers more
+    than 75 % of V, the same choice on every rank."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    k = 8
+    procs = [ctx.Process(target=_allgather_worker, args=(r, world, port, q, k))
+             for r in range(world)]
+    for p in procs:
+        p.start()
+    for p in procs:
+        p.join(timeout=240)
+    assert all(p.exitcode == 0 for p in procs), [p.exitcode for p in procs]
+    ey, ed, flags = q.get(timeout=5)
+    assert ey <= 1e-4 and ed <= 1e-4
+    assert all(f[0] for f in flags), flags
+    assert len({f[1] for f in flags}) == 1          # one collective on every rank
+    for same, mode, nbytes in flags:
+        assert nbytes["allgather_fwd"] >= nbytes["records_fwd"] > 0

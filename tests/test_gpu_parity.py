@@ -975,7 +975,9 @@ def test_staged_edge_auto_flow(dev, g_small):
     data, sel = random_cbsr(v, k, h, seed=3)
     d, s = T(data, dev), T(sel, dev)
     grad = T(np.random.default_rng(4).random((v, h), dtype=np.float32), dev)
-    g.forward(d, s, h)                        # writes the edge selectors of s
+    g.forward(d, s, h)                        # default: no edge selectors
+    assert g.edge_selectors(s) is None
+    g.forward(d, s, h, edge_sel="auto")       # a training forward: writes those of s
     a = g.backward(grad, s)
     assert g.last_bwd_algo == "staged_edge"
     s2 = s.clone()                            # no forward wrote its edge selectors

@@ -1,0 +1,172 @@
+"""The row-partitioned HIP path pinned against the unpartitioned one at the
+BASELINE shapes and rank counts.
+
+BASELINE config 4 (ogbn-products-shaped, k = 32) at world 2, 4 and 8 and
+config 5 (ogbn-proteins-shaped, R = 8 relations) at world 8, every rank on
+cuda:0 (gloo stands in for RCCL: the exchange is staged through host memory).
+Each rank generates only its block -- columns, edge values, features and
+gradient rows are hashes of global ids (graphs.synthetic_*), so the blocks are
+rows of the single-GPU graph -- runs forward + backward through
+PartitionedMaxK, and its own rows of Y and dXs are compared per element with a
+single MaxKGraph over the whole graph (per row: spmm_maxk.cu:17-106 and
+spmm_maxk_backward.cu:15-115 semantics), within 1e-4 relative.  A consistent
+halo-renumbering error (a permuted send list, a wrong owner) changes rows and
+fails here, which the adjoint identity alone could not see.  Also checked:
+with the local backward pinned to one algorithm, dXs with the overlapped
+backward (own / halo parts) is bitwise the single block's."""
+import multiprocessing as mp
+import os
+import socket
+
+import pytest
+import torch
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+TOL = 1e-4
+H, K, SEED = 256, 32, 123
+SEED_X, SEED_G = 1001, 2002
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _values(R, e0, e1, dev):
+    from spgemm_new_amd.graphs import synthetic_values
+    if R == 1:
+        return synthetic_values(SEED, e0, e1, device=dev)
+    return torch.stack([synthetic_values(SEED + 7 + q, e0, e1, device=dev) for q in range(R)],
+                       1).contiguous()
+
+
+def _grad(R, r0, r1, dev):
+    from spgemm_new_amd.graphs import synthetic_features
+    if R == 1:
+        return synthetic_features(SEED_G, r0, r1, H, dev)
+    return torch.stack([synthetic_features(SEED_G + q, r0, r1, H, dev) for q in range(R)])
+
+
+def _worker(rank, world, port, graph, R, outdir, q):
+    import sys
+    sys.path.insert(0, ROOT)
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    import torch.distributed as dist
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from spgemm_new_amd import _lib
+        from spgemm_new_amd.distributed import PartitionedMaxK, row_partition
+        from spgemm_new_amd.graphs import (CONFIGS, synthetic_columns, synthetic_features,
+                                           synthetic_indptr)
+        from spgemm_new_amd.ops import topk_cbsr
+        dev = torch.device("cuda", 0)
+        torch.cuda.set_device(dev)
+        V, E = CONFIGS[graph]
+        indptr = synthetic_indptr(V, E, seed=SEED, device=dev)
+        b = row_partition(indptr, world)
+        r0, r1 = b[rank], b[rank + 1]
+        e0, e1 = int(indptr[r0]), int(indptr[r1])
+        cols = synthetic_columns(indptr, seed=SEED, rows=(r0, r1))
+        vals = _values(R, e0, e1, dev)
+        data, sel = topk_cbsr(synthetic_features(SEED_X, r0, r1, H, dev), K)
+        G = _grad(R, r0, r1, dev)
+        staged = _lib.MAXK_BWD_STAGED
+        m = PartitionedMaxK(indptr, cols, vals, rank, world, dev, local_block=True,
+                            bwd_algo=None if R > 1 else staged)
+        if R == 1:
+            y = m.forward(data, sel, H)
+            dx = m.backward(G, sel)
+            assert m.overlap_backward
+            # the single-block backward (no own / halo split), same local algorithm
+            m1 = PartitionedMaxK(indptr, cols, vals, rank, world, dev, local_block=True,
+                                 overlap=False, bwd_algo=staged)
+            y1 = m1.forward(data, sel, H)
+            dx1 = m1.backward(G, sel)
+            bitwise = bool(torch.equal(dx, dx1))
+            fwd_split = float(((y - y1).abs() / y1.abs().clamp_min(1)).max())
+        else:
+            y = m.forward_multi(data, sel, H)
+            dx = m.backward_multi(G, sel)
+            bitwise, fwd_split = True, 0.0
+        torch.cuda.synchronize()
+        torch.save({"r0": r0, "r1": r1, "y": y.cpu(), "dx": dx.cpu(), "halo": m.plan.num_halo},
+                   os.path.join(outdir, f"rank{rank}.pt"))
+        flags = torch.tensor([float(not bitwise), fwd_split])
+        dist.all_reduce(flags, op=dist.ReduceOp.MAX)
+        if rank == 0:
+            q.put(flags.tolist())
+    finally:
+        dist.destroy_process_group()
+
+
+_REF = {}
+
+
+def _reference(graph, R):
+    """Y and dXs of the whole graph on one GPU (single MaxKGraph), cached per graph."""
+    key = (graph, R)
+    if key not in _REF:
+        import spgemm_new_amd as S
+        from spgemm_new_amd import _lib
+        from spgemm_new_amd.graphs import (CONFIGS, synthetic_columns, synthetic_features,
+                                           synthetic_indptr)
+        from spgemm_new_amd.ops import topk_cbsr
+        dev = torch.device("cuda", 0)
+        V, E = CONFIGS[graph]
+        indptr = synthetic_indptr(V, E, seed=SEED, device=dev)
+        indices = synthetic_columns(indptr, seed=SEED)
+        vals = _values(R, 0, E, dev)
+        data, sel = topk_cbsr(synthetic_features(SEED_X, 0, V, H, dev), K)
+        G = _grad(R, 0, V, dev)
+        if R == 1:
+            g = S.MaxKGraph(indptr, indices, vals)
+            y = g.forward(data, sel, H)
+            dx = g.backward(G, sel, algo=_lib.MAXK_BWD_STAGED)
+        else:
+            g = S.MaxKGraph(indptr, indices, vals[:, 0].contiguous())
+            y = g.forward_multi(data, sel, vals, H)
+            dx = g.backward_multi(G, sel, vals)
+        torch.cuda.synchronize()
+        _REF.clear()
+        _REF[key] = (y.cpu(), dx.cpu())
+        del g, y, dx, G, data, sel, vals, indices, indptr
+        torch.cuda.empty_cache()
+    return _REF[key]
+
+
+def _rel_err(a, b):
+    return float(((a - b).abs() / b.abs().clamp_min(1)).max()) if b.numel() else 0.0
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("graph,world,R", [("products", 2, 1), ("products", 4, 1),
+                                           ("products", 8, 1), ("proteins", 8, 8)])
+def test_partitioned_rows_match_single_gpu(graph, world, R, tmp_path):
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, world, port, graph, R, str(tmp_path), q))
+             for r in range(world)]
+    for p in procs:
+        p.start()
+    for p in procs:
+        p.join(timeout=600)
+    assert all(p.exitcode == 0 for p in procs), [p.exitcode for p in procs]
+    not_bitwise, fwd_split = q.get(timeout=5)
+    assert not_bitwise == 0.0, "overlapped backward differs bitwise from the single block"
+    assert fwd_split <= TOL
+    y_ref, dx_ref = _reference(graph, R)
+    rows = 0
+    for r in range(world):
+        part = torch.load(os.path.join(str(tmp_path), f"rank{r}.pt"), weights_only=True)
+        r0, r1 = part["r0"], part["r1"]
+        rows += r1 - r0
+        assert part["halo"] > 0
+        yr = y_ref[r0:r1] if R == 1 else y_ref[:, r0:r1]
+        assert part["y"].shape == yr.shape
+        assert _rel_err(part["y"], yr) <= TOL, (r, _rel_err(part["y"], yr))
+        assert _rel_err(part["dx"], dx_ref[r0:r1]) <= TOL, (r, _rel_err(part["dx"], dx_ref[r0:r1]))
+    assert rows == y_ref.shape[-2]

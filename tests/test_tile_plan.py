@@ -212,6 +212,83 @@ def test_tile_capture_sees_value_changes(dev):
 
 
 @pytest.mark.gpu
+def test_tile_capture_then_foreign_values(dev):
+    """a replay rewrites the TILE records with the graph's own values
+    behind the Python state.  Sequence: capture with own values, eager with
+    foreign values w, replay, eager with w again -- the last eager call must
+    use w (the records are rewritten on every eager call once captured)."""
+    import spgemm_new_amd as S
+    V = 3000
+    indptr, idx, vals = _graph(V, V, 40, seed=11)
+    grad, sel = _inputs(V, V, seed=11)
+    g = S.MaxKGraph(torch.from_numpy(indptr).to(dev), torch.from_numpy(idx).to(dev),
+                    torch.from_numpy(vals).to(dev))
+    G, sl = torch.from_numpy(grad).to(dev), torch.from_numpy(sel).to(dev)
+    w = torch.rand(idx.size, device=dev)
+    dx = torch.empty((V, 32), device=dev)
+    g.backward(G, sl, out=dx, algo=S._lib.MAXK_BWD_TILE)
+    torch.cuda.synchronize()
+    graph = torch.cuda.CUDAGraph()
+    stream = torch.cuda.Stream()
+    stream.wait_stream(torch.cuda.current_stream())
+    with torch.cuda.stream(stream):
+        with torch.cuda.graph(graph, stream=stream):
+            g.backward(G, sl, out=dx, algo=S._lib.MAXK_BWD_TILE)
+    torch.cuda.current_stream().wait_stream(stream)
+    ref_own = g.backward(G, sl, algo=S._lib.MAXK_BWD_STAGED)
+    ref_w = g.backward(G, sl, values=w, algo=S._lib.MAXK_BWD_STAGED)
+
+    def close(a, b):
+        return (a - b).abs().max().item() <= 1e-4 * max(1.0, b.abs().max().item())
+    assert close(g.backward(G, sl, values=w, algo=S._lib.MAXK_BWD_TILE), ref_w)
+    graph.replay()
+    torch.cuda.synchronize()
+    assert close(dx, ref_own)
+    assert close(g.backward(G, sl, values=w, algo=S._lib.MAXK_BWD_TILE), ref_w)
+    assert close(g.backward(G, sl, algo=S._lib.MAXK_BWD_TILE), ref_own)
+
+
+@pytest.mark.gpu
+def test_edge_selector_buffer_pinned_under_capture(dev):
+    """an edge-selector buffer written under capture is never handed to
+    another selector tensor (a replay would overwrite it between that tensor's
+    eager forward and backward)."""
+    import spgemm_new_amd as S
+    from spgemm_new_amd import ops
+    V = 3000
+    indptr, idx, vals = _graph(V, V, 40, seed=12)
+    g = S.MaxKGraph(torch.from_numpy(indptr).to(dev), torch.from_numpy(idx).to(dev),
+                    torch.from_numpy(vals).to(dev))
+    k, h = 16, 256
+    gen = torch.Generator(device=dev)
+    gen.manual_seed(3)
+    sels = [torch.argsort(torch.rand((V, h), generator=gen, device=dev), 1)[:, :k].sort(1)
+            .values.to(torch.uint8).contiguous() for _ in range(ops.ESEL_CACHE + 2)]
+    data = torch.rand((V, k), generator=gen, device=dev)
+    y = torch.empty((V, h), device=dev)
+    g.forward(data, sels[0], h, out=y, edge_sel=True)    # outside: a plain slot
+    torch.cuda.synchronize()
+    graph = torch.cuda.CUDAGraph()
+    stream = torch.cuda.Stream()
+    stream.wait_stream(torch.cuda.current_stream())
+    with torch.cuda.stream(stream):
+        with torch.cuda.graph(graph, stream=stream):
+            g.forward(data, sels[1], h, out=y, edge_sel=True)
+    torch.cuda.current_stream().wait_stream(stream)
+    pinned = g.edge_selectors(sels[1])
+    assert pinned is not None
+    for s in sels[2:]:                                    # more than the cache holds
+        g.forward(data, s, h, out=y, edge_sel=True)
+        assert g.edge_selectors(s).data_ptr() != pinned.data_ptr()
+    assert g.edge_selectors(sels[1]) is pinned
+    graph.replay()
+    torch.cuda.synchronize()
+    es = g.edge_selectors(sels[-1]).view(-1)[: idx.size * k].view(idx.size, k)
+    ref = sels[-1][torch.from_numpy(idx).to(dev).long()]
+    assert torch.equal(es, ref)
+
+
+@pytest.mark.gpu
 @pytest.mark.parametrize("V,C,deg,k", [(3000, 3000, 40, 32), (9000, 9000, 120, 32),
                                        (3000, 5000, 60, 32), (4000, 1500, 30, 32),
                                        (3000, 3000, 40, 64), (5000, 2500, 50, 64)])

@@ -70,8 +70,22 @@ def main(tag: str, root: str = ".", workload: str | None = None):
 
         per_launch = {n: r["hbm_read_bytes_x2"] + r["hbm_write_bytes"] for n, r in k.items()
                       if "hbm_read_bytes_x2" in r and "hbm_write_bytes" in r}
-        # bench.py composes a call's traffic from these (launches per call known there)
-        idx[workload] = {"profile": tag, "kernels": per_launch}
+        # bench.py composes a call's traffic from these (launches per call known there);
+        # the entry is keyed to the kernel sources it measured (bench.py refuses a
+        # profile whose key differs from the tree's), so it must be summarised from
+        # the same tree that ran the profile
+        sys.path.insert(0, os.path.abspath(root))
+        from bench import kernel_source_sha
+        issue = {}
+        for n, r in k.items():
+            c = {x: r[x] for x in ("avg_ms", "GRBM_GUI_ACTIVE", "SQ_INSTS_SALU", "SQ_INSTS_VALU",
+                                   "SQ_INSTS_SMEM", "SQ_INSTS_LDS", "SQ_LDS_IDX_ACTIVE",
+                                   "SQ_WAIT_INST_ANY", "SQ_WAIT_ANY", "SQ_ACTIVE_INST_ANY",
+                                   "SQ_WAVE_CYCLES", "SQ_BUSY_CYCLES") if x in r}
+            if "GRBM_GUI_ACTIVE" in c and len(c) > 2:
+                issue[n] = c
+        idx[workload] = {"profile": tag, "source_sha": kernel_source_sha(os.path.abspath(root)),
+                         "kernels": per_launch, "issue": issue}
         json.dump(idx, open(idx_path, "w"), indent=1)
     with open(os.path.join(dst, f"{tag}_summary.md"), "w") as fh:
         fh.write(f"# rocprofv3 summary `{tag}`\n\nSource: `tools/profile.sh {tag}` "
