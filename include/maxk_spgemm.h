@@ -358,10 +358,11 @@ int maxk_sspmm_backward_tile(const void *headers, const int64_t *header_start,
  *    groups of <= 2048 (k = 32) / 1024 (k = 64) destinations and source
  *    ranges so that about one workgroup runs per CU.
  *  maxk_tile_plan_build: call once with headers == NULL (count call): writes
- *    sizes (host int64[3]) = {header entries, records (int32x2), largest
+ *    sizes (host int64[3]) = {header entries, records, largest
  *    padded per-segment record count}; the plan is usable only if sizes[2] <=
  *    65535.  Then call with headers int32x4[sizes[0]], header_start
- *    int64[G*S*16], records int32x2[sizes[1]], record_start int64[G*S*16],
+ *    int64[G*S*16], records int32 x maxk_tile_record_words() each [sizes[1]],
+ *    record_start int64[G*S*16],
  *    num_chunks int32[G*S] and optionally edge_record int32[E] (the record of
  *    each CSR edge, for maxk_tile_plan_set_values).  Both calls synchronise
  *    the stream once.  Deterministic: records keep CSR order per segment.
@@ -372,6 +373,8 @@ int maxk_tile_plan_shape(int num_cols, int num_cus, int dim_k, int *num_groups, 
 /* The plan format the library was built with (host out): LDS ring buffers and rows per
  * buffer (chunks hold rows - 1 source rows; the header stream leads by buffers - 1). */
 int maxk_tile_format(int *num_buffers, int *buffer_rows);
+/* int32 words per TILE record in this build (2 or 4; tile_format.h). */
+int maxk_tile_record_words(void);
 size_t maxk_tile_plan_workspace_bytes(int64_t num_edges, int num_workgroups);
 int maxk_tile_plan_build(const int32_t *indptr, const int32_t *indices, const float *values,
                          int num_rows, int num_cols, int64_t num_edges, int dim_k, int num_groups,

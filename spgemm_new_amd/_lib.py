@@ -65,6 +65,7 @@ SIGNATURES = {
     "maxk_sspmm_backward_tile": (_I, [_P, _P, _P, _P, _P, _I, _I, _I, _P, _P, _P, _I, _I, _I, _I,
                                       _P, _P, _P]),
     "maxk_tile_format": (_I, [ctypes.POINTER(_I), ctypes.POINTER(_I)]),
+    "maxk_tile_record_words": (_I, []),
     "maxk_blocked_plan_workspace_bytes": (_S, [_L, _I, _I]),
     "maxk_blocked_plan_build": (_I, [_P, _P, _P, _I, _I, _L, _I, _P, _P, _P, _P, _P, _S, _P]),
     "maxk_permute_f32": (_I, [_P, _P, _L, _P, _P]),

@@ -427,10 +427,31 @@ __global__ void tile_headers_kernel(const int32_t *__restrict__ chunk_base,
     hdrs[t] = out;
 }
 
-__global__ void tile_records_init_kernel(int2 *__restrict__ recs, int64_t capacity)
+// the record of (slot, staged row index in the ring, value) in the build's format
+__device__ __forceinline__ void tile_put_record(uint32_t *__restrict__ recs, int64_t pos, int slot,
+                                                int ring_row, float value)
+{
+    uint32_t *r = recs + pos * kTileRecWords;
+    if constexpr (kTileRecWords == 2) {
+        r[0] = (uint32_t)slot | ((uint32_t)ring_row << 24);
+        r[1] = __float_as_uint(value);
+    } else {
+        // v_perm_b32 selector control: byte 0 = selector register index (slot / 4,
+        // M0 for the indexed read; also D's byte 0 selector, don't care), byte 1 =
+        // 0x0c (D byte 1 = 0), byte 2 = 4 + slot % 4 (D byte 2 = that byte of the
+        // indexed selector register), byte 3 = 0x0c (D byte 3 = 0)
+        r[0] = (uint32_t)(slot >> 2) | (0x0cu << 8) | ((uint32_t)(4 + (slot & 3)) << 16) |
+               (0x0cu << 24);
+        r[1] = (uint32_t)slot;
+        r[2] = (uint32_t)ring_row << 10;  // LDS byte address of the staged row
+        r[3] = __float_as_uint(value);
+    }
+}
+
+__global__ void tile_records_init_kernel(uint32_t *__restrict__ recs, int64_t capacity)
 {
     const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (t < capacity) recs[t] = make_int2((kTileBufRows - 1) << 24, 0);  // slot 0, zero row, 0
+    if (t < capacity) tile_put_record(recs, t, 0, kTileBufRows - 1, 0.f);  // slot 0, zero row, 0
 }
 
 __global__ void tile_records_kernel(const int32_t *__restrict__ segs, const int32_t *__restrict__ perm2,
@@ -440,7 +461,7 @@ __global__ void tile_records_kernel(const int32_t *__restrict__ segs, const int3
                                     const int32_t *__restrict__ indices,
                                     const float *__restrict__ values,
                                     const int64_t *__restrict__ rec_off, int GS, int k, int64_t n,
-                                    int64_t capacity, int2 *__restrict__ recs,
+                                    int64_t capacity, uint32_t *__restrict__ recs,
                                     int32_t *__restrict__ edge_record)
 {
     const int64_t j = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
@@ -453,18 +474,17 @@ __global__ void tile_records_kernel(const int32_t *__restrict__ segs, const int3
     tile_edge_place(e, wgs[i], uidx[i] - 1, indices, wg_start, GS, k, wave, slot, half, chunk, rin);
     const int64_t pos = rec_off[s] + (j - first);
     if (pos >= capacity) return;
-    const uint32_t w0 =
-        (uint32_t)slot | ((uint32_t)((chunk % kTileBufs) * kTileBufRows + rin) << 24);
-    recs[pos] = make_int2((int)w0, __float_as_int(values[e]));
+    tile_put_record(recs, pos, slot, (chunk % kTileBufs) * kTileBufRows + rin, values[e]);
     if (edge_record) edge_record[e] = (int32_t)pos;
 }
 
 __global__ void tile_set_values_kernel(const int32_t *__restrict__ edge_record,
                                        const float *__restrict__ values, int64_t n,
-                                       int2 *__restrict__ recs)
+                                       uint32_t *__restrict__ recs)
 {
     const int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (e < n) recs[edge_record[e]].y = __float_as_int(values[e]);
+    if (e < n)
+        recs[(int64_t)edge_record[e] * kTileRecWords + kTileRecWords - 1] = __float_as_uint(values[e]);
 }
 
 size_t inclusive_scan_temp_bytes(int64_t n)
@@ -701,6 +721,8 @@ int maxk_tile_format(int *num_buffers, int *buffer_rows)
     return MAXK_OK;
 }
 
+int maxk_tile_record_words(void) { return kTileRecWords; }
+
 int maxk_tile_plan_shape(int num_cols, int num_cus, int dim_k, int *num_groups, int *group_size,
                          int *splits)
 {
@@ -832,10 +854,10 @@ int maxk_tile_plan_build(const int32_t *indptr, const int32_t *indices, const fl
                            dim3(kThreads), 0, st, chunk_base, wg_start, urow, pad, NWG,
                            header_capacity, static_cast<int4 *>(headers));
         hipLaunchKernelGGL(tile_records_init_kernel, dim3((unsigned)blocks_for(record_capacity)),
-                           dim3(kThreads), 0, st, static_cast<int2 *>(records), record_capacity);
+                           dim3(kThreads), 0, st, static_cast<uint32_t *>(records), record_capacity);
         hipLaunchKernelGGL(tile_records_kernel, dim3(eb), dim3(kThreads), 0, st, segs, perm2, perm,
                            wgs, uidx, wg_start, indices, values, rec_off, group_size, dim_k, E,
-                           record_capacity, static_cast<int2 *>(records), edge_record);
+                           record_capacity, static_cast<uint32_t *>(records), edge_record);
         if ((rc = launch_status())) return rc;
     }
     e = hipMemcpyAsync(sizes, dsizes, 3 * sizeof(int64_t), hipMemcpyDeviceToHost, st);
@@ -853,7 +875,7 @@ int maxk_tile_plan_set_values(const int32_t *edge_record, const float *values, i
     if (num_edges == 0) return MAXK_OK;
     hipLaunchKernelGGL(tile_set_values_kernel, dim3((unsigned)blocks_for(num_edges)), dim3(kThreads),
                        0, static_cast<hipStream_t>(stream), edge_record, values, num_edges,
-                       static_cast<int2 *>(records));
+                       static_cast<uint32_t *>(records));
     return launch_status();
 }
 

@@ -27,6 +27,7 @@
 //  * wave64 everywhere; no CUDA-isms, no warp32 tiling.
 #include <hip/hip_runtime.h>
 #include <stdint.h>
+#include <stdlib.h>
 
 #include "../../include/maxk_spgemm.h"
 #include "tile_format.h"
@@ -1908,6 +1909,37 @@ typedef unsigned tile_sel_t __attribute__((ext_vector_type(16)));
 typedef int tile_hdr_t __attribute__((ext_vector_type(4)));
 typedef uint32_t tile_g16_t __attribute__((ext_vector_type(16)));
 
+// The wave's three pieces of a chunk by range-checked buffer LDS-DMA: lane l of
+// piece i loads 16 B at byte offset off_i (row * 1024 + 16 l) of the gradient
+// (descriptor rsrc: base G, num_records = its bytes) into LDS at lds_byte +
+// 1024 i + 16 l.  A zero-row piece carries an offset past the end (row -1:
+// 0xFFFFFC00 + 16 l >= num_records), which the range check turns into zeros
+// without any memory access.  soffset is the constant 0 (it is not range
+// checked); the descriptor is built from kernel arguments once (no fresh
+// readfirstlane SGPRs, so no VALU->SGPR->VMEM wait states are needed); M0 (the
+// LDS address) is written by SALU and read after one wait state (s_nop 0).
+// Always three VMEM operations per call, as the counted vmcnt requires.
+typedef int32_t tile_rsrc_t __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ void tile_bdma3(tile_rsrc_t rsrc, uint32_t off0, uint32_t off1,
+                                           uint32_t off2, uint32_t lds_byte)
+{
+    uint32_t keep;
+    asm volatile("s_mov_b32 %0, m0\n\t"
+                 "s_mov_b32 m0, %5\n\t"
+                 "s_nop 0\n\t"
+                 "buffer_load_dwordx4 %1, %4, 0 offen lds\n\t"
+                 "s_add_u32 m0, m0, 0x400\n\t"
+                 "s_nop 0\n\t"
+                 "buffer_load_dwordx4 %2, %4, 0 offen lds\n\t"
+                 "s_add_u32 m0, m0, 0x400\n\t"
+                 "s_nop 0\n\t"
+                 "buffer_load_dwordx4 %3, %4, 0 offen lds\n\t"
+                 "s_mov_b32 m0, %0"
+                 : "=&s"(keep)
+                 : "v"(off0), "v"(off1), "v"(off2), "s"(rsrc), "s"(lds_byte)
+                 : "memory", "scc");
+}
+
 __device__ __forceinline__ void tile_glds(const float *g, uint32_t lds_byte)
 {
     uint32_t keep;
@@ -2270,6 +2302,301 @@ __device__ __forceinline__ void tile_group_loop(const uint32_t *rb, uint32_t ro,
         : "memory", "scc", "s64", "s65", "s66", "s67", "s68", "s69", "s70", "s71", "s72", "s73", "s74", "s75", "s76", "s77", "s78", "s79", "s80", "s81", "s82", "s83", "s84", "s85", "s86", "s87", "s88", "s89", "s90", "s91");
 }
 
+// TILE_REC_WORDS = 4 (tile_format.h): record = {v_perm control, slot, row's LDS
+// byte address, value}.  Per record: the selector byte by one v_perm_b32 of the
+// selector register picked by s_set_gpr_idx (SRC0, index = control byte 0,
+// the byte picked by control byte 2 lands in byte 2, bytes 1 / 3 are zero), so
+// address = (perm >> 14) + row; one ds_read_b32; v_fma_f32 into the slot
+// register picked by s_set_gpr_idx (SRC2 | DST).  No scalar shifts: per group
+// of four records 10 gpr-index instructions plus the exec and count updates
+// (the two-word format spends 12 more on field shifts).  Records sit in
+// pinned SGPRs: the two groups loaded before the chunk's barrier in s[64:79]
+// and s[80:95] (the loop below reuses them).
+__device__ __forceinline__ void tile_groups2_r16(const tile_g16_t &pa, const tile_g16_t &pb,
+                                                 uint32_t &n, uint32_t &m, uint64_t lo, uint64_t hi,
+                                                 tile_sel_t &selv, tile_acc_t &acc0,
+                                                 tile_acc_t &acc1)
+{
+    uint32_t t0, t1, t2, t3, t4, t5, t6, t7;
+    uint64_t ex;
+    asm volatile(
+        "s_waitcnt lgkmcnt(0)\n\t"
+        "s_cmp_eq_u32 %[n], 0\n\t"
+        "s_cbranch_scc1 .Lr2_done%=\n\t"
+        "s_mov_b64 %[ex], exec\n\t"
+        "s_cmp_lt_i32 %[m], 0\n\t"
+        "s_cselect_b64 exec, %[lo], %[hi]\n\t"
+        "s_set_gpr_idx_on s64, gpr_idx(SRC0)\n\t"
+        "v_perm_b32 %[t0], v48, 0, s64\n\t"
+        "s_set_gpr_idx_idx s68\n\t"
+        "v_perm_b32 %[t1], v48, 0, s68\n\t"
+        "s_set_gpr_idx_idx s72\n\t"
+        "v_perm_b32 %[t2], v48, 0, s72\n\t"
+        "s_set_gpr_idx_idx s76\n\t"
+        "v_perm_b32 %[t3], v48, 0, s76\n\t"
+        "s_set_gpr_idx_off\n\t"
+        "v_lshrrev_b32 %[t0], 14, %[t0]\n\t"
+        "v_lshrrev_b32 %[t1], 14, %[t1]\n\t"
+        "v_lshrrev_b32 %[t2], 14, %[t2]\n\t"
+        "v_lshrrev_b32 %[t3], 14, %[t3]\n\t"
+        "v_add_u32 %[t0], s66, %[t0]\n\t"
+        "v_add_u32 %[t1], s70, %[t1]\n\t"
+        "v_add_u32 %[t2], s74, %[t2]\n\t"
+        "v_add_u32 %[t3], s78, %[t3]\n\t"
+        "ds_read_b32 %[t0], %[t0]\n\t"
+        "ds_read_b32 %[t1], %[t1]\n\t"
+        "ds_read_b32 %[t2], %[t2]\n\t"
+        "ds_read_b32 %[t3], %[t3]\n\t"
+        "s_cmp_eq_u32 %[n], -1\n\t"
+        "s_cbranch_scc1 .Lr2_one%=\n\t"
+        "s_cmp_lt_i32 %[m], -1\n\t"
+        "s_cselect_b64 exec, %[lo], %[hi]\n\t"
+        "s_set_gpr_idx_on s80, gpr_idx(SRC0)\n\t"
+        "v_perm_b32 %[t4], v48, 0, s80\n\t"
+        "s_set_gpr_idx_idx s84\n\t"
+        "v_perm_b32 %[t5], v48, 0, s84\n\t"
+        "s_set_gpr_idx_idx s88\n\t"
+        "v_perm_b32 %[t6], v48, 0, s88\n\t"
+        "s_set_gpr_idx_idx s92\n\t"
+        "v_perm_b32 %[t7], v48, 0, s92\n\t"
+        "s_set_gpr_idx_off\n\t"
+        "v_lshrrev_b32 %[t4], 14, %[t4]\n\t"
+        "v_lshrrev_b32 %[t5], 14, %[t5]\n\t"
+        "v_lshrrev_b32 %[t6], 14, %[t6]\n\t"
+        "v_lshrrev_b32 %[t7], 14, %[t7]\n\t"
+        "v_add_u32 %[t4], s82, %[t4]\n\t"
+        "v_add_u32 %[t5], s86, %[t5]\n\t"
+        "v_add_u32 %[t6], s90, %[t6]\n\t"
+        "v_add_u32 %[t7], s94, %[t7]\n\t"
+        "ds_read_b32 %[t4], %[t4]\n\t"
+        "ds_read_b32 %[t5], %[t5]\n\t"
+        "ds_read_b32 %[t6], %[t6]\n\t"
+        "ds_read_b32 %[t7], %[t7]\n\t"
+        "s_waitcnt lgkmcnt(4)\n\t"
+        "s_cmp_lt_i32 %[m], 0\n\t"
+        "s_cselect_b64 exec, %[lo], %[hi]\n\t"
+        "s_set_gpr_idx_on s65, gpr_idx(SRC2,DST)\n\t"
+        "v_fma_f32 v64, %[t0], s67, v64\n\t"
+        "s_set_gpr_idx_idx s69\n\t"
+        "v_fma_f32 v64, %[t1], s71, v64\n\t"
+        "s_set_gpr_idx_idx s73\n\t"
+        "v_fma_f32 v64, %[t2], s75, v64\n\t"
+        "s_set_gpr_idx_idx s77\n\t"
+        "v_fma_f32 v64, %[t3], s79, v64\n\t"
+        "s_set_gpr_idx_off\n\t"
+        "s_waitcnt lgkmcnt(0)\n\t"
+        "s_cmp_lt_i32 %[m], -1\n\t"
+        "s_cselect_b64 exec, %[lo], %[hi]\n\t"
+        "s_set_gpr_idx_on s81, gpr_idx(SRC2,DST)\n\t"
+        "v_fma_f32 v64, %[t4], s83, v64\n\t"
+        "s_set_gpr_idx_idx s85\n\t"
+        "v_fma_f32 v64, %[t5], s87, v64\n\t"
+        "s_set_gpr_idx_idx s89\n\t"
+        "v_fma_f32 v64, %[t6], s91, v64\n\t"
+        "s_set_gpr_idx_idx s93\n\t"
+        "v_fma_f32 v64, %[t7], s95, v64\n\t"
+        "s_set_gpr_idx_off\n\t"
+        "s_add_u32 %[n], %[n], 2\n\t"
+        "s_add_u32 %[m], %[m], 2\n\t"
+        "s_branch .Lr2_end%=\n\t"
+        ".Lr2_one%=:\n\t"
+        "s_waitcnt lgkmcnt(0)\n\t"
+        "s_cmp_lt_i32 %[m], 0\n\t"
+        "s_cselect_b64 exec, %[lo], %[hi]\n\t"
+        "s_set_gpr_idx_on s65, gpr_idx(SRC2,DST)\n\t"
+        "v_fma_f32 v64, %[t0], s67, v64\n\t"
+        "s_set_gpr_idx_idx s69\n\t"
+        "v_fma_f32 v64, %[t1], s71, v64\n\t"
+        "s_set_gpr_idx_idx s73\n\t"
+        "v_fma_f32 v64, %[t2], s75, v64\n\t"
+        "s_set_gpr_idx_idx s77\n\t"
+        "v_fma_f32 v64, %[t3], s79, v64\n\t"
+        "s_set_gpr_idx_off\n\t"
+        "s_add_u32 %[n], %[n], 1\n\t"
+        "s_add_u32 %[m], %[m], 1\n\t"
+        ".Lr2_end%=:\n\t"
+        "s_mov_b64 exec, %[ex]\n\t"
+        ".Lr2_done%=:\n\t"
+        : [t0] "=&v"(t0), [t1] "=&v"(t1), [t2] "=&v"(t2), [t3] "=&v"(t3), [t4] "=&v"(t4),
+          [t5] "=&v"(t5), [t6] "=&v"(t6), [t7] "=&v"(t7), [ex] "=&s"(ex), [n] "+s"(n),
+          [m] "+s"(m), "+{v[48:63]}"(selv), "+{v[64:95]}"(acc0), "+{v[96:127]}"(acc1)
+        : [lo] "s"(lo), [hi] "s"(hi), "{s[64:79]}"(pa), "{s[80:95]}"(pb)
+        : "memory", "scc");
+}
+
+// the groups after the two loaded before the barrier (four-word records): s_load
+// into s[64:79] / s[80:95] alternately, the next group in flight
+__device__ __forceinline__ void tile_group_loop_r16(const uint32_t *rb, uint32_t ro, uint32_t &n,
+                                                    uint32_t &m, uint64_t lo, uint64_t hi,
+                                                    tile_sel_t &selv, tile_acc_t &acc0,
+                                                    tile_acc_t &acc1)
+{
+    uint32_t t0, t1, t2, t3;
+    uint64_t ex;
+    asm volatile(
+        "s_cmp_eq_u32 %[n], 0\n\t"
+        "s_cbranch_scc1 .Lr4_done%=\n\t"
+        "s_mov_b64 %[ex], exec\n\t"
+        "s_cmp_lt_i32 %[m], 0\n\t"
+        "s_cselect_b64 exec, %[lo], %[hi]\n\t"
+        "s_load_dwordx16 s[64:79], %[rb], %[ro]\n\t"
+        "s_add_u32 %[ro], %[ro], 64\n\t"
+        "s_waitcnt lgkmcnt(0)\n\t"
+        ".Lr4_a%=:\n\t"
+        "s_add_u32 %[n], %[n], 1\n\t"
+        "s_cbranch_scc1 .Lr4_a_last%=\n\t"
+        "s_load_dwordx16 s[80:95], %[rb], %[ro]\n\t"
+        "s_add_u32 %[ro], %[ro], 64\n\t"
+        "s_set_gpr_idx_on s64, gpr_idx(SRC0)\n\t"
+        "v_perm_b32 %[t0], v48, 0, s64\n\t"
+        "s_set_gpr_idx_idx s68\n\t"
+        "v_perm_b32 %[t1], v48, 0, s68\n\t"
+        "s_set_gpr_idx_idx s72\n\t"
+        "v_perm_b32 %[t2], v48, 0, s72\n\t"
+        "s_set_gpr_idx_idx s76\n\t"
+        "v_perm_b32 %[t3], v48, 0, s76\n\t"
+        "s_set_gpr_idx_off\n\t"
+        "v_lshrrev_b32 %[t0], 14, %[t0]\n\t"
+        "v_lshrrev_b32 %[t1], 14, %[t1]\n\t"
+        "v_lshrrev_b32 %[t2], 14, %[t2]\n\t"
+        "v_lshrrev_b32 %[t3], 14, %[t3]\n\t"
+        "v_add_u32 %[t0], s66, %[t0]\n\t"
+        "v_add_u32 %[t1], s70, %[t1]\n\t"
+        "v_add_u32 %[t2], s74, %[t2]\n\t"
+        "v_add_u32 %[t3], s78, %[t3]\n\t"
+        "ds_read_b32 %[t0], %[t0]\n\t"
+        "ds_read_b32 %[t1], %[t1]\n\t"
+        "ds_read_b32 %[t2], %[t2]\n\t"
+        "ds_read_b32 %[t3], %[t3]\n\t"
+        "s_waitcnt lgkmcnt(0)\n\t"
+        "s_set_gpr_idx_on s65, gpr_idx(SRC2,DST)\n\t"
+        "v_fma_f32 v64, %[t0], s67, v64\n\t"
+        "s_set_gpr_idx_idx s69\n\t"
+        "v_fma_f32 v64, %[t1], s71, v64\n\t"
+        "s_set_gpr_idx_idx s73\n\t"
+        "v_fma_f32 v64, %[t2], s75, v64\n\t"
+        "s_set_gpr_idx_idx s77\n\t"
+        "v_fma_f32 v64, %[t3], s79, v64\n\t"
+        "s_set_gpr_idx_off\n\t"
+        "s_add_u32 %[m], %[m], 1\n\t"
+        "s_cselect_b64 exec, %[hi], exec\n\t"
+        "s_add_u32 %[n], %[n], 1\n\t"
+        "s_cbranch_scc1 .Lr4_b_last%=\n\t"
+        "s_load_dwordx16 s[64:79], %[rb], %[ro]\n\t"
+        "s_add_u32 %[ro], %[ro], 64\n\t"
+        "s_set_gpr_idx_on s80, gpr_idx(SRC0)\n\t"
+        "v_perm_b32 %[t0], v48, 0, s80\n\t"
+        "s_set_gpr_idx_idx s84\n\t"
+        "v_perm_b32 %[t1], v48, 0, s84\n\t"
+        "s_set_gpr_idx_idx s88\n\t"
+        "v_perm_b32 %[t2], v48, 0, s88\n\t"
+        "s_set_gpr_idx_idx s92\n\t"
+        "v_perm_b32 %[t3], v48, 0, s92\n\t"
+        "s_set_gpr_idx_off\n\t"
+        "v_lshrrev_b32 %[t0], 14, %[t0]\n\t"
+        "v_lshrrev_b32 %[t1], 14, %[t1]\n\t"
+        "v_lshrrev_b32 %[t2], 14, %[t2]\n\t"
+        "v_lshrrev_b32 %[t3], 14, %[t3]\n\t"
+        "v_add_u32 %[t0], s82, %[t0]\n\t"
+        "v_add_u32 %[t1], s86, %[t1]\n\t"
+        "v_add_u32 %[t2], s90, %[t2]\n\t"
+        "v_add_u32 %[t3], s94, %[t3]\n\t"
+        "ds_read_b32 %[t0], %[t0]\n\t"
+        "ds_read_b32 %[t1], %[t1]\n\t"
+        "ds_read_b32 %[t2], %[t2]\n\t"
+        "ds_read_b32 %[t3], %[t3]\n\t"
+        "s_waitcnt lgkmcnt(0)\n\t"
+        "s_set_gpr_idx_on s81, gpr_idx(SRC2,DST)\n\t"
+        "v_fma_f32 v64, %[t0], s83, v64\n\t"
+        "s_set_gpr_idx_idx s85\n\t"
+        "v_fma_f32 v64, %[t1], s87, v64\n\t"
+        "s_set_gpr_idx_idx s89\n\t"
+        "v_fma_f32 v64, %[t2], s91, v64\n\t"
+        "s_set_gpr_idx_idx s93\n\t"
+        "v_fma_f32 v64, %[t3], s95, v64\n\t"
+        "s_set_gpr_idx_off\n\t"
+        "s_add_u32 %[m], %[m], 1\n\t"
+        "s_cselect_b64 exec, %[hi], exec\n\t"
+        "s_waitcnt lgkmcnt(0)\n\t"
+        "s_branch .Lr4_a%=\n\t"
+        ".Lr4_a_last%=:\n\t"
+        "s_set_gpr_idx_on s64, gpr_idx(SRC0)\n\t"
+        "v_perm_b32 %[t0], v48, 0, s64\n\t"
+        "s_set_gpr_idx_idx s68\n\t"
+        "v_perm_b32 %[t1], v48, 0, s68\n\t"
+        "s_set_gpr_idx_idx s72\n\t"
+        "v_perm_b32 %[t2], v48, 0, s72\n\t"
+        "s_set_gpr_idx_idx s76\n\t"
+        "v_perm_b32 %[t3], v48, 0, s76\n\t"
+        "s_set_gpr_idx_off\n\t"
+        "v_lshrrev_b32 %[t0], 14, %[t0]\n\t"
+        "v_lshrrev_b32 %[t1], 14, %[t1]\n\t"
+        "v_lshrrev_b32 %[t2], 14, %[t2]\n\t"
+        "v_lshrrev_b32 %[t3], 14, %[t3]\n\t"
+        "v_add_u32 %[t0], s66, %[t0]\n\t"
+        "v_add_u32 %[t1], s70, %[t1]\n\t"
+        "v_add_u32 %[t2], s74, %[t2]\n\t"
+        "v_add_u32 %[t3], s78, %[t3]\n\t"
+        "ds_read_b32 %[t0], %[t0]\n\t"
+        "ds_read_b32 %[t1], %[t1]\n\t"
+        "ds_read_b32 %[t2], %[t2]\n\t"
+        "ds_read_b32 %[t3], %[t3]\n\t"
+        "s_waitcnt lgkmcnt(0)\n\t"
+        "s_set_gpr_idx_on s65, gpr_idx(SRC2,DST)\n\t"
+        "v_fma_f32 v64, %[t0], s67, v64\n\t"
+        "s_set_gpr_idx_idx s69\n\t"
+        "v_fma_f32 v64, %[t1], s71, v64\n\t"
+        "s_set_gpr_idx_idx s73\n\t"
+        "v_fma_f32 v64, %[t2], s75, v64\n\t"
+        "s_set_gpr_idx_idx s77\n\t"
+        "v_fma_f32 v64, %[t3], s79, v64\n\t"
+        "s_set_gpr_idx_off\n\t"
+        "s_branch .Lr4_end%=\n\t"
+        ".Lr4_b_last%=:\n\t"
+        "s_waitcnt lgkmcnt(0)\n\t"
+        "s_set_gpr_idx_on s80, gpr_idx(SRC0)\n\t"
+        "v_perm_b32 %[t0], v48, 0, s80\n\t"
+        "s_set_gpr_idx_idx s84\n\t"
+        "v_perm_b32 %[t1], v48, 0, s84\n\t"
+        "s_set_gpr_idx_idx s88\n\t"
+        "v_perm_b32 %[t2], v48, 0, s88\n\t"
+        "s_set_gpr_idx_idx s92\n\t"
+        "v_perm_b32 %[t3], v48, 0, s92\n\t"
+        "s_set_gpr_idx_off\n\t"
+        "v_lshrrev_b32 %[t0], 14, %[t0]\n\t"
+        "v_lshrrev_b32 %[t1], 14, %[t1]\n\t"
+        "v_lshrrev_b32 %[t2], 14, %[t2]\n\t"
+        "v_lshrrev_b32 %[t3], 14, %[t3]\n\t"
+        "v_add_u32 %[t0], s82, %[t0]\n\t"
+        "v_add_u32 %[t1], s86, %[t1]\n\t"
+        "v_add_u32 %[t2], s90, %[t2]\n\t"
+        "v_add_u32 %[t3], s94, %[t3]\n\t"
+        "ds_read_b32 %[t0], %[t0]\n\t"
+        "ds_read_b32 %[t1], %[t1]\n\t"
+        "ds_read_b32 %[t2], %[t2]\n\t"
+        "ds_read_b32 %[t3], %[t3]\n\t"
+        "s_waitcnt lgkmcnt(0)\n\t"
+        "s_set_gpr_idx_on s81, gpr_idx(SRC2,DST)\n\t"
+        "v_fma_f32 v64, %[t0], s83, v64\n\t"
+        "s_set_gpr_idx_idx s85\n\t"
+        "v_fma_f32 v64, %[t1], s87, v64\n\t"
+        "s_set_gpr_idx_idx s89\n\t"
+        "v_fma_f32 v64, %[t2], s91, v64\n\t"
+        "s_set_gpr_idx_idx s93\n\t"
+        "v_fma_f32 v64, %[t3], s95, v64\n\t"
+        "s_set_gpr_idx_off\n\t"
+        ".Lr4_end%=:\n\t"
+        "s_mov_b64 exec, %[ex]\n\t"
+        ".Lr4_done%=:\n\t"
+        : [t0] "=&v"(t0), [t1] "=&v"(t1), [t2] "=&v"(t2), [t3] "=&v"(t3), [ex] "=&s"(ex),
+          [ro] "+s"(ro), [m] "+s"(m), [n] "+s"(n), "+{v[48:63]}"(selv), "+{v[64:95]}"(acc0),
+          "+{v[96:127]}"(acc1)
+        : [rb] "s"(rb), [lo] "s"(lo), [hi] "s"(hi)
+        : "memory", "scc", "s64", "s65", "s66", "s67", "s68", "s69", "s70", "s71", "s72", "s73",
+          "s74", "s75", "s76", "s77", "s78", "s79", "s80", "s81", "s82", "s83", "s84", "s85",
+          "s86", "s87", "s88", "s89", "s90", "s91", "s92", "s93", "s94", "s95");
+}
+
 __device__ __forceinline__ tile_hdr_t tile_load_hdr(const tile_hdr_t *p)
 {
     tile_hdr_t h;
@@ -2288,13 +2615,16 @@ __device__ __forceinline__ void tile_prefetch(const uint32_t *p, uint32_t &d)
 // K = 32: slot register s holds destinations (2s + half) * 16 + wave, lanes
 // 0-31 / 32-63 their 32 entries; K = 64: destination s * 16 + wave, one entry
 // per lane, the records all in "half 0" with exec on every lane.
-template <int K>
+// BDMA: the DMA pieces by range-checked buffer loads (tile_bdma3: offsets from
+// the header VGPRs, ~6 SALU per chunk) instead of one 64-bit address select per
+// piece (~9 SALU each); needs the gradient below 4 GiB - 1 KiB.
+template <int K, bool BDMA>
 __global__ __launch_bounds__(kTileWaves * kWave) void bwd_tile_kernel(
     const tile_hdr_t *__restrict__ hdrs, const int64_t *__restrict__ hdr_start,
     const uint32_t *__restrict__ recs, const int64_t *__restrict__ rec_start,
     const int32_t *__restrict__ num_chunks, const float *__restrict__ grad,
     const float *__restrict__ zero_row, const uint8_t *__restrict__ sel, int num_cols,
-    int group_size, int splits, float *__restrict__ dxs, float *__restrict__ part)
+    int group_size, int splits, float *__restrict__ dxs, float *__restrict__ part, int num_rows)
 {
     __shared__ __attribute__((aligned(16))) float tb[kTileBufs * kTileBufRows * kMaxDim];
     const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -2335,9 +2665,22 @@ __global__ __launch_bounds__(kTileWaves * kWave) void bwd_tile_kernel(
     const uint32_t tb_base = (uint32_t)reinterpret_cast<uintptr_t>(tb);
     const int bw = blockIdx.x * kTileWaves + wv;
     const tile_hdr_t *hs = hdrs + hdr_start[bw];
-    const uint32_t *rb = recs + 2 * rec_start[bw];
+    const uint32_t *rb = recs + kTileRecWords * rec_start[bw];
     uint32_t ro = 0;  // byte offset of the next record group in this wave's stream
     const int nch = num_chunks[blockIdx.x];
+    // raw buffer descriptor of the gradient: base, stride 0, num_records = its bytes
+    const uint64_t gbase = reinterpret_cast<uint64_t>(grad);
+    const tile_rsrc_t rsrc = {(int32_t)(uint32_t)gbase, (int32_t)(uint32_t)(gbase >> 32) & 0xffff,
+                              BDMA ? (int32_t)((uint32_t)num_rows * 1024u) : 0, 0x00020000};
+    const uint32_t lane16 = (uint32_t)lane * 16u;
+    // pieces of rows wv*3 .. wv*3+2 of the chunk's buffer (48 rows = 16 waves x 3)
+    static_assert(!BDMA || kTileWaves * kTilePieces == kTileBufRows, "consecutive piece rows");
+    auto bdma = [&](int c, const tile_hdr_t &h) {
+        const uint32_t buf = tb_base + (uint32_t)(c % kTileBufs) * kTileBufRows * 1024u +
+                             (uint32_t)wv * 3u * 1024u;
+        tile_bdma3(rsrc, ((uint32_t)h.y << 10) + lane16, ((uint32_t)h.z << 10) + lane16,
+                   ((uint32_t)h.w << 10) + lane16, __builtin_amdgcn_readfirstlane(buf));
+    };
     auto dma = [&](int c, int r0, int r1, int r2) {
         static_assert(kTilePieces == 3, "three DMA pieces per wave and chunk");
         const uint32_t buf = tb_base + (uint32_t)(c % kTileBufs) * kTileBufRows * 1024u;
@@ -2363,7 +2706,8 @@ __global__ __launch_bounds__(kTileWaves * kWave) void bwd_tile_kernel(
 #endif
     // the window must stay inside the record stream's padding: 512 records =
     // 1024 dwords after the last wave's stream (kTileRecPad in maxk_plan.hip)
-    static_assert(TILE_PF_AHEAD + 4 * kWave <= 2 * 512, "TILE prefetch past the record padding");
+    static_assert(TILE_PF_AHEAD + 4 * kWave <= kTileRecWords * 512,
+                  "TILE prefetch past the record padding");
 #ifndef TILE_NO_PREFETCH
     auto prefetch = [&]() { tile_prefetch(rb + (ro >> 2) + TILE_PF_AHEAD + lane * 4, pf); };
 #else
@@ -2379,15 +2723,24 @@ __global__ __launch_bounds__(kTileWaves * kWave) void bwd_tile_kernel(
     hh[0] = tile_load_hdr(hs + kTileLead);
 #pragma unroll
     for (int i = 0; i < kTileLead; ++i) {
-        dma(i, e[i].y, e[i].z, e[i].w);
+        if constexpr (BDMA)
+            bdma(i, e[i]);
+        else
+            dma(i, e[i].y, e[i].z, e[i].w);
         hh[i + 1] = tile_load_hdr(hs + kTileLead + 1 + i);
         prefetch();
     }
     auto step = [&](int c, tile_hdr_t &h) {
-        // the chunk's first record group, in flight across the barrier
+        // the chunk's first record groups, in flight across the barrier (four-word
+        // records: pinned to s[64:79] / s[80:95], where the record asm reads them)
         tile_g16_t pa, pb;
-        asm volatile("s_load_dwordx16 %0, %2, %3\n\ts_load_dwordx16 %1, %2, %4"
-                     : "=&s"(pa), "=&s"(pb) : "s"(rb), "s"(ro), "s"(ro + 64) : "memory");
+        if constexpr (kTileRecWords == 4)
+            asm volatile("s_load_dwordx16 s[64:79], %2, %3\n\ts_load_dwordx16 s[80:95], %2, %4"
+                         : "=&{s[64:79]}"(pa), "=&{s[80:95]}"(pb)
+                         : "s"(rb), "s"(ro), "s"(ro + 64) : "memory");
+        else
+            asm volatile("s_load_dwordx16 %0, %2, %3\n\ts_load_dwordx16 %1, %2, %4"
+                         : "=&s"(pa), "=&s"(pb) : "s"(rb), "s"(ro), "s"(ro + 64) : "memory");
         // this wave's DMA of chunk c and header of chunk c landed; after the
         // barrier everyone's have, and chunk c-1's buffer is free
 #if TILE_ABLATE & 1  // timing ablation (wrong results): no chunk barrier
@@ -2401,8 +2754,11 @@ __global__ __launch_bounds__(kTileWaves * kWave) void bwd_tile_kernel(
         // counted vmcnt above relies on it.  A step that issues fewer lets the wave
         // read a header that has not landed -> garbage record counts -> s_loads past
         // the record stream -> memory-access fault; measured with a "no DMA" ablation.)
-        dma(c + kTileLead, __builtin_amdgcn_readfirstlane(h.y), __builtin_amdgcn_readfirstlane(h.z),
-            __builtin_amdgcn_readfirstlane(h.w));
+        if constexpr (BDMA)
+            bdma(c + kTileLead, h);
+        else
+            dma(c + kTileLead, __builtin_amdgcn_readfirstlane(h.y),
+                __builtin_amdgcn_readfirstlane(h.z), __builtin_amdgcn_readfirstlane(h.w));
         h = tile_load_hdr(hs + c + 2 * kTileLead + 1);
         prefetch();
         const uint32_t g0n = (cnt & 0xffffu) >> 2, gn = g0n + (cnt >> 18);
@@ -2416,6 +2772,13 @@ __global__ __launch_bounds__(kTileWaves * kWave) void bwd_tile_kernel(
         // the next step's s_loads into the same SGPRs race with these (SMEM
         // returns out of order), i.e. stale records, on graphs with empty
         // wave-chunks (products k=32: runs differed in the last bits)
+        if constexpr (kTileRecWords == 4) {
+            asm volatile("s_waitcnt lgkmcnt(0)" : "+{s[64:79]}"(pa), "+{s[80:95]}"(pb)::"memory");
+            tile_groups2_r16(pa, pb, n, m, lo, hi, selv, acc0, acc1);
+            tile_group_loop_r16(rb, ro + 128, n, m, lo, hi, selv, acc0, acc1);
+            ro += 64 * gn;
+            return;
+        }
         asm volatile("s_waitcnt lgkmcnt(0)" : "+s"(pa), "+s"(pb)::"memory");
         uint32_t ga[16], gb[16];
 #pragma unroll
@@ -3404,12 +3767,19 @@ int maxk_sspmm_backward_tile(const void *headers, const int64_t *header_start,
          reinterpret_cast<uintptr_t>(cbsr_sel)) & 15)
         return MAXK_E_ARG;
     hipStream_t st = as_stream(stream);
-    hipLaunchKernelGGL(dim_k == 32 ? bwd_tile_kernel<32> : bwd_tile_kernel<64>,
-                       dim3((unsigned)(num_groups * splits)),
-                       dim3(kTileWaves * kWave), 0, st,
+    // buffer DMA while the gradient's bytes and a zero-row offset fit the 32-bit
+    // range check (V <= 4 M rows); MAXK_TILE_GDMA=1 keeps the global-address form
+    static const bool gdma = [] {
+        const char *v = getenv("MAXK_TILE_GDMA");
+        return v && v[0] == '1';
+    }();
+    const bool bdma = !gdma && (int64_t)num_rows * 1024 <= (int64_t)0xFFFFFC00u - 1024;
+    auto kern = dim_k == 32 ? (bdma ? bwd_tile_kernel<32, true> : bwd_tile_kernel<32, false>)
+                            : (bdma ? bwd_tile_kernel<64, true> : bwd_tile_kernel<64, false>);
+    hipLaunchKernelGGL(kern, dim3((unsigned)(num_groups * splits)), dim3(kTileWaves * kWave), 0, st,
                        reinterpret_cast<const tile_hdr_t *>(headers), header_start,
                        reinterpret_cast<const uint32_t *>(records), record_start, num_chunks, grad,
-                       zero_row, cbsr_sel, num_cols, group_size, splits, dxs, part);
+                       zero_row, cbsr_sel, num_cols, group_size, splits, dxs, part, num_rows);
     int rc = launch_status();
     if (rc || splits == 1) return rc;
     const int64_t n4 = (int64_t)num_cols * dim_k / 4;

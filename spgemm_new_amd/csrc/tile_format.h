@@ -19,6 +19,19 @@
 #define TILE_BUF_ROWS 48
 #endif
 
+// Record format: TILE_REC_WORDS = 2 -- {w = slot | staged row << 24, value}: the
+// kernel derives the selector word, its bit offset and the row's LDS address
+// from w with three scalar shifts per record; 4 -- {selector control word (byte
+// 0: selector register index, byte 2: 4 + byte of it, bytes 1 / 3: 0x0c; the
+// S2 operand of a v_perm_b32 that extracts the selector into byte 2), slot,
+// LDS byte address of the staged row, value}: no scalar work besides the two
+// register-index writes per record.
+#ifndef TILE_REC_WORDS
+#define TILE_REC_WORDS 4
+#endif
+constexpr int kTileRecWords = TILE_REC_WORDS;
+static_assert(kTileRecWords == 2 || kTileRecWords == 4, "record words");
+
 constexpr int kTileWaves = 16;
 constexpr int kTileBufs = TILE_NBUF;
 constexpr int kTileBufRows = TILE_BUF_ROWS;

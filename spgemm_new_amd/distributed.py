@@ -213,8 +213,10 @@ class PartitionedMaxK:
         # forward computes the own part while the halo CBSR is in flight; the
         # backward (overlap_backward, on for N > 1) computes the halo columns
         # first and their partial sums travel while the own columns are computed.
-        # The column sets are disjoint, so with the same local algorithm on every
-        # part (bwd_algo pinned) dXs is bitwise the single block's; the forward
+        # The column sets are disjoint, so with bwd_algo pinned to an algorithm
+        # whose per-destination order ignores the other columns (LOCAL: a
+        # destination's in-edges in source-row order) dXs is bitwise the single
+        # block's; STAGED's merge-path panel splits depend on the whole block.  The forward
         # adds each row's own-column edges before its halo-column edges, a
         # different fp32 order than the single block's edge order.
         self.bwd_algo = bwd_algo

@@ -168,7 +168,7 @@ class MaxKGraph:
                  values: torch.Tensor | None = None, *, panel_cost: int | None = None,
                  row_cost: int = _lib.DEFAULT_ROW_COST, bwd_panel_cost: int | None = None,
                  csc_panel_cost: int | None = None, num_cols: int | None = None,
-                 validate: bool = True):
+                 validate: bool = True, tile_splits: int | None = None):
         check_tensor(indptr, "indptr", torch.int32, dim=1)
         check_tensor(indices, "indices", torch.int32, dim=1)
         if values is None:
@@ -219,6 +219,10 @@ class MaxKGraph:
         self._csc = None
         self._local = {}
         self._tile = {}
+        # TILE source ranges (None: enough to fill the CUs); 1 makes each
+        # destination's sum one sequential FMA chain in source-row order, the same
+        # bits whatever other columns the graph holds (tests of the row partition)
+        self.tile_splits = tile_splits
         self._ws = {}
         self._bwd_choice = {}
         self._bwd_alt = {}        # AUTO's best algorithm other than STAGED_EDGE, per key
@@ -409,9 +413,13 @@ class MaxKGraph:
             plan = None
             if self.num_edges > 0 and self.device.type == "cuda":
                 cus = torch.cuda.get_device_properties(self.device).multi_processor_count
+                shape = None
+                if self.tile_splits is not None:
+                    G, GS, _ = tile.choose_shape(self.num_cols, cus, dim_k)
+                    shape = (G, GS, max(1, int(self.tile_splits)))
                 plan = tile.build(self.indptr, self.indices[: self.num_edges],
                                   self.values[: self.num_edges], self.num_rows, self.num_cols,
-                                  cus=cus, k=dim_k)
+                                  cus=cus, k=dim_k, shape=shape)
             if plan is not None:
                 # the values the records hold: key + the tensor (kept alive so its
                 # address cannot be reused by another tensor with the same key)

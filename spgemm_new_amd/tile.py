@@ -56,6 +56,11 @@ def ring_format() -> tuple[int, int, int]:
 _FMT = None
 
 
+def record_words() -> int:
+    """int32 words per record in the compiled library's format (2 or 4)."""
+    return int(_lib.load().maxk_tile_record_words())
+
+
 def max_group(k: int) -> int:
     return (128 if k == 32 else 64) * WAVES
 
@@ -101,7 +106,7 @@ def build(indptr: torch.Tensor, indices: torch.Tensor, values: torch.Tensor, num
     i32 = dict(dtype=torch.int32, device=dev)
     i64 = dict(dtype=torch.int64, device=dev)
     hdrs = torch.empty(sizes[0], 4, **i32)
-    recs = torch.empty(sizes[1], 2, **i32)
+    recs = torch.empty(sizes[1], record_words(), **i32)
     hstart, rstart = torch.empty(NWG * WAVES, **i64), torch.empty(NWG * WAVES, **i64)
     nch = torch.empty(NWG, **i32)
     edge_record = torch.empty(E, **i32)
@@ -169,12 +174,22 @@ def emulate(plan, grad: torch.Tensor, sel: torch.Tensor) -> torch.Tensor:
                 cols = torch.where(j < nd, sel[(d0 + j).clamp(max=C - 1), ent], 0)   # [slot, lane]
                 for t in range(n0 + n1):
                     r = recs[ro[wv] + t]
-                    w0 = int(r[0]) & 0xFFFFFFFF
-                    val = r[1:2].view(torch.float32).item()
-                    # the kernel's decode: slot = w0 & 63 (register index reads bits 7:0),
-                    # selector word = w0 >> 2, byte offset = (w0 << 3) & 24, row = w0 >> 14
-                    s, addr = w0 & 63, w0 >> 14
-                    assert (w0 >> 6) & 0x3FFFF == 0
+                    val = r[-1:].view(torch.float32).item()
+                    if r.numel() == 2:
+                        w0 = int(r[0]) & 0xFFFFFFFF
+                        # the kernel's decode: slot = w0 & 63 (register index reads bits
+                        # 7:0), selector word = w0 >> 2, byte offset = (w0 << 3) & 24,
+                        # row = w0 >> 14
+                        s, addr = w0 & 63, w0 >> 14
+                        assert (w0 >> 6) & 0x3FFFF == 0
+                    else:
+                        # {v_perm control, slot, row address, value}: the selector register
+                        # index (byte 0) and the byte the perm picks (byte 2 - 4) must name
+                        # the slot's selector byte; bytes 1 and 3 select zeros
+                        ctl = int(r[0]) & 0xFFFFFFFF
+                        s, addr = int(r[1]), int(r[2])
+                        assert ctl == (s >> 2) | 0x0c << 8 | (4 + (s & 3)) << 16 | 0x0c << 24
+                        assert 0 <= s < 64 and addr % 1024 == 0
                     lanes = (slice(0, 64) if K == 64 else
                              slice(0, 32) if t < n0 else slice(32, 64))
                     acc[wv, s, lanes] += val * lds[addr // 4 + cols[s, lanes]]

@@ -12,8 +12,13 @@ single MaxKGraph over the whole graph (per row: spmm_maxk.cu:17-106 and
 spmm_maxk_backward.cu:15-115 semantics), within 1e-4 relative.  A consistent
 halo-renumbering error (a permuted send list, a wrong owner) changes rows and
 fails here, which the adjoint identity alone could not see.  Also checked:
-with the local backward pinned to one algorithm, dXs with the overlapped
-backward (own / halo parts) is bitwise the single block's."""
+with the local backward pinned to TILE with one source range (per destination
+one sequential FMA chain over its in-edges in source-row order, whatever other
+columns the block holds), dXs with the overlapped backward (own / halo parts)
+is bitwise the single block's.  (The defaults are not bitwise across blocks:
+STAGED's merge-path panels split destinations at places that depend on the
+block's other columns, LOCAL rounds some products in its tail rounds, TILE's
+source-range count follows the block's column count.)"""
 import multiprocessing as mp
 import os
 import socket
@@ -54,6 +59,8 @@ def _worker(rank, world, port, graph, R, outdir, q):
     import sys
     sys.path.insert(0, ROOT)
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    # up to 8 ranks share the box's CPU share: keep each one's host thread pool small
+    torch.set_num_threads(2)
     import torch.distributed as dist
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
@@ -73,16 +80,19 @@ def _worker(rank, world, port, graph, R, outdir, q):
         vals = _values(R, e0, e1, dev)
         data, sel = topk_cbsr(synthetic_features(SEED_X, r0, r1, H, dev), K)
         G = _grad(R, r0, r1, dev)
-        staged = _lib.MAXK_BWD_STAGED
-        m = PartitionedMaxK(indptr, cols, vals, rank, world, dev, local_block=True,
-                            bwd_algo=None if R > 1 else staged)
+        tile = _lib.MAXK_BWD_TILE
+        log = lambda msg: print(f"[pin {graph} N={world} rank {rank}] {msg}", flush=True)
+        log("block generated")
+        kw = {} if R > 1 else {"bwd_algo": tile, "tile_splits": 1}
+        m = PartitionedMaxK(indptr, cols, vals, rank, world, dev, local_block=True, **kw)
+        log(f"partition built (halo {m.plan.num_halo}, mode {m.halo_mode})")
         if R == 1:
             y = m.forward(data, sel, H)
             dx = m.backward(G, sel)
             assert m.overlap_backward
             # the single-block backward (no own / halo split), same local algorithm
             m1 = PartitionedMaxK(indptr, cols, vals, rank, world, dev, local_block=True,
-                                 overlap=False, bwd_algo=staged)
+                                 overlap=False, **kw)
             y1 = m1.forward(data, sel, H)
             dx1 = m1.backward(G, sel)
             bitwise = bool(torch.equal(dx, dx1))
@@ -92,6 +102,7 @@ def _worker(rank, world, port, graph, R, outdir, q):
             dx = m.backward_multi(G, sel)
             bitwise, fwd_split = True, 0.0
         torch.cuda.synchronize()
+        log("forward + backward done")
         torch.save({"r0": r0, "r1": r1, "y": y.cpu(), "dx": dx.cpu(), "halo": m.plan.num_halo},
                    os.path.join(outdir, f"rank{rank}.pt"))
         flags = torch.tensor([float(not bitwise), fwd_split])
@@ -150,8 +161,16 @@ def test_partitioned_rows_match_single_gpu(graph, world, R, tmp_path):
     port = _free_port()
     procs = [ctx.Process(target=_worker, args=(r, world, port, graph, R, str(tmp_path), q))
              for r in range(world)]
-    for p in procs:
-        p.start()
+    saved = os.environ.get("OMP_NUM_THREADS")
+    os.environ["OMP_NUM_THREADS"] = "2"      # the children's OpenMP pools (spawned now)
+    try:
+        for p in procs:
+            p.start()
+    finally:
+        if saved is None:
+            os.environ.pop("OMP_NUM_THREADS", None)
+        else:
+            os.environ["OMP_NUM_THREADS"] = saved
     for p in procs:
         p.join(timeout=600)
     assert all(p.exitcode == 0 for p in procs), [p.exitcode for p in procs]

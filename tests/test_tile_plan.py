@@ -42,14 +42,18 @@ def _inputs(V, C, seed, k=32, h=256):
     (200, 64, 4, (1, 64, 1), 0),       # few destinations, one range
 ])
 def test_plan_emulated_matches_oracle(oracle, V, C, deg, shape, hubs, k):
+    """Both record formats (tile_format.h TILE_REC_WORDS 2 and 4) replayed on
+    the CPU equal the oracle."""
     indptr, idx, vals = _graph(V, C, deg, seed=V + C, hub_rows=hubs)
     grad, sel = _inputs(V, C, seed=V, k=k)
-    plan = tile_ref.build(torch.from_numpy(indptr), torch.from_numpy(idx), torch.from_numpy(vals),
-                          V, C, cus=16, shape=shape, k=k)
-    assert plan is not None
-    got = tile.emulate(plan, torch.from_numpy(grad), torch.from_numpy(sel)).numpy()
     ref = oracle.np_backward(indptr, idx, vals, grad, sel)
-    assert oracle.parity_error(got, ref) < TOL
+    for rw in (2, 4):
+        plan = tile_ref.build(torch.from_numpy(indptr), torch.from_numpy(idx),
+                              torch.from_numpy(vals), V, C, cus=16, shape=shape, k=k,
+                              record_words=rw)
+        assert plan is not None and plan["records"].shape[1] == rw
+        got = tile.emulate(plan, torch.from_numpy(grad), torch.from_numpy(sel)).numpy()
+        assert oracle.parity_error(got, ref) < TOL
 
 
 def test_plan_invariants():
@@ -75,10 +79,13 @@ def test_plan_invariants():
                     n0, n1 = int(e[0]) & 0xFFFF, int(e[0]) >> 16
                     assert n0 % 4 == 0 and n1 % 4 == 0
                     seg = recs[ro: ro + n0 + n1]
-                    real = seg[:, 1] != 0
+                    real = seg[:, -1] != 0
                     n_real += int(real.sum())
                     # real records read rows of the chunk's own buffer
-                    rowf = (seg[real][:, 0].long() & 0xFFFFFFFF) >> 24
+                    if seg.shape[1] == 2:
+                        rowf = (seg[real][:, 0].long() & 0xFFFFFFFF) >> 24
+                    else:
+                        rowf = seg[real][:, 2].long() >> 10
                     assert bool(((rowf // BR) == (c - lead) % NB).all())
                     ro += n0 + n1
     assert n_real == int((torch.from_numpy(vals) != 0).sum())
@@ -121,13 +128,13 @@ def test_device_plan_matches_reference_builder(dev, V, C, deg, shape, hubs, k):
         assert a.shape == b.shape and torch.equal(a, b), key
     rec = got["records"].cpu()
     er = got["edge_record"].cpu().long()
-    assert torch.equal(rec[er, 1], args[2].cpu().view(torch.int32))
+    assert torch.equal(rec[er, -1], args[2].cpu().view(torch.int32))
     # set_values rewrites exactly the value words
     new = torch.rand(idx.size, device=dev)
     tile.set_values(got, new)
     rec2 = got["records"].cpu()
-    assert torch.equal(rec2[er, 1], new.cpu().view(torch.int32))
-    assert torch.equal(rec2[:, 0], rec[:, 0])
+    assert torch.equal(rec2[er, -1], new.cpu().view(torch.int32))
+    assert torch.equal(rec2[:, :-1], rec[:, :-1])
 
 
 @pytest.mark.gpu

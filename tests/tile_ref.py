@@ -28,10 +28,15 @@ def choose_shape(num_cols: int, cus: int = 256, k: int = 32) -> tuple[int, int, 
 
 
 def build(indptr: torch.Tensor, indices: torch.Tensor, values: torch.Tensor, num_rows: int,
-          num_cols: int, cus: int = 256, shape: tuple[int, int, int] | None = None, k: int = 32):
+          num_cols: int, cus: int = 256, shape: tuple[int, int, int] | None = None, k: int = 32,
+          record_words: int | None = None):
     """The TILE plan as a dict, or None when a chunk would overflow a wave's
     64-slot segment (many edges of few source rows into one wave's
-    destinations; the other algorithms serve such graphs)."""
+    destinations; the other algorithms serve such graphs).  record_words: the
+    record format (tile_format.h: 2 or 4; default the compiled library's)."""
+    if record_words is None:
+        from spgemm_new_amd.tile import record_words as _rw
+        record_words = _rw()
     NB, BUF_ROWS, CHUNK_ROWS = ring_format()
     lead = NB - 1
     dev = indices.device
@@ -89,8 +94,22 @@ def build(indptr: torch.Tensor, indices: torch.Tensor, values: torch.Tensor, num
     rstart = torch.cumsum(rlen, 0) - rlen
     seg_off = rstart.view(NWG, WAVES, 1) + torch.cumsum(nrec, -1) - nrec  # first record of (wg,w,c)
     total = int(rlen.sum()) + 512                                          # + 4 KB over-read pad
-    recs = torch.zeros(total, 2, dtype=torch.int32, device=dev)
-    recs[:, 0] = (BUF_ROWS - 1) << 24                                     # padding: slot 0, zero row
+    RW = record_words
+    recs = torch.zeros(total, RW, dtype=torch.int32, device=dev)
+
+    def put(at, slot_, ring_row, vals):                                   # tile_put_record
+        if RW == 2:
+            w0 = slot_ | (ring_row << 24)
+            recs[at, 0] = torch.where(w0 >= (1 << 31), w0 - (1 << 32), w0).to(torch.int32)
+        else:
+            ctl = (slot_ >> 2) | (0x0c << 8) | ((4 + (slot_ & 3)) << 16) | (0x0c << 24)
+            recs[at, 0] = torch.where(ctl >= (1 << 31), ctl - (1 << 32), ctl).to(torch.int32)
+            recs[at, 1] = slot_.to(torch.int32)
+            recs[at, 2] = (ring_row << 10).to(torch.int32)
+        recs[at, RW - 1] = vals
+    every = torch.arange(total, **i64)
+    put(every, torch.zeros_like(every), torch.full_like(every, BUF_ROWS - 1),
+        torch.zeros(total, dtype=torch.int32, device=dev))                # padding: slot 0, zero row
     order = torch.argsort(seg, stable=True)
     sseg = seg[order]
     first = torch.searchsorted(sseg, sseg)
@@ -101,9 +120,7 @@ def build(indptr: torch.Tensor, indices: torch.Tensor, values: torch.Tensor, num
     pos = seg_off.flatten()[base_seg] + h * pad.view(-1, 2)[base_seg, 0] + rank
     del sseg, rank, base_seg, h
     so = slot[order]
-    w0 = so | (((c % NB) * BUF_ROWS + rin)[order] << 24)
-    recs[pos, 0] = torch.where(w0 >= (1 << 31), w0 - (1 << 32), w0).to(torch.int32)
-    recs[pos, 1] = values[order].contiguous().view(torch.int32)
+    put(pos, so, ((c % NB) * BUF_ROWS + rin)[order], values[order].contiguous().view(torch.int32))
     del order, pos, so, seg, slot, rin, c
     # header stream: e(0) .. e(lead - 1), then e(c + lead) per chunk
     wv = torch.arange(WAVES, **i64)
