@@ -372,7 +372,7 @@ void test_graph(const std::string &dir, const std::string &graph, int idx, int c
             if (sizes[2] <= 0xFFFF) {
                 const int nw = G * NS * 16;
                 void *hdrs = dev_alloc<int32_t>((size_t)sizes[0] * 4);
-                void *recs = dev_alloc<int32_t>((size_t)sizes[1] * 2);
+                void *recs = dev_alloc<int32_t>((size_t)sizes[1] * maxk_tile_record_words());
                 int64_t *hstart = dev_alloc<int64_t>(nw), *rstart = dev_alloc<int64_t>(nw);
                 int32_t *nch = dev_alloc<int32_t>((size_t)G * NS);
                 MAXKCHECK(maxk_tile_plan_build(indptr, indices, val, V, V, E, k, G, GS, NS, hdrs,

@@ -4,9 +4,11 @@ BASELINE shapes and rank counts.
 BASELINE config 4 (ogbn-products-shaped, k = 32) at world 2, 4 and 8 and
 config 5 (ogbn-proteins-shaped, R = 8 relations) at world 8, every rank on
 cuda:0 (gloo stands in for RCCL: the exchange is staged through host memory).
-Each rank generates only its block -- columns, edge values, features and
-gradient rows are hashes of global ids (graphs.synthetic_*), so the blocks are
-rows of the single-GPU graph -- runs forward + backward through
+The parent process generates the graph's CSR once (power-law indptr and
+columns take many synchronising passes, and N processes time-share the one
+card) and each rank maps only its rows' slice of it; edge values, features and
+gradient rows are hashes of global ids (graphs.synthetic_*) that a rank
+generates for its own rows.  Every rank runs forward + backward through
 PartitionedMaxK, and its own rows of Y and dXs are compared per element with a
 single MaxKGraph over the whole graph (per row: spmm_maxk.cu:17-106 and
 spmm_maxk_backward.cu:15-115 semantics), within 1e-4 relative.  A consistent
@@ -55,33 +57,36 @@ def _grad(R, r0, r1, dev):
     return torch.stack([synthetic_features(SEED_G + q, r0, r1, H, dev) for q in range(R)])
 
 
-def _worker(rank, world, port, graph, R, outdir, q):
+def _worker(rank, world, port, graph, R, graphdir, outdir, q):
     import sys
     sys.path.insert(0, ROOT)
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     # up to 8 ranks share the box's CPU share: keep each one's host thread pool small
     torch.set_num_threads(2)
+    import faulthandler
+    faulthandler.dump_traceback_later(45, repeat=True)   # where a slow rank is, every 45 s
     import torch.distributed as dist
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
         from spgemm_new_amd import _lib
         from spgemm_new_amd.distributed import PartitionedMaxK, row_partition
-        from spgemm_new_amd.graphs import (CONFIGS, synthetic_columns, synthetic_features,
-                                           synthetic_indptr)
+        from spgemm_new_amd.graphs import synthetic_features
         from spgemm_new_amd.ops import topk_cbsr
+        import numpy as np
         dev = torch.device("cuda", 0)
         torch.cuda.set_device(dev)
-        V, E = CONFIGS[graph]
-        indptr = synthetic_indptr(V, E, seed=SEED, device=dev)
+        log = lambda msg: print(f"[pin {graph} N={world} rank {rank}] {msg}", flush=True)
+        indptr = torch.from_numpy(np.load(os.path.join(graphdir, "indptr.npy"))).to(dev)
         b = row_partition(indptr, world)
         r0, r1 = b[rank], b[rank + 1]
         e0, e1 = int(indptr[r0]), int(indptr[r1])
-        cols = synthetic_columns(indptr, seed=SEED, rows=(r0, r1))
+        log(f"rows [{r0}, {r1}) edges [{e0}, {e1})")
+        cols_all = np.load(os.path.join(graphdir, "indices.npy"), mmap_mode="r")
+        cols = torch.from_numpy(np.ascontiguousarray(cols_all[e0:e1])).to(dev)
         vals = _values(R, e0, e1, dev)
         data, sel = topk_cbsr(synthetic_features(SEED_X, r0, r1, H, dev), K)
         G = _grad(R, r0, r1, dev)
         tile = _lib.MAXK_BWD_TILE
-        log = lambda msg: print(f"[pin {graph} N={world} rank {rank}] {msg}", flush=True)
         log("block generated")
         kw = {} if R > 1 else {"bwd_algo": tile, "tile_splits": 1}
         m = PartitionedMaxK(indptr, cols, vals, rank, world, dev, local_block=True, **kw)
@@ -116,10 +121,12 @@ def _worker(rank, world, port, graph, R, outdir, q):
 _REF = {}
 
 
-def _reference(graph, R):
-    """Y and dXs of the whole graph on one GPU (single MaxKGraph), cached per graph."""
+def _reference(graph, R, graphdir):
+    """Y and dXs of the whole graph on one GPU (single MaxKGraph), cached per graph;
+    the graph's indptr / indices are written to `graphdir` for the ranks."""
     key = (graph, R)
     if key not in _REF:
+        import numpy as np
         import spgemm_new_amd as S
         from spgemm_new_amd import _lib
         from spgemm_new_amd.graphs import (CONFIGS, synthetic_columns, synthetic_features,
@@ -129,6 +136,8 @@ def _reference(graph, R):
         V, E = CONFIGS[graph]
         indptr = synthetic_indptr(V, E, seed=SEED, device=dev)
         indices = synthetic_columns(indptr, seed=SEED)
+        np.save(os.path.join(graphdir, "indptr.npy"), indptr.cpu().numpy())
+        np.save(os.path.join(graphdir, "indices.npy"), indices.cpu().numpy())
         vals = _values(R, 0, E, dev)
         data, sel = topk_cbsr(synthetic_features(SEED_X, 0, V, H, dev), K)
         G = _grad(R, 0, V, dev)
@@ -142,7 +151,7 @@ def _reference(graph, R):
             dx = g.backward_multi(G, sel, vals)
         torch.cuda.synchronize()
         _REF.clear()
-        _REF[key] = (y.cpu(), dx.cpu())
+        _REF[key] = (y.cpu(), dx.cpu(), graphdir)
         del g, y, dx, G, data, sel, vals, indices, indptr
         torch.cuda.empty_cache()
     return _REF[key]
@@ -155,29 +164,37 @@ def _rel_err(a, b):
 @pytest.mark.gpu
 @pytest.mark.parametrize("graph,world,R", [("products", 2, 1), ("products", 4, 1),
                                            ("products", 8, 1), ("proteins", 8, 8)])
-def test_partitioned_rows_match_single_gpu(graph, world, R, tmp_path):
+def test_partitioned_rows_match_single_gpu(graph, world, R, tmp_path, tmp_path_factory):
+    y_ref, dx_ref, graphdir = _reference(graph, R, str(tmp_path_factory.mktemp(graph)))
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, world, port, graph, R, str(tmp_path), q))
+    procs = [ctx.Process(target=_worker,
+                         args=(r, world, port, graph, R, graphdir, str(tmp_path), q))
              for r in range(world)]
-    saved = os.environ.get("OMP_NUM_THREADS")
-    os.environ["OMP_NUM_THREADS"] = "2"      # the children's OpenMP pools (spawned now)
+    # the children's OpenMP pools, and one hardware queue per rank: N processes time-share
+    # the one card, and more queues than the scheduler maps at once stall every sync
+    child_env = {"OMP_NUM_THREADS": "2", "GPU_MAX_HW_QUEUES": "1"}
+    saved = {k: os.environ.get(k) for k in child_env}
+    os.environ.update(child_env)
     try:
         for p in procs:
             p.start()
     finally:
-        if saved is None:
-            os.environ.pop("OMP_NUM_THREADS", None)
-        else:
-            os.environ["OMP_NUM_THREADS"] = saved
+        for k, v in saved.items():
+            if v is None:
+                os.environ.pop(k, None)
+            else:
+                os.environ[k] = v
     for p in procs:
         p.join(timeout=600)
+        if p.exitcode is None:
+            p.kill()
+            p.join()
     assert all(p.exitcode == 0 for p in procs), [p.exitcode for p in procs]
     not_bitwise, fwd_split = q.get(timeout=5)
     assert not_bitwise == 0.0, "overlapped backward differs bitwise from the single block"
     assert fwd_split <= TOL
-    y_ref, dx_ref = _reference(graph, R)
     rows = 0
     for r in range(world):
         part = torch.load(os.path.join(str(tmp_path), f"rank{r}.pt"), weights_only=True)
