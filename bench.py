@@ -41,7 +41,8 @@ def parse():
     p.add_argument("--h", type=int, default=256)
     p.add_argument("--seed", type=int, default=123)
     p.add_argument("--bwd-algo", default="auto",
-                   choices=["auto", "atomic", "staged", "local", "tile", "staged_edge", "edge_gather"])
+                   choices=["auto", "atomic", "staged", "local", "tile", "staged_edge", "edge_gather",
+                            "binned", "binned_edge"])
     p.add_argument("--panel-cost", type=int, default=None)
     p.add_argument("--row-cost", type=int, default=None)
     p.add_argument("--no-cpu-baseline", action="store_true")
@@ -485,7 +486,9 @@ def config_sweep(args, dev, only=None):
                 "fwd_frac": round(b / (fs["mean"] / 1e3) / 1e9 / HBM_PEAK_GBS, 4),
                 "bwd_frac": round(b / (bs["mean"] / 1e3) / 1e9 / HBM_PEAK_GBS, 4),
                 "step_GBs": round(2 * b / (sum(st) / len(st) / 1e3) / 1e9, 1),
-                "bwd_algo": algo, "fwd_form": (f"column-blocked nb={nb}" if nb else
+                "bwd_algo": algo,
+                "bwd_candidates_ms": getattr(g, "bwd_candidates", {}).get((k, h, True)),
+                "fwd_form": (f"column-blocked nb={nb}" if nb else
                                                "packed CBSR records" if k <= 16 else "plain"),
                 "bwd_check": {"vs": "staged",
                               "max_rel_diff": float(((dx - dx_ref).abs()
@@ -702,7 +705,8 @@ def main():
     algo = {"auto": _lib.MAXK_BWD_AUTO, "atomic": _lib.MAXK_BWD_ATOMIC,
             "staged": _lib.MAXK_BWD_STAGED, "local": _lib.MAXK_BWD_LOCAL,
             "tile": _lib.MAXK_BWD_TILE, "staged_edge": _lib.MAXK_BWD_STAGED_EDGE,
-            "edge_gather": _lib.MAXK_BWD_EDGE_GATHER}[args.bwd_algo]
+            "edge_gather": _lib.MAXK_BWD_EDGE_GATHER, "binned": _lib.MAXK_BWD_BINNED,
+            "binned_edge": _lib.MAXK_BWD_BINNED_EDGE}[args.bwd_algo]
     kw = {}
     if args.panel_cost:
         kw["panel_cost"] = args.panel_cost

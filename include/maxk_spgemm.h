@@ -280,6 +280,9 @@ int maxk_spgemm_forward_multi(const int32_t *sched, int64_t num_panels, const in
                                   gathers them per destination: csc_pos is then the CSC slot ->
                                   CSR edge permutation (maxk_csc_perm_build); k a power of
                                   two in [4, 256] */
+#define MAXK_BWD_BINNED 7      /* destination bins summed in LDS (maxk_sspmm_backward_binned,
+                                  node selectors); not accepted by maxk_sspmm_backward */
+#define MAXK_BWD_BINNED_EDGE 8 /* BINNED reading edge selectors (as STAGED_EDGE) */
 size_t maxk_backward_workspace_bytes(int algo, int64_t num_edges, int dim_k,
                                      int64_t csc_num_panels);
 int maxk_sspmm_backward(int algo, const int32_t *sched, int64_t num_panels,
@@ -384,6 +387,44 @@ int maxk_tile_plan_build(const int32_t *indptr, const int32_t *indices, const fl
                          int64_t *sizes, void *workspace, size_t workspace_bytes, void *stream);
 int maxk_tile_plan_set_values(const int32_t *edge_record, const float *values, int64_t num_edges,
                               void *records, void *stream);
+
+/* ---------------------------------------------------------------------------
+ * Backward SSpMM, BINNED algorithm (propagation blocking; no counterpart in the
+ * reference, whose backward scatters with atomics, spmm_maxk_backward.cu:
+ * 86-112).  Phase 1 pushes over the CSR panels (sched, as the forward and
+ * STAGED) and writes each edge's k products, unpadded, to slot bin_pos[e] of
+ * destination bin idx[e] / MAXK_BIN_DESTS; phase 2 sums every bin in LDS (one
+ * wave per bin) and stores its rows of dxs.  Versus STAGED it writes k*4 B
+ * instead of a 64-B row per edge at k = 8, in streams its XCD's L2 completes
+ * line by line, and replaces the segmented sum's CSC panels by one pass.
+ * dim_k in {8, 16, 32}; sel = node CBSR selectors, or edge selectors (uint8
+ * [E, k] from maxk_spgemm_forward_esel) when edge_selectors != 0.
+ * Deterministic (the slot order is fixed by the plan).  Workspace:
+ * maxk_backward_binned_workspace_bytes(num_slots, dim_k) (the products).
+ *  maxk_bin_plan_build: bins of MAXK_BIN_DESTS destinations; a bin's slots hold
+ *    its in-edges ordered by (XCD of the panel's workgroup, edge), packed
+ *    first-fit into windows of 64 slots with distinct destinations (at most 8
+ *    windows open; padding slots have bin_dst 0xFF).  Count call
+ *    (bin_pos == NULL): writes *num_slots (host) and synchronises; fill call:
+ *    bin_pos int32[E], bin_ptr int32[num_bins + 1] (slot offsets, multiples of
+ *    64), bin_dst uint8[num_slots].  The plan is tied to `sched` (the XCD
+ *    order follows its panels).  num_bins = ceil(num_cols / MAXK_BIN_DESTS).
+ * ------------------------------------------------------------------------- */
+#define MAXK_BIN_DESTS 255
+#define MAXK_BIN_WINDOW 64
+size_t maxk_bin_plan_workspace_bytes(int64_t num_edges, int num_cols);
+int maxk_bin_plan_build(const int32_t *sched, int64_t num_panels, const int32_t *indices,
+                        int64_t num_edges, int num_cols, int32_t *bin_pos, int32_t *bin_ptr,
+                        uint8_t *bin_dst, int64_t slot_capacity, int64_t *num_slots,
+                        void *workspace, size_t workspace_bytes, void *stream);
+size_t maxk_backward_binned_workspace_bytes(int64_t num_slots, int dim_k);
+int maxk_sspmm_backward_binned(const int32_t *sched, int64_t num_panels, const int32_t *indptr,
+                               const int32_t *indices, const float *values, const float *grad,
+                               const uint8_t *sel, int edge_selectors, int num_rows, int num_cols,
+                               int64_t num_edges, int dim_origin, int dim_k, float *dxs,
+                               const int32_t *bin_pos, const int32_t *bin_ptr,
+                               const uint8_t *bin_dst, int num_bins, int64_t num_slots,
+                               void *workspace, size_t workspace_bytes, void *stream);
 
 /* ---------------------------------------------------------------------------
  * CBSR producer (MaxK top-k) and dense-gradient scatter.

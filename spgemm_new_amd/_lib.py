@@ -30,6 +30,10 @@ MAXK_BWD_LOCAL = 3
 MAXK_BWD_TILE = 4
 MAXK_BWD_STAGED_EDGE = 5
 MAXK_BWD_EDGE_GATHER = 6
+MAXK_BWD_BINNED = 7
+MAXK_BWD_BINNED_EDGE = 8
+MAXK_BIN_DESTS = 255
+MAXK_BIN_WINDOW = 64
 MAXK_TOPK_ORDER_COLUMN = 0
 MAXK_TOPK_ORDER_VALUE = 1
 MAXK_TOPK_ORDER_LANE = 2
@@ -99,6 +103,12 @@ SIGNATURES = {
     "maxk_topk_cbsr": (_I, [_P, _I, _I, _L, _I, _I, _P, _P, _P, _P]),
     "maxk_cbsr_scatter": (_I, [_P, _P, _I, _I, _I, _P, _P]),
     "maxk_cbsr_mask": (_I, [_P, _P, _I, _I, _I, _P, _P]),
+    "maxk_bin_plan_workspace_bytes": (_S, [_L, _I]),
+    "maxk_bin_plan_build": (_I, [_P, _L, _P, _L, _I, _P, _P, _P, _L, ctypes.POINTER(ctypes.c_int64),
+                                 _P, _S, _P]),
+    "maxk_backward_binned_workspace_bytes": (_S, [_L, _I]),
+    "maxk_sspmm_backward_binned": (_I, [_P, _L, _P, _P, _P, _P, _P, _I, _I, _I, _L, _I, _I, _P, _P,
+                                        _P, _P, _I, _L, _P, _S, _P]),
     "maxk_spmm_forward_warp4": (_I, [_P, _P, _P, _P, _P, _P, _I, _I, _I, _I, _I, _P]),
     "maxk_spmm_backward_warp4": (_I, [_P, _P, _P, _P, _P, _P, _I, _I, _I, _I, _I, _P]),
 }

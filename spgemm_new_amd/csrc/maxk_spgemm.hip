@@ -1176,9 +1176,17 @@ struct PRow {
     static constexpr int KP = K == 8 ? 16 : K;
 };
 
-// CSRP: P rows in edge (CSR) order -- P[e] -- written as one sequential stream
-// (unpadded; the EDGE_GATHER segmented sum gathers them per destination).
-template <int K, bool ESEL = false, bool CSRP = false>
+// Where the products go (PM): kPmCsc -- P[csc_pos[e]], rows padded (PRow);
+// kPmEdge -- P rows in edge (CSR) order, P[e], written as one sequential stream
+// (unpadded; the EDGE_GATHER segmented sum gathers them per destination);
+// kPmBin -- P[bin_pos[e]], unpadded: the BINNED backward's destination bins,
+// each bin's slots in (XCD, edge) order (maxk_bin_plan_build), so the rows a
+// wave scatters land in lines its XCD's L2 fills before writing them back --
+// plain stores, to be combined there (non-temporal ones would go out as
+// partial lines).
+constexpr int kPmCsc = 0, kPmEdge = 1, kPmBin = 2;
+
+template <int K, bool ESEL = false, int PM = kPmCsc>
 __device__ __forceinline__ void bwd_edges_stage_vec(int e0, int e1,
                                                     const int32_t *__restrict__ idx,
                                                     const float *__restrict__ val,
@@ -1186,7 +1194,8 @@ __device__ __forceinline__ void bwd_edges_stage_vec(int e0, int e1,
                                                     const uint8_t *__restrict__ sel,
                                                     const float *gs, float *__restrict__ P)
 {
-    constexpr int KP = CSRP ? K : PRow<K>::KP;
+    constexpr bool CSRP = PM == kPmEdge;
+    constexpr int KP = PM == kPmCsc ? PRow<K>::KP : K;
     constexpr int LPE = KP / 4;
     constexpr int EPS = kWave / LPE;
     constexpr int STEPS = kWave / EPS;
@@ -1230,7 +1239,13 @@ __device__ __forceinline__ void bwd_edges_stage_vec(int e0, int e1,
                     }
                     // non-temporal: plain stores measured slower (Reddit 6.60 -> 6.97 ms,
                     // products 7.85 -> 8.20 ms): the staging lines would evict selector lines
-                    __builtin_nontemporal_store(o, reinterpret_cast<f4 *>(P + (size_t)p * KP + sub * 4));
+                    f4 *dst = reinterpret_cast<f4 *>(P + (size_t)p * KP + sub * 4);
+#ifndef MAXK_BIN_NT_STORE
+                    if constexpr (PM == kPmBin)
+                        *dst = o;
+                    else
+#endif
+                        __builtin_nontemporal_store(o, dst);
                 }
             }
         }
@@ -1255,7 +1270,7 @@ __device__ __forceinline__ void bwd_edges_stage_scalar(int e0, int e1, int k,
 }
 
 // Panel-scheduled backward push (ATOMIC when P == nullptr, STAGED otherwise).
-template <int K, bool STAGED, bool ESEL = false, bool CSRP = false>
+template <int K, bool STAGED, bool ESEL = false, int PM = kPmCsc>
 __global__ __launch_bounds__(kBlock) void bwd_panel_kernel(
     const int2 *__restrict__ sched, int64_t num_panels, const int32_t *__restrict__ indptr,
     const int32_t *__restrict__ idx, const float *__restrict__ val,
@@ -1279,7 +1294,7 @@ __global__ __launch_bounds__(kBlock) void bwd_panel_kernel(
         stage_row(gs, grad + (size_t)r * dim, dim);
         if constexpr (STAGED) {
             if constexpr (K > 0)
-                bwd_edges_stage_vec<K, ESEL, CSRP>(eb, ee, idx, val, csc_pos, sel, gs, P);
+                bwd_edges_stage_vec<K, ESEL, PM>(eb, ee, idx, val, csc_pos, sel, gs, P);
             else
                 bwd_edges_stage_scalar(eb, ee, k, idx, val, csc_pos, sel, gs, P, ESEL);
         } else {
@@ -1403,6 +1418,79 @@ __global__ __launch_bounds__(kBlock) void bwd_segsum_kernel(
         }
         if (lane == 0) carry_row[w] = has ? i1 : -1;
     }
+}
+
+// BINNED phase 2 (propagation blocking): destination bin b = columns
+// [b*255, b*255 + 255) is summed by one wave in LDS (255 x K floats).  Its
+// slots P[bin_ptr[b] .. bin_ptr[b+1]) come in windows of 64 whose destinations
+// are distinct (maxk_bin_plan_build packs them so), so one lane per slot adds
+// its row into the destination's LDS row with a plain read-add-write: no two
+// lanes of an instruction touch one row, and the wave's LDS operations are in
+// order.  Padding slots carry destination 0xFF.  U windows of rows are loaded
+// before their adds.  Summation order per destination = slot order, fixed by
+// the plan: deterministic.
+constexpr int kBinDests = MAXK_BIN_DESTS;
+
+template <int K>
+__global__ __launch_bounds__(kWave) void bwd_bin_sum_kernel(const int32_t *__restrict__ bin_ptr,
+                                                           int num_bins,
+                                                           const uint8_t *__restrict__ bin_dst,
+                                                           const float *__restrict__ P,
+                                                           int num_cols, float *__restrict__ dxs)
+{
+    constexpr int Q = K / 4;                       // float4 per row
+    constexpr int QS = Q + 1;                      // LDS row stride in float4: a pad quad
+                                                   // spreads a window's rows over the banks
+    constexpr int U = K == 32 ? 3 : 6;             // windows in flight (register ring)
+    extern __shared__ __attribute__((aligned(16))) float lds[];   // one wave per block
+    const int lane = lane_id();
+    f4 *acc = reinterpret_cast<f4 *>(lds);
+    for (int i = lane; i < kBinDests * QS; i += kWave) acc[i] = f4{0.f, 0.f, 0.f, 0.f};
+    const int64_t b = blockIdx.x;
+    if (b >= num_bins) return;
+    const int q0 = bin_ptr[b];
+    const int nw = (bin_ptr[b + 1] - q0) / kWave;  // windows of 64 slots
+    if (nw > 0) {
+    const f4 *P4 = reinterpret_cast<const f4 *>(P) + (size_t)q0 * Q;
+    const uint8_t *D = bin_dst + q0;
+    // ring of U windows: window w sits in slot w % U; after its adds the slot
+    // is refilled with window w + U (clamped: the last windows reload a valid
+    // one instead of branching, so every step issues the same loads)
+    uint32_t d[U];
+    f4 v[U][Q];
+    const int last = nw - 1;
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+        const int w = u < last ? u : last;
+        d[u] = __builtin_nontemporal_load(D + w * kWave + lane);
+#pragma unroll
+        for (int j = 0; j < Q; ++j)
+            v[u][j] = __builtin_nontemporal_load(P4 + (size_t)(w * kWave + lane) * Q + j);
+    }
+    for (int w0 = 0; w0 < nw; w0 += U) {
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            if (w0 + u < nw && d[u] != 0xFFu) {
+                f4 *a = acc + d[u] * QS;
+#pragma unroll
+                for (int j = 0; j < Q; ++j) {
+                    f4 t = a[j];
+                    t.x += v[u][j].x; t.y += v[u][j].y; t.z += v[u][j].z; t.w += v[u][j].w;
+                    a[j] = t;
+                }
+            }
+            const int wn = w0 + u + U < last ? w0 + u + U : last;
+            d[u] = __builtin_nontemporal_load(D + wn * kWave + lane);
+#pragma unroll
+            for (int j = 0; j < Q; ++j)
+                v[u][j] = __builtin_nontemporal_load(P4 + (size_t)(wn * kWave + lane) * Q + j);
+        }
+    }
+    }
+    const int64_t c0 = b * kBinDests;
+    const int rows = (int)((num_cols - c0) < kBinDests ? (num_cols - c0) : kBinDests);
+    f4 *out = reinterpret_cast<f4 *>(dxs + c0 * K);
+    for (int i = lane; i < rows * Q; i += kWave) out[i] = acc[(i / Q) * QS + i % Q];
 }
 
 // Backward, warp4-driven (drop-in): atomic push, G staged per row change.
@@ -3183,17 +3271,34 @@ struct BwdPanel {
     static int run(bool staged, const int32_t *sched, int64_t P, const int32_t *indptr,
                    const int32_t *idx, const float *val, const float *grad, const uint8_t *sel,
                    const int32_t *csc_pos, int V, int dim, int k, float *dxs, float *Pbuf,
-                   hipStream_t st, bool esel = false, bool csrp = false)
+                   hipStream_t st, bool esel = false, int pm = kPmCsc)
     {
         const int64_t blocks = ceil_div(P, kWavesPerBlock);
-        if (csrp) {  // EDGE_GATHER phase 1 (edge selectors, P in edge order)
+        if (pm == kPmEdge) {  // EDGE_GATHER phase 1 (edge selectors, P in edge order)
             if constexpr (K == 0) {
                 return MAXK_E_DIM;
             } else {
-                hipLaunchKernelGGL((bwd_panel_kernel<K, true, true, true>), dim3((unsigned)blocks),
+                hipLaunchKernelGGL((bwd_panel_kernel<K, true, true, kPmEdge>), dim3((unsigned)blocks),
                                    dim3(kBlock), row_lds_bytes(), st,
                                    reinterpret_cast<const int2 *>(sched), P, indptr, idx, val,
                                    grad, sel, csc_pos, V, dim, k, dxs, Pbuf);
+                return launch_status();
+            }
+        }
+        if (pm == kPmBin) {  // BINNED phase 1: csc_pos = bin_pos
+            if constexpr (K != 8 && K != 16 && K != 32) {
+                return MAXK_E_DIM;
+            } else {
+                if (esel)
+                    hipLaunchKernelGGL((bwd_panel_kernel<K, true, true, kPmBin>),
+                                       dim3((unsigned)blocks), dim3(kBlock), row_lds_bytes(), st,
+                                       reinterpret_cast<const int2 *>(sched), P, indptr, idx, val,
+                                       grad, sel, csc_pos, V, dim, k, dxs, Pbuf);
+                else
+                    hipLaunchKernelGGL((bwd_panel_kernel<K, true, false, kPmBin>),
+                                       dim3((unsigned)blocks), dim3(kBlock), row_lds_bytes(), st,
+                                       reinterpret_cast<const int2 *>(sched), P, indptr, idx, val,
+                                       grad, sel, csc_pos, V, dim, k, dxs, Pbuf);
                 return launch_status();
             }
         }
@@ -3666,11 +3771,63 @@ int maxk_sspmm_backward(int algo, const int32_t *sched, int64_t num_panels,
                                                      carry_bytes);
     int rc = dispatch_k<BwdPanel>(dim_k, true, sched, num_panels, indptr, indices, values, grad,
                                   cbsr_sel, csc_pos, num_rows, dim_origin, dim_k, dxs, Pbuf, st,
-                                  esel, gather);
+                                  esel, gather ? kPmEdge : kPmCsc);
     if (rc) return rc;
     return dispatch_k<BwdSegsum>(dim_k, csc_sched, csc_num_panels, csc_indptr, Pbuf, num_cols,
                                  dim_k, dxs, carry, carry_row, st,
                                  gather ? csc_pos : (const int32_t *)nullptr);
+}
+
+size_t maxk_backward_binned_workspace_bytes(int64_t num_slots, int dim_k)
+{
+    if (num_slots < 0 || (dim_k != 8 && dim_k != 16 && dim_k != 32)) return 0;
+    return align_up((size_t)num_slots * dim_k * sizeof(float), 256);
+}
+
+int maxk_sspmm_backward_binned(const int32_t *sched, int64_t num_panels, const int32_t *indptr,
+                               const int32_t *indices, const float *values, const float *grad,
+                               const uint8_t *sel, int edge_selectors, int num_rows, int num_cols,
+                               int64_t num_edges, int dim_origin, int dim_k, float *dxs,
+                               const int32_t *bin_pos, const int32_t *bin_ptr,
+                               const uint8_t *bin_dst, int num_bins, int64_t num_slots,
+                               void *workspace, size_t workspace_bytes, void *stream)
+{
+    if (!sched || !indptr || !dxs || num_panels < 1 || num_rows < 0 || num_cols < 0 ||
+        num_edges < 0 || num_slots < 0)
+        return MAXK_E_ARG;
+    if (!dims_ok(dim_origin, dim_k)) return MAXK_E_DIM;
+    if (dim_k != 8 && dim_k != 16 && dim_k != 32) return MAXK_E_DIM;
+    hipStream_t st = as_stream(stream);
+    if (num_cols == 0) return MAXK_OK;
+    if (num_rows == 0 || num_edges == 0) return zero_floats(dxs, (size_t)num_cols * dim_k, st);
+    if (!indices || !values || !grad || !sel || !bin_pos || !bin_ptr || !bin_dst) return MAXK_E_ARG;
+    if (num_bins != (int)((num_cols + kBinDests - 1) / kBinDests) || num_slots < num_edges ||
+        num_slots > INT32_MAX)
+        return MAXK_E_ARG;
+    if (!workspace || workspace_bytes < maxk_backward_binned_workspace_bytes(num_slots, dim_k))
+        return MAXK_E_WORKSPACE;
+    float *Pbuf = static_cast<float *>(workspace);
+    int rc = dispatch_k<BwdPanel>(dim_k, true, sched, num_panels, indptr, indices, values, grad,
+                                  sel, bin_pos, num_rows, dim_origin, dim_k, dxs, Pbuf, st,
+                                  edge_selectors != 0, kPmBin);
+    if (rc) return rc;
+    const unsigned blocks = (unsigned)num_bins;      // one wave (block) per bin
+    const size_t lds = (size_t)kBinDests * (dim_k + 4) * sizeof(float);
+    switch (dim_k) {
+    case 8:
+        hipLaunchKernelGGL(bwd_bin_sum_kernel<8>, dim3(blocks), dim3(kWave), lds, st, bin_ptr,
+                           num_bins, bin_dst, Pbuf, num_cols, dxs);
+        break;
+    case 16:
+        hipLaunchKernelGGL(bwd_bin_sum_kernel<16>, dim3(blocks), dim3(kWave), lds, st, bin_ptr,
+                           num_bins, bin_dst, Pbuf, num_cols, dxs);
+        break;
+    default:
+        hipLaunchKernelGGL(bwd_bin_sum_kernel<32>, dim3(blocks), dim3(kWave), lds, st, bin_ptr,
+                           num_bins, bin_dst, Pbuf, num_cols, dxs);
+        break;
+    }
+    return launch_status();
 }
 
 size_t maxk_backward_local_lds_bytes(int dmax, int dim_k)

@@ -71,6 +71,10 @@ MIN_PANELS = int(os.environ.get("MAXK_MIN_PANELS", 16384))
 TILE_AUTO = os.environ.get("MAXK_TILE", "1") != "0"
 # STAGED_EDGE backward (edge selectors written by the forward) among the AUTO candidates
 ESEL_AUTO = os.environ.get("MAXK_ESEL", "1") != "0"
+# BINNED backward (destination bins summed in LDS, k in {8, 16, 32}) among the AUTO
+# candidates; its plan is dropped when window padding would exceed this many slots per edge
+BIN_AUTO = os.environ.get("MAXK_BIN", "1") != "0"
+BIN_MAX_SLOTS_PER_EDGE = 1.5
 # AUTO backward: "measure" (time the candidates once per graph and shape; the fastest
 # is kept) or "fixed" (a rule of the shape alone, no timing: the same algorithm -- and
 # so the same fp32 summation order -- on every run and machine)
@@ -134,7 +138,18 @@ def _validate_csr(indptr: torch.Tensor, indices: torch.Tensor, num_cols: int) ->
         raise RuntimeError(f"indices out of range: every column must be in [0, {num_cols})")
 
 
-_ESEL_ALGOS = (_lib.MAXK_BWD_STAGED_EDGE, _lib.MAXK_BWD_EDGE_GATHER)
+_ESEL_ALGOS = (_lib.MAXK_BWD_STAGED_EDGE, _lib.MAXK_BWD_EDGE_GATHER, _lib.MAXK_BWD_BINNED_EDGE)
+_BIN_ALGOS = (_lib.MAXK_BWD_BINNED, _lib.MAXK_BWD_BINNED_EDGE)
+
+
+_ALGO_NAMES = {_lib.MAXK_BWD_ATOMIC: "atomic", _lib.MAXK_BWD_STAGED: "staged",
+               _lib.MAXK_BWD_LOCAL: "local", _lib.MAXK_BWD_TILE: "tile",
+               _lib.MAXK_BWD_STAGED_EDGE: "staged_edge", _lib.MAXK_BWD_EDGE_GATHER: "edge_gather",
+               _lib.MAXK_BWD_BINNED: "binned", _lib.MAXK_BWD_BINNED_EDGE: "binned_edge"}
+
+
+def bin_shape_ok(dim_k: int) -> bool:
+    return dim_k in (8, 16, 32)
 
 
 def _edge_gather_ok(k: int) -> bool:
@@ -229,6 +244,7 @@ class MaxKGraph:
         self._esel_on = set()     # (k, h): forwards write edge selectors (AUTO chose STAGED_EDGE)
         self._esel = []           # [(sel key, sel, uint8 buffer[E * k], pinned)], most recent last
         self.last_bwd_algo = None
+        self._bin = None          # BINNED backward plan (False: padding too high)
         self._blocked = {}        # column-blocked forward plans, per block count
         self._fwd_blocks = {}     # (k, h) -> block count chosen (0: plain forward)
 
@@ -318,6 +334,43 @@ class MaxKGraph:
                        "maxk_csc_perm_build")
             self._csc_perm = perm
         return self._csc_perm
+
+    def bin_plan(self):
+        """Plan of the BINNED backward (maxk_sspmm_backward_binned), built once on
+        the device (maxk_bin_plan_build; one host read of the slot count), or None
+        when the graph has no edges or its destination windows would need more
+        than BIN_MAX_SLOTS_PER_EDGE slots per edge, plus the partly filled windows
+        that end each bin (hub destinations: a window holds each destination once).  Tied to bwd_sched (phase 1's panels)."""
+        if self._bin is None:
+            self._bin = False
+            E, C = self.num_edges, self.num_cols
+            if E > 0:
+                import ctypes
+                L = _lib.load()
+                ws = torch.empty(max(1, L.maxk_bin_plan_workspace_bytes(E, C)), dtype=torch.uint8,
+                                 device=self.device)
+                st = _stream(ws)
+                n = ctypes.c_int64(0)
+                args = (self.bwd_sched.data_ptr(), self.bwd_num_panels, self.indices.data_ptr(),
+                        E, C)
+                _lib.check(L.maxk_bin_plan_build(*args, None, None, None, 0, ctypes.byref(n),
+                                                 ws.data_ptr(), ws.numel(), st),
+                           "maxk_bin_plan_build(count)")
+                slots = int(n.value)
+                nb = -(-C // _lib.MAXK_BIN_DESTS)
+                # beyond the <= 8 partly filled windows every bin may end with
+                if slots <= BIN_MAX_SLOTS_PER_EDGE * E + nb * 8 * _lib.MAXK_BIN_WINDOW:
+                    pos = torch.empty(E, dtype=torch.int32, device=self.device)
+                    ptr = torch.empty(nb + 1, dtype=torch.int32, device=self.device)
+                    dst = torch.empty(slots, dtype=torch.uint8, device=self.device)
+                    _lib.check(L.maxk_bin_plan_build(*args, pos.data_ptr(), ptr.data_ptr(),
+                                                     dst.data_ptr(), slots, ctypes.byref(n),
+                                                     ws.data_ptr(), ws.numel(), st),
+                               "maxk_bin_plan_build")
+                    self._bin = {"bin_pos": pos, "bin_ptr": ptr, "bin_dst": dst,
+                                 "num_bins": nb, "num_slots": slots}
+                del ws
+        return self._bin or None
 
     def local_plan(self, dim_k: int):
         """Plan of the LOCAL backward (maxk_sspmm_backward_local), or None when
@@ -557,6 +610,9 @@ class MaxKGraph:
             cands.append(_lib.MAXK_BWD_LOCAL)
         if tile_ok and self.tile_plan(k) is not None:
             cands.append(_lib.MAXK_BWD_TILE)
+        bin_ok = BIN_AUTO and bin_shape_ok(k) and self.bin_plan() is not None
+        if bin_ok:
+            cands.append(_lib.MAXK_BWD_BINNED)
         pair = None
         if ESEL_AUTO and grad.shape[1] <= 256:
             # STAGED_EDGE moves work into the forward (it writes the edge
@@ -567,6 +623,8 @@ class MaxKGraph:
             cands.append(_lib.MAXK_BWD_STAGED_EDGE)
             if _edge_gather_ok(k):
                 cands.append(_lib.MAXK_BWD_EDGE_GATHER)
+            if bin_ok:
+                cands.append(_lib.MAXK_BWD_BINNED_EDGE)
             dummy = self._workspace(("esel_data", k), self.num_cols * k * 4)
             dummy = dummy[: self.num_cols * k * 4].view(torch.float32).view(self.num_cols, k)
             yd = torch.empty((self.num_rows, grad.shape[1]), dtype=torch.float32,
@@ -576,11 +634,13 @@ class MaxKGraph:
                 spgemm_forward(self, dummy, sel, grad.shape[1], out=yd, edge_sel=a in _ESEL_ALGOS)
                 sspmm_backward(self, grad, sel, out, values, a)
         best, best_ms, alt, alt_ms = None, float("inf"), None, float("inf")
+        timed = {}
         for a in cands:
             if pair is not None:
                 ms = _min_ms(lambda: pair(a))
             else:
                 ms = _min_ms(lambda: sspmm_backward(self, grad, sel, out, values, a))
+            timed[_ALGO_NAMES[a]] = round(ms, 4)
             if a not in _ESEL_ALGOS and ms < alt_ms:
                 alt, alt_ms = a, ms
             if ms < best_ms:
@@ -591,6 +651,9 @@ class MaxKGraph:
             self._esel_on.add((k, grad.shape[1]))
         self.bwd_timings = getattr(self, "bwd_timings", {})
         self.bwd_timings[key] = best_ms
+        # every candidate's time (forward + backward when the edge-selector ones ran)
+        self.bwd_candidates = getattr(self, "bwd_candidates", {})
+        self.bwd_candidates[key] = timed
         return best
 
     def nbytes_fwd(self, dim_k: int, dim_origin: int) -> int:
@@ -1072,6 +1135,23 @@ def sspmm_backward(g: MaxKGraph, grad, sel, out=None, values=None, algo: int = _
             plan["edge_rc"].data_ptr(), ev.data_ptr(), grad.data_ptr(),
             sel.data_ptr(), g.num_rows, dim_origin, k, out.data_ptr(), _stream(out)),
             "maxk_sspmm_backward_local")
+        return out
+    if algo in _BIN_ALGOS:
+        plan = g.bin_plan() if bin_shape_ok(k) else None
+        if plan is None:
+            raise RuntimeError("BINNED backward unsupported for this graph / shape (k in {8, 16, 32})")
+        edge = algo == _lib.MAXK_BWD_BINNED_EDGE
+        sel_arg = g.make_edge_selectors(sel) if edge else sel
+        ws = g._workspace(("bwd_bin", k),
+                          L.maxk_backward_binned_workspace_bytes(plan["num_slots"], k))
+        g.last_bwd_algo = "binned_edge" if edge else "binned"
+        _lib.check(L.maxk_sspmm_backward_binned(
+            g.bwd_sched.data_ptr(), g.bwd_num_panels, g.indptr.data_ptr(), g.indices.data_ptr(),
+            values.data_ptr(), grad.data_ptr(), sel_arg.data_ptr(), int(edge), g.num_rows,
+            g.num_cols, g.num_edges, dim_origin, k, out.data_ptr(), plan["bin_pos"].data_ptr(),
+            plan["bin_ptr"].data_ptr(), plan["bin_dst"].data_ptr(), plan["num_bins"],
+            plan["num_slots"], ws.data_ptr(), ws.numel(), _stream(out)),
+            "maxk_sspmm_backward_binned")
         return out
     csc_pos = csc_indptr = csc_sched = None
     CP = 0
