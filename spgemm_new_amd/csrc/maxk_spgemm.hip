@@ -1441,7 +1441,7 @@ __global__ __launch_bounds__(kWave) void bwd_bin_sum_kernel(const int32_t *__res
     constexpr int Q = K / 4;                       // float4 per row
     constexpr int QS = Q + 1;                      // LDS row stride in float4: a pad quad
                                                    // spreads a window's rows over the banks
-    constexpr int U = K == 32 ? 3 : 6;             // windows in flight (register ring)
+    constexpr int U = K == 32 ? 2 : K == 16 ? 4 : 6;   // windows per register batch
     extern __shared__ __attribute__((aligned(16))) float lds[];   // one wave per block
     const int lane = lane_id();
     f4 *acc = reinterpret_cast<f4 *>(lds);
@@ -1453,21 +1453,23 @@ __global__ __launch_bounds__(kWave) void bwd_bin_sum_kernel(const int32_t *__res
     if (nw > 0) {
     const f4 *P4 = reinterpret_cast<const f4 *>(P) + (size_t)q0 * Q;
     const uint8_t *D = bin_dst + q0;
-    // ring of U windows: window w sits in slot w % U; after its adds the slot
-    // is refilled with window w + U (clamped: the last windows reload a valid
-    // one instead of branching, so every step issues the same loads)
-    uint32_t d[U];
-    f4 v[U][Q];
+    // two batches of U windows in registers: batch i + 1 is loaded before
+    // batch i is added, so a wave always has U windows of loads in flight;
+    // batches past the end reload the last window (no branch around loads)
     const int last = nw - 1;
+    uint32_t da[U], db[U];
+    f4 va[U][Q], vb[U][Q];
+    auto load = [&](uint32_t (&d)[U], f4 (&v)[U][Q], int w0) {
 #pragma unroll
-    for (int u = 0; u < U; ++u) {
-        const int w = u < last ? u : last;
-        d[u] = __builtin_nontemporal_load(D + w * kWave + lane);
+        for (int u = 0; u < U; ++u) {
+            const int w = w0 + u < last ? w0 + u : last;
+            d[u] = __builtin_nontemporal_load(D + w * kWave + lane);
 #pragma unroll
-        for (int j = 0; j < Q; ++j)
-            v[u][j] = __builtin_nontemporal_load(P4 + (size_t)(w * kWave + lane) * Q + j);
-    }
-    for (int w0 = 0; w0 < nw; w0 += U) {
+            for (int j = 0; j < Q; ++j)
+                v[u][j] = __builtin_nontemporal_load(P4 + (size_t)(w * kWave + lane) * Q + j);
+        }
+    };
+    auto add = [&](const uint32_t (&d)[U], const f4 (&v)[U][Q], int w0) {
 #pragma unroll
         for (int u = 0; u < U; ++u) {
             if (w0 + u < nw && d[u] != 0xFFu) {
@@ -1479,12 +1481,15 @@ __global__ __launch_bounds__(kWave) void bwd_bin_sum_kernel(const int32_t *__res
                     a[j] = t;
                 }
             }
-            const int wn = w0 + u + U < last ? w0 + u + U : last;
-            d[u] = __builtin_nontemporal_load(D + wn * kWave + lane);
-#pragma unroll
-            for (int j = 0; j < Q; ++j)
-                v[u][j] = __builtin_nontemporal_load(P4 + (size_t)(wn * kWave + lane) * Q + j);
         }
+    };
+    load(da, va, 0);
+    for (int w0 = 0; w0 < nw; w0 += 2 * U) {
+        load(db, vb, w0 + U);
+        add(da, va, w0);
+        if (w0 + U >= nw) break;
+        load(da, va, w0 + 2 * U);
+        add(db, vb, w0 + U);
     }
     }
     const int64_t c0 = b * kBinDests;
