@@ -2794,6 +2794,11 @@ __global__ __launch_bounds__(kTileWaves * kWave) void bwd_tile_kernel(
 #ifndef TILE_PF_AHEAD
 #define TILE_PF_AHEAD 128  // dwords: the window starts 512 B past the chunk's records
 #endif
+#ifndef TILE_KPF
+// record groups 3 and 4 pulled into the scalar cache with the first two (0 or 2; 4
+// measured no better): Reddit k=32 2.81 -> 2.78 ms
+#define TILE_KPF 2
+#endif
 #ifndef TILE_ABLATE
 #define TILE_ABLATE 0  // development timing ablations (results wrong): bits 1 / 2 / 4 / 8 below
 #endif
@@ -2827,11 +2832,32 @@ __global__ __launch_bounds__(kTileWaves * kWave) void bwd_tile_kernel(
         // the chunk's first record groups, in flight across the barrier (four-word
         // records: pinned to s[64:79] / s[80:95], where the record asm reads them)
         tile_g16_t pa, pb;
+#if TILE_KPF
+        // groups 3..2+TILE_KPF pulled into the scalar cache with the first two, so
+        // that the loop's s_loads hit it (their lgkmcnt waits also wait for the
+        // LDS reads; a K$ hit keeps that short); dummies stay live to the wait
+        uint32_t kp[4];
+        const uint32_t *rp = rb + (ro >> 2);
+        if constexpr (kTileRecWords == 4)
+            asm volatile("s_load_dwordx16 s[64:79], %6, 0x0\n\t"
+                         "s_load_dwordx16 s[80:95], %6, 0x40\n\t"
+                         "s_load_dword %2, %6, 0x80\n\t"
+                         "s_load_dword %3, %6, 0xc0\n\t"
+                         ".if %7 > 2\n\t"
+                         "s_load_dword %4, %6, 0x100\n\t"
+                         "s_load_dword %5, %6, 0x140\n\t"
+                         ".endif"
+                         : "=&{s[64:79]}"(pa), "=&{s[80:95]}"(pb), "=&s"(kp[0]), "=&s"(kp[1]),
+                           "=&s"(kp[2]), "=&s"(kp[3])
+                         : "s"(rp), "n"(TILE_KPF) : "memory");
+        else
+#else
         if constexpr (kTileRecWords == 4)
             asm volatile("s_load_dwordx16 s[64:79], %2, %3\n\ts_load_dwordx16 s[80:95], %2, %4"
                          : "=&{s[64:79]}"(pa), "=&{s[80:95]}"(pb)
                          : "s"(rb), "s"(ro), "s"(ro + 64) : "memory");
         else
+#endif
             asm volatile("s_load_dwordx16 %0, %2, %3\n\ts_load_dwordx16 %1, %2, %4"
                          : "=&s"(pa), "=&s"(pb) : "s"(rb), "s"(ro), "s"(ro + 64) : "memory");
         // this wave's DMA of chunk c and header of chunk c landed; after the
@@ -2866,7 +2892,12 @@ __global__ __launch_bounds__(kTileWaves * kWave) void bwd_tile_kernel(
         // returns out of order), i.e. stale records, on graphs with empty
         // wave-chunks (products k=32: runs differed in the last bits)
         if constexpr (kTileRecWords == 4) {
+#if TILE_KPF
+            asm volatile("s_waitcnt lgkmcnt(0)" : "+{s[64:79]}"(pa), "+{s[80:95]}"(pb),
+                         "+s"(kp[0]), "+s"(kp[1]), "+s"(kp[2]), "+s"(kp[3])::"memory");
+#else
             asm volatile("s_waitcnt lgkmcnt(0)" : "+{s[64:79]}"(pa), "+{s[80:95]}"(pb)::"memory");
+#endif
             tile_groups2_r16(pa, pb, n, m, lo, hi, selv, acc0, acc1);
             tile_group_loop_r16(rb, ro + 128, n, m, lo, hi, selv, acc0, acc1);
             ro += 64 * gn;

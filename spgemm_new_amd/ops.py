@@ -610,7 +610,10 @@ class MaxKGraph:
             cands.append(_lib.MAXK_BWD_LOCAL)
         if tile_ok and self.tile_plan(k) is not None:
             cands.append(_lib.MAXK_BWD_TILE)
-        bin_ok = BIN_AUTO and bin_shape_ok(k) and self.bin_plan() is not None
+        # (k <= 16 only: at k = 32 the records are whole lines and STAGED's layout
+        # serves as well, and the plan's per-bin packing is slow on graphs with few
+        # bins -- Reddit: 914 bins of 125 K edges, 0.45 s)
+        bin_ok = BIN_AUTO and k in (8, 16) and self.bin_plan() is not None
         if bin_ok:
             cands.append(_lib.MAXK_BWD_BINNED)
         pair = None

@@ -22,3 +22,13 @@ for path in glob.glob(root + "/**/*counter_collection.csv", recursive=True):
         n = max(len(v) for v in cs.values())
         if any(x > 1e5 for x in vals.values()):
             print(f"PMC {n:4d} " + " ".join(f"{c}={x / 1e9:.3f}G" for c, x in vals.items()) + f"  {k}")
+# KT_SERIES=<substring>: the last 24 durations of every kernel whose name holds it
+import os  # noqa: E402
+pat = os.environ.get("KT_SERIES")
+if pat:
+    for path in glob.glob(root + "/**/*kernel_trace.csv", recursive=True):
+        rows = [r for r in csv.DictReader(open(path)) if pat in r["Kernel_Name"]]
+        rows.sort(key=lambda r: int(r["Start_Timestamp"]))
+        for r in rows[-24:]:
+            print(f"SERIES {(int(r['End_Timestamp']) - int(r['Start_Timestamp'])) / 1e6:8.3f} ms  "
+                  f"{r['Kernel_Name'][:100]}")
