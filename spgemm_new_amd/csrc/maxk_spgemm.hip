@@ -168,9 +168,15 @@ __global__ __launch_bounds__(256) void exclusive_scan_1block(int32_t *c, int n, 
 // EPS = 64 / LPE edges per step = LDS row copies.  LPE >= 8 keeps the copies
 // at <= 8 KB per wave for every k >= 8.
 // ---------------------------------------------------------------------------
+#ifndef FWD_VEC16
+#define FWD_VEC16 2   // CBSR entries per lane at k = 16 (development knob)
+#endif
+#ifndef FWD_VEC8
+#define FWD_VEC8 1    // ... at k = 8
+#endif
 template <int K>
 struct FwdLayout {
-    static constexpr int VEC = K >= 32 ? 4 : (K >= 16 ? 2 : 1);
+    static constexpr int VEC = K >= 32 ? 4 : (K >= 16 ? FWD_VEC16 : (K >= 8 ? FWD_VEC8 : 1));
     static constexpr int LPE = K / VEC;
     static constexpr int EPS = kWave / LPE;
 };
