@@ -56,6 +56,8 @@ def test_bench_two_ranks_rehearsal():
     assert d["n_gpus"] == 2 and d["config"]["parallelism"] == "rowpart2"
     assert d["value"] > 0 and d["roofline"]["achieved"] > 0
     assert d["config"]["halo_nodes_rank0"] > 0 and d["config"]["overlap"] is True
+    assert d["config"]["halo_mode"] in ("records", "allgather")
+    assert d["config"]["halo_bytes_rank0"]["reverse_bwd"] > 0
 
 
 @pytest.mark.gpu
