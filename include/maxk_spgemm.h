@@ -182,6 +182,12 @@ int maxk_spgemm_forward_esel(const int32_t *sched, int64_t num_panels, const int
 int maxk_segment_rows_add(const float *src, int width, const int64_t *order,
                           const int64_t *seg_off, const int64_t *seg_row, int64_t num_segments,
                           float *dst, void *stream);
+/* out_sel[i, :] = the dim_k selector bytes of record rows[i] of a records array
+ * (5*dim_k bytes per record, as maxk_cbsr_gather_records writes them): the halo
+ * columns' selectors out of an all-gathered table (PartitionedMaxK halo_mode
+ * "allgather"). */
+int maxk_records_sel_gather(const uint8_t *records, int dim_k, const int32_t *rows, int64_t n,
+                            uint8_t *out_sel, void *stream);
 int maxk_cbsr_gather_records(const float *cbsr_data, const uint8_t *cbsr_sel, const int32_t *rows,
                              int64_t num_records, int dim_k, void *records, void *stream);
 int maxk_spgemm_forward_records(const int32_t *sched, int64_t num_panels, const int32_t *indptr,

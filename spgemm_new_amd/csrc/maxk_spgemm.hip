@@ -3035,6 +3035,26 @@ __global__ __launch_bounds__(kBlock) void cbsr_records_kernel(const float *__res
     }
 }
 
+// out[i, :] = the selector bytes of record rows[i] (bytes 4K .. 5K of a 5K-byte
+// record): 16-B pieces when K % 16 == 0, else dwords
+template <int K>
+__global__ __launch_bounds__(kBlock) void records_sel_kernel(const uint8_t *__restrict__ rec,
+                                                             const int32_t *__restrict__ rows,
+                                                             int64_t n, uint8_t *__restrict__ out)
+{
+    constexpr int PB = K % 16 == 0 ? 16 : 4;   // piece bytes
+    constexpr int W = K / PB;                  // pieces per row
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n * W) return;
+    const int64_t j = i / W;
+    const int w = (int)(i - j * W);
+    const uint8_t *src = rec + (size_t)rows[j] * (5 * K) + 4 * K + (size_t)w * PB;
+    if constexpr (PB == 16)
+        reinterpret_cast<f4 *>(out)[i] = *reinterpret_cast<const f4 *>(src);
+    else
+        reinterpret_cast<uint32_t *>(out)[i] = *reinterpret_cast<const uint32_t *>(src);
+}
+
 // dst[seg_row[s], :] += sum over j in [seg_off[s], seg_off[s+1]) of src[order[j], :]
 // (width floats per row): the owners' sum of the halo partial sums their peers
 // returned, in a fixed order (no atomics; index_add_ took 0.23 ms on products
@@ -3674,6 +3694,27 @@ int maxk_spgemm_forward_esel(const int32_t *sched, int64_t num_panels, const int
     return dispatch_k<FwdPanel>(dim_k, sched, num_panels, indptr, indices, values, cbsr_data,
                                 cbsr_sel, num_rows, dim_origin, dim_k, out, carry, carry_row, owner,
                                 false, st, edge_sel);
+}
+
+int maxk_records_sel_gather(const uint8_t *records, int dim_k, const int32_t *rows, int64_t n,
+                            uint8_t *out_sel, void *stream)
+{
+    if (n < 0 || (n > 0 && (!records || !rows || !out_sel))) return MAXK_E_ARG;
+    if (dim_k < 4 || dim_k > 256 || (dim_k & (dim_k - 1))) return MAXK_E_DIM;
+    if (n == 0) return MAXK_OK;
+    hipStream_t st = as_stream(stream);
+    const int64_t pieces = n * (dim_k % 16 == 0 ? dim_k / 16 : dim_k / 4);
+    const dim3 g((unsigned)ceil_div(pieces, kBlock));
+    switch (dim_k) {
+    case 4: hipLaunchKernelGGL(records_sel_kernel<4>, g, dim3(kBlock), 0, st, records, rows, n, out_sel); break;
+    case 8: hipLaunchKernelGGL(records_sel_kernel<8>, g, dim3(kBlock), 0, st, records, rows, n, out_sel); break;
+    case 16: hipLaunchKernelGGL(records_sel_kernel<16>, g, dim3(kBlock), 0, st, records, rows, n, out_sel); break;
+    case 32: hipLaunchKernelGGL(records_sel_kernel<32>, g, dim3(kBlock), 0, st, records, rows, n, out_sel); break;
+    case 64: hipLaunchKernelGGL(records_sel_kernel<64>, g, dim3(kBlock), 0, st, records, rows, n, out_sel); break;
+    case 128: hipLaunchKernelGGL(records_sel_kernel<128>, g, dim3(kBlock), 0, st, records, rows, n, out_sel); break;
+    default: hipLaunchKernelGGL(records_sel_kernel<256>, g, dim3(kBlock), 0, st, records, rows, n, out_sel); break;
+    }
+    return launch_status();
 }
 
 int maxk_cbsr_gather_records(const float *cbsr_data, const uint8_t *cbsr_sel, const int32_t *rows,

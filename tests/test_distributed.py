@@ -551,3 +551,23 @@ def test_allgather_halo_mode_bitwise_equals_records(world):
     assert len({f[1] for f in flags}) == 1          # one collective on every rank
     for same, mode, nbytes in flags:
         assert nbytes["allgather_fwd"] >= nbytes["records_fwd"] > 0
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("k", [4, 8, 16, 32, 64])
+def test_records_sel_gather(k):
+    """maxk_records_sel_gather (the all-gather halo mode's selector gather) equals
+    the selector rows of the records it reads."""
+    from spgemm_new_amd import _lib
+    from spgemm_new_amd.ops import cbsr_gather_records
+    dev = torch.device("cuda:0")
+    n_rows = 3001
+    data = torch.rand((n_rows, k), device=dev)
+    sel = torch.randint(0, 256, (n_rows, k), dtype=torch.uint8, device=dev)
+    rec = cbsr_gather_records(data, sel)
+    rows = torch.randint(0, n_rows, (777,), dtype=torch.int32, device=dev)
+    out = torch.empty((777, k), dtype=torch.uint8, device=dev)
+    _lib.check(_lib.load().maxk_records_sel_gather(rec.data_ptr(), k, rows.data_ptr(), 777,
+                                                    out.data_ptr(), _lib.stream_ptr(dev)),
+               "maxk_records_sel_gather")
+    assert torch.equal(out, sel[rows.long()])

@@ -59,6 +59,24 @@ class Loopback:
 
 
 import spgemm_new_amd.ops as D_ops  # noqa: E402
+from spgemm_new_amd import _lib as D_lib  # noqa: E402
+
+
+class GatherLoopback:
+    """Stands in for the all-gather of the "allgather" halo mode: the table of
+    every rank's own records, rank q's block at rows q * max_own ..."""
+
+    def __init__(self, bounds, data, sel):
+        self.bounds, self.data, self.sel = bounds, data, sel
+
+    def __call__(self, out, inp, async_op=False):
+        world = len(self.bounds) - 1
+        max_own = out.shape[0] // world
+        for q in range(world):
+            r0, r1 = self.bounds[q], self.bounds[q + 1]
+            rows = torch.arange(r0, r1, device=out.device, dtype=torch.int32)
+            D_ops.cbsr_gather_records(self.data, self.sel, rows, out=out[q * max_own:q * max_own + r1 - r0])
+        return D._Done() if async_op else out
 
 
 def timed(fn, reps=20):
@@ -81,6 +99,7 @@ def main():
     ap.add_argument("--h", type=int, default=256)
     ap.add_argument("--worlds", default="1,2,4,8")
     ap.add_argument("--rows", action="store_true", help="unpacked-rows halo path (no records)")
+    ap.add_argument("--halo-mode", default="records", choices=["records", "allgather"])
     a = ap.parse_args()
     dev = torch.device("cuda:0")
     V, E = CONFIGS[a.graph]
@@ -97,17 +116,33 @@ def main():
         for p in sorted({0, world - 1}):
             lb = Loopback(indptr, indices, bounds, p, data, sel)
             D.a2a = lb
-            m = D.PartitionedMaxK(indptr, indices, values, p, world, dev, records=not a.rows)
+            D.ag = GatherLoopback(bounds, data, sel)
+            m = D.PartitionedMaxK(indptr, indices, values, p, world, dev, records=not a.rows,
+                                  halo_mode=a.halo_mode if world > 1 else "records")
             d_l, s_l, g_l = m.local_rows(data), m.local_rows(sel), m.local_rows(G)
             tf = timed(lambda: m.forward(d_l, s_l, h))
             tb = timed(lambda: m.backward(g_l, s_l))
             ts = timed(lambda: (m.forward(d_l, s_l, h), m.backward(g_l, s_l)))
             pl = m.plan
+            if m.halo_mode == "allgather":
+                max_own, pos, eng = m._table()
+                tab = m._bufs[("ag_table", k)]
+                y_h = torch.empty((pl.num_own, h), device=dev)
+                parts = {
+                    "table (loopback all-gather)": lambda: D.ag(tab, None),
+                    "halo part over table": lambda: eng.forward_records(tab, k, h, out=y_h,
+                                                                        accumulate=True),
+                    "halo selectors": lambda: D_lib.load().maxk_records_sel_gather(
+                        tab.data_ptr(), k, pos.data_ptr(), pl.num_halo,
+                        m._bufs[("ag_halo_sel", k)].data_ptr(), D_lib.stream_ptr(dev)),
+                    "own part": lambda: m.local_own.forward(d_l, s_l, h),
+                }
+                print("   " + ", ".join(f"{n} {timed(f, reps=10):.3f}" for n, f in parts.items()))
             print(f"world={world} rank={p}: own={pl.num_own} halo={pl.num_halo} "
                   f"send={m.send_rows.numel()} edges={pl.local_indices.numel()} | fwd {tf:.3f} "
                   f"bwd {tb:.3f} step {ts:.3f} ms (no wire time) | halo fwd "
                   f"{pl.num_halo * 5 * k / 1e6:.1f} MB in, {m.send_rows.numel() * 5 * k / 1e6:.1f}"
-                  f" MB out; bwd algo {m.local.last_bwd_algo}", flush=True)
+                  f" MB out; bwd algo {m.local.last_bwd_algo}; halo mode {m.halo_mode}", flush=True)
             del m, lb, d_l, s_l, g_l
             torch.cuda.empty_cache()
 
@@ -129,7 +164,7 @@ def breakdown(graph="products", k=32, world=8, rank=0):
     bounds = D.row_partition(indptr, world)
     lb = Loopback(indptr, indices, bounds, rank, data, sel)
     D.a2a = lb
-    m = D.PartitionedMaxK(indptr, indices, values, rank, world, dev)
+    m = D.PartitionedMaxK(indptr, indices, values, rank, world, dev, halo_mode="records")
     d_l, s_l, g_l = m.local_rows(data), m.local_rows(sel), m.local_rows(G)
     m.forward(d_l, s_l, h)
     m.backward(g_l, s_l)
