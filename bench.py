@@ -52,6 +52,9 @@ def parse():
     p.add_argument("--partitioned", action="store_true",
                    help="use the multi-GPU (row partition + halo exchange) path even at N=1")
     p.add_argument("--verbose", action="store_true")
+    p.add_argument("--overlap", default="auto", choices=["auto", "on", "off"],
+                   help="N > 1: split each rank's block into own | halo parts to hide the "
+                        "exchange (auto: when the halo records reach 64 MB)")
     p.add_argument("--no-vendor", action="store_true",
                    help="skip the rocSPARSE (torch.sparse.mm) forward baseline")
     p.add_argument("--cbsr-order", default="column", choices=["column", "lane", "value"],
@@ -719,7 +722,9 @@ def main():
 
     if partitioned:
         from spgemm_new_amd.distributed import PartitionedMaxK
-        model = PartitionedMaxK(indptr, indices, values, rank, world, dev, local_block=True, **kw)
+        ov = {"auto": "auto", "on": True, "off": False}[args.overlap]
+        model = PartitionedMaxK(indptr, indices, values, rank, world, dev, local_block=True,
+                                overlap=ov, **kw)
         data_l, sel_l = model.local_rows(data), model.local_rows(sel)
         G_l = model.local_rows(G)
 

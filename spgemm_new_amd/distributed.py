@@ -70,6 +70,12 @@ def ag(out: torch.Tensor, inp: torch.Tensor, async_op: bool = False):
     return out
 
 
+# overlap="auto": split a rank's block into own | halo parts (the forward's
+# exchange hidden behind the own part) only when the halo records, sized at the
+# benchmark's k = 32 (160 B per node), reach this many bytes
+OVERLAP_MIN_HALO_BYTES = 64 << 20
+OVERLAP_BYTES_PER_HALO_NODE = 160
+
 # all-gather the CBSR instead of the all-to-all-v of halo records when some
 # rank's halo covers more than this fraction of V ("when the halo
 # is close to the full vertex set"; then both move about (N-1)/N of the table)
@@ -162,7 +168,7 @@ class PartitionedMaxK:
     """
 
     def __init__(self, indptr, indices, values, rank: int, world: int, device,
-                 engine=None, row_cost: int = 16, overlap: bool = True, records: bool = True,
+                 engine=None, row_cost: int = 16, overlap: bool | str = True, records: bool = True,
                  local_block: bool = False, overlap_backward: bool | None = None,
                  bwd_algo: int | None = None, halo_mode: str = "auto", **engine_kw):
         """indptr: the GLOBAL row pointer (V + 1 entries, cheap); indices /
@@ -220,6 +226,15 @@ class PartitionedMaxK:
         # adds each row's own-column edges before its halo-column edges, a
         # different fp32 order than the single block's edge order.
         self.bwd_algo = bwd_algo
+        if overlap == "auto":
+            # split only when the exchange is worth hiding: the split costs 0.15-0.4 ms
+            # of compute per step on Reddit blocks (two engines, their own launches
+            # and partials: N=2/4/8 step 3.10/1.84/1.04 ms split vs 2.72/1.57/0.89
+            # single, tools/exp_rank_step.py) against 19-33 MB of halo records, a
+            # few tenths of that over 7 xGMI links; products' 200-340 MB are not
+            overlap = p.num_halo * OVERLAP_BYTES_PER_HALO_NODE >= OVERLAP_MIN_HALO_BYTES
+        elif not isinstance(overlap, bool):
+            raise RuntimeError("overlap must be True, False or 'auto'")
         self.overlap = overlap and p.num_halo > 0
         if self.overlap:
             li = p.local_indices.long()

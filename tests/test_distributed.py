@@ -506,6 +506,16 @@ def _allgather_worker(rank, world, port, q, k):
         m_rec = PartitionedMaxK(*args, engine=OracleEngine, halo_mode="records")
         m_ag = PartitionedMaxK(*args, engine=OracleEngine, halo_mode="allgather")
         m_auto = PartitionedMaxK(*args, engine=OracleEngine)
+        # overlap="auto": a few KB of halo records -> single block; threshold 0 -> split
+        import spgemm_new_amd.distributed as Dm
+        m_ov_auto = PartitionedMaxK(*args, engine=OracleEngine, overlap="auto")
+        saved = Dm.OVERLAP_MIN_HALO_BYTES
+        Dm.OVERLAP_MIN_HALO_BYTES = 0
+        try:
+            m_ov_zero = PartitionedMaxK(*args, engine=OracleEngine, overlap="auto")
+        finally:
+            Dm.OVERLAP_MIN_HALO_BYTES = saved
+        assert m_ov_auto.overlap is False and m_ov_zero.overlap is True
         d_l, s_l = m_rec.local_rows(torch.from_numpy(data)), m_rec.local_rows(torch.from_numpy(sel))
         g_l = m_rec.local_rows(torch.from_numpy(grad))
         y_r, y_a = m_rec.forward(d_l, s_l, h), m_ag.forward(d_l, s_l, h)

@@ -100,6 +100,7 @@ def main():
     ap.add_argument("--worlds", default="1,2,4,8")
     ap.add_argument("--rows", action="store_true", help="unpacked-rows halo path (no records)")
     ap.add_argument("--halo-mode", default="records", choices=["records", "allgather"])
+    ap.add_argument("--no-overlap", action="store_true", help="single block: no own / halo split")
     a = ap.parse_args()
     dev = torch.device("cuda:0")
     V, E = CONFIGS[a.graph]
@@ -118,7 +119,8 @@ def main():
             D.a2a = lb
             D.ag = GatherLoopback(bounds, data, sel)
             m = D.PartitionedMaxK(indptr, indices, values, p, world, dev, records=not a.rows,
-                                  halo_mode=a.halo_mode if world > 1 else "records")
+                                  halo_mode=a.halo_mode if world > 1 else "records",
+                                  overlap=not a.no_overlap)
             d_l, s_l, g_l = m.local_rows(data), m.local_rows(sel), m.local_rows(G)
             tf = timed(lambda: m.forward(d_l, s_l, h))
             tb = timed(lambda: m.backward(g_l, s_l))
@@ -143,6 +145,11 @@ def main():
                   f"bwd {tb:.3f} step {ts:.3f} ms (no wire time) | halo fwd "
                   f"{pl.num_halo * 5 * k / 1e6:.1f} MB in, {m.send_rows.numel() * 5 * k / 1e6:.1f}"
                   f" MB out; bwd algo {m.local.last_bwd_algo}; halo mode {m.halo_mode}", flush=True)
+            for nm in ("local_own", "local_halo"):
+                e = getattr(m, nm, None)
+                if e is not None:
+                    print(f"   {nm}: bwd {getattr(e, 'last_bwd_algo', None)}, fwd blocks "
+                          f"{getattr(e, '_fwd_blocks', {})}", flush=True)
             del m, lb, d_l, s_l, g_l
             torch.cuda.empty_cache()
 
