@@ -52,6 +52,9 @@ def parse():
     p.add_argument("--partitioned", action="store_true",
                    help="use the multi-GPU (row partition + halo exchange) path even at N=1")
     p.add_argument("--verbose", action="store_true")
+    p.add_argument("--auto", default="fixed", choices=["fixed", "measure"],
+                   help="AUTO algorithm choice: a rule of the shape that reproduces the measured "
+                        "picks on the BASELINE shapes (bitwise repeatable), or timed per graph")
     p.add_argument("--overlap", default="auto", choices=["auto", "on", "off"],
                    help="N > 1: split each rank's block into own | halo parts to hide the "
                         "exchange (auto: when the halo records reach 64 MB)")
@@ -449,7 +452,8 @@ def config_sweep(args, dev, only=None):
     steps, warmup = max(args.steps, 20), max(args.warmup, 5)
     h = 256
     out = {"protocol": f"{warmup} warm-up + {steps} timed steps, HIP events per call, "
-                       "AUTO algorithms, same synthetic generator as the headline (seed 123)"}
+                       f"AUTO algorithms (MAXK_AUTO={os.environ.get('MAXK_AUTO')}), same "
+                       "synthetic generator as the headline (seed 123)"}
     want = set(only) if only else set(SWEEP_ENTRIES)
     t_all = time.time()
     ks = [k for k in (8, 16, 32, 64) if f"products_k{k}" in want]
@@ -648,6 +652,9 @@ def bench_multi(args, S, indptr, indices, data, sel, V, E, h, k, dev, world, ran
 
 def main():
     args = parse()
+    # the algorithm choices (forward column blocks, backward algorithm): by rule of the
+    # shape (default; the same choices, summation order and bits on every box) or timed
+    os.environ.setdefault("MAXK_AUTO", args.auto)
     import spgemm_new_amd as S
     from spgemm_new_amd import _lib
     from spgemm_new_amd.graphs import (CONFIGS, synthetic_columns, synthetic_indptr,
@@ -780,7 +787,7 @@ def main():
         "config": {"workload": f"{args.graph} fwd SpGEMM + bwd SSpMM", "graph": args.graph,
                    "num_nodes": V, "num_edges": E, "hidden": h, "k": k,
                    "parallelism": f"rowpart{world}" if partitioned else "single",
-                   "bwd_algo": args.bwd_algo},
+                   "bwd_algo": args.bwd_algo, "auto_mode": os.environ.get("MAXK_AUTO")},
     }
 
     if partitioned:

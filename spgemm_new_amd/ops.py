@@ -562,13 +562,23 @@ class MaxKGraph:
         return buf
 
     def _fixed_choice(self, k: int, h: int, own: bool) -> int:
-        """MAXK_AUTO=fixed: TILE when its plan serves the shape and the graph's own
-        values; else LOCAL when the gradient fits a few source bands; else STAGED
-        (what measurement picks on the BASELINE shapes, minus the ties)."""
-        if own and TILE_AUTO and tile_shape_ok(k, h) and self.tile_plan(k) is not None:
+        """MAXK_AUTO=fixed: a rule of the shape that reproduces what measurement
+        picks on the BASELINE shapes, so the algorithm -- and every
+        bit of the result -- repeats on every box: TILE on long-row graphs (mean
+        degree >= 128: Reddit, proteins) and at k = 64; else LOCAL when the gradient
+        fits a few source bands (small graphs); else, on large short-row graphs
+        (products), EDGE_GATHER at k = 8, STAGED_EDGE at k = 32 (both with the
+        forward writing the edge selectors) and STAGED otherwise."""
+        long_rows = self.num_edges >= FWD_BLOCKED_MIN_DEGREE * max(self.num_rows, 1)
+        if (own and TILE_AUTO and tile_shape_ok(k, h) and (long_rows or k == 64)
+                and self.tile_plan(k) is not None):
             return _lib.MAXK_BWD_TILE
         if self.num_rows * h * 4 <= 8 * LOCAL_BAND_BYTES and self.local_plan(k) is not None:
             return _lib.MAXK_BWD_LOCAL
+        if ESEL_AUTO and h <= 256 and k == 8:
+            return _lib.MAXK_BWD_EDGE_GATHER
+        if ESEL_AUTO and h <= 256 and k == 32:
+            return _lib.MAXK_BWD_STAGED_EDGE
         return _lib.MAXK_BWD_STAGED
 
     def autotune_backward(self, grad, sel, out, values=None) -> int:
@@ -594,6 +604,11 @@ class MaxKGraph:
         if AUTO_MODE == "fixed":
             choice = self._fixed_choice(k, grad.shape[1], own)
             self._bwd_choice[key] = choice
+            if choice in _ESEL_ALGOS:
+                # the forwards of this shape write the edge selectors from now on; this
+                # call (no such forward yet) takes STAGED
+                self._esel_on.add((k, grad.shape[1]))
+                self._bwd_alt[key] = _lib.MAXK_BWD_STAGED
             return choice
         if torch.cuda.is_current_stream_capturing():
             # nothing can be timed (or planned) while a graph is captured: the
@@ -953,9 +968,16 @@ def _fwd_blocks(g: MaxKGraph, data, sel, dim_origin: int, out, values) -> int:
     nb = g._fwd_blocks.get(key)
     if nb is not None:
         return nb
-    if g.num_edges < FWD_BLOCKED_MIN_DEGREE * g.num_rows or AUTO_MODE == "fixed":
+    if g.num_edges < FWD_BLOCKED_MIN_DEGREE * g.num_rows:
         g._fwd_blocks[key] = 0
         return 0
+    if AUTO_MODE == "fixed":
+        # the measured best on Reddit at k = 32 and 64, when its partial
+        # outputs fit comfortably
+        free, _ = torch.cuda.mem_get_info(g.device)
+        nb = 4 if 4 * 4 * g.num_rows * dim_origin + 16 * g.num_edges <= free // 4 else 0
+        g._fwd_blocks[key] = nb
+        return nb
     if torch.cuda.is_current_stream_capturing():
         return 0
     L = _lib.load()
