@@ -92,3 +92,61 @@ def test_compiled_module_errors(dev):
         m.spmm_maxk_forward(w4, ix, vv, d, s.int(), 1, 8)
     with pytest.raises(RuntimeError, match="Invalid k value"):
         m.cuda_topk_maxk_float(d, 9)
+
+
+# ------------------------------------------------ the compiled `spmm_kernels` module
+# kernels/spmm_bindings.cpp:209-262
+SPMM_CLASS_METHODS = ["update_input_output", "set_sparse_params", "run_kernel", "get_graph_name"]
+
+
+def _spmm_module():
+    if LIBDIR not in sys.path:
+        sys.path.insert(0, LIBDIR)
+    import spmm_kernels
+    assert os.path.dirname(os.path.abspath(spmm_kernels.__file__)) == LIBDIR
+    return spmm_kernels
+
+
+def test_compiled_spmm_kernels_exports_reference_surface():
+    m = _spmm_module()
+    for cls in ("SpmmMaxK", "SpmmMaxKBackward"):
+        for meth in SPMM_CLASS_METHODS:
+            assert hasattr(getattr(m, cls), meth), (cls, meth)
+    assert callable(m.prepare_cbsr_format) and callable(m.topk_nonlinearity)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("k", [8, 32])
+def test_compiled_spmm_kernels_matches_oracle(dev, oracle, k):
+    from spgemm_new_amd.graphs import random_cbsr, small_csr
+    m = _spmm_module()
+    indptr, indices = small_csr(2000, seed=9)
+    v, h = len(indptr) - 1, 256
+    values = np.random.default_rng(1).random(len(indices), dtype=np.float32)
+    data, sel = random_cbsr(v, k, h, seed=5)
+    grad = np.random.default_rng(2).random((v, h), dtype=np.float32)
+    T = lambda a: torch.from_numpy(np.ascontiguousarray(a)).to(dev)  # noqa: E731
+    ip, ix, vv, d, g = (T(a) for a in (indptr, indices, values, data, grad))
+    s32 = T(sel.astype(np.int32))             # the reference passes int32 selectors
+    y = torch.full((v, h), float("nan"), device=dev)
+    fwd = m.SpmmMaxK("g", ip, ix, vv, d, y)
+    fwd.set_sparse_params(s32, k)
+    assert fwd.run_kernel(False, h) == 0.0 and fwd.get_graph_name() == "g"
+    assert oracle.parity_error(y.cpu().numpy(),
+                               oracle.np_forward(indptr, indices, values, data, sel, h)) <= 1e-4
+    assert fwd.run_kernel(True) > 0.0           # spmm_base.h's 4 + 4 protocol, seconds
+    dx = torch.full((v, k), float("nan"), device=dev)
+    bwd = m.SpmmMaxKBackward("g", ip, ix, vv, g, dx)
+    bwd.set_sparse_params(s32, k)
+    bwd.run_kernel()
+    assert oracle.parity_error(dx.cpu().numpy(),
+                               oracle.np_backward(indptr, indices, values, grad, sel)) <= 1e-4
+    x = torch.rand((v, h), device=dev)
+    vals, idx = m.prepare_cbsr_format(x, k)
+    ref_v, ref_i = torch.topk(x, k, dim=1)
+    assert idx.dtype == torch.int32 and torch.equal(vals, ref_v)
+    assert torch.equal(torch.sort(idx, 1)[0], torch.sort(ref_i.int(), 1)[0])
+    dense = m.topk_nonlinearity(x, k)
+    assert torch.equal(dense, torch.zeros_like(x).scatter_(1, ref_i, ref_v))
+    with pytest.raises(RuntimeError):
+        m.SpmmMaxK("g", ip, ix, vv, d, y).run_kernel()   # no set_sparse_params yet
