@@ -747,8 +747,13 @@ def main():
         dx = torch.empty((V, k), device=dev)
         g.backward(G, sel, out=dx, algo=algo)  # builds CSC/workspaces once
 
-        def fwd_call():   # a training forward: its backward follows with this sel
-            g.forward(data, sel, h, out=y, edge_sel="auto")
+        from spgemm_new_amd.ops import _ESEL_ALGOS
+        # a training forward: its backward follows with this sel (an explicitly chosen
+        # edge-selector backward makes every forward write the edge selectors)
+        esel_mode = True if algo in _ESEL_ALGOS else "auto"
+
+        def fwd_call():
+            g.forward(data, sel, h, out=y, edge_sel=esel_mode)
 
         def bwd_call():
             g.backward(G, sel, out=dx, algo=algo)

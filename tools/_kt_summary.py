@@ -21,7 +21,7 @@ for path in glob.glob(root + "/**/*counter_collection.csv", recursive=True):
         vals = {c: sum(v) / len(v) for c, v in cs.items()}
         n = max(len(v) for v in cs.values())
         if any(x > 1e5 for x in vals.values()):
-            print(f"PMC {n:4d} " + " ".join(f"{c}={x / 1e9:.3f}G" for c, x in vals.items()) + f"  {k}")
+            print(f"PMC {n:4d} " + " ".join(f"{c}={x:.6g}" for c, x in vals.items()) + f"  {k}")
 # KT_SERIES=<substring>: the last 24 durations of every kernel whose name holds it
 import os  # noqa: E402
 pat = os.environ.get("KT_SERIES")
