@@ -2523,170 +2523,6 @@ __device__ __forceinline__ void tile_groups2_r16(const tile_g16_t &pa, const til
         : "memory", "scc");
 }
 
-// TILE_LOOP2: the groups after the first two as a rolling pipeline -- group
-// i+1's selector bytes and LDS reads are issued before group i's FMAs, so the
-// LDS latency of one group hides behind the other's FMAs; the next group's
-// s_load goes into the bank the FMAs just freed
-__device__ __forceinline__ void tile_group_loop2_r16(const uint32_t *rb, uint32_t ro, uint32_t &n,
-                                                     uint32_t &m, uint64_t lo, uint64_t hi,
-                                                     tile_sel_t &selv, tile_acc_t &acc0,
-                                                     tile_acc_t &acc1)
-{
-    uint32_t t0, t1, t2, t3, t4, t5, t6, t7;
-    uint64_t ex;
-    asm volatile(
-        "s_cmp_eq_u32 %[n], 0\n\t"
-        "s_cbranch_scc1 .Lq_done%=\n\t"
-        "s_mov_b64 %[ex], exec\n\t"
-        "s_load_dwordx16 s[64:79], %[rb], %[ro]\n\t"
-        "s_add_u32 %[ro], %[ro], 64\n\t"
-        "s_waitcnt lgkmcnt(0)\n\t"
-        "s_cmp_lt_i32 %[m], 0\n\t"
-        "s_cselect_b64 exec, %[lo], %[hi]\n\t"
-        "s_set_gpr_idx_on s64, gpr_idx(SRC0)\n\t"
-        "v_perm_b32 %[t0], v48, 0, s64\n\t"
-        "s_set_gpr_idx_idx s68\n\t"
-        "v_perm_b32 %[t1], v48, 0, s68\n\t"
-        "s_set_gpr_idx_idx s72\n\t"
-        "v_perm_b32 %[t2], v48, 0, s72\n\t"
-        "s_set_gpr_idx_idx s76\n\t"
-        "v_perm_b32 %[t3], v48, 0, s76\n\t"
-        "s_set_gpr_idx_off\n\t"
-        "v_lshrrev_b32 %[t0], 14, %[t0]\n\t"
-        "v_lshrrev_b32 %[t1], 14, %[t1]\n\t"
-        "v_lshrrev_b32 %[t2], 14, %[t2]\n\t"
-        "v_lshrrev_b32 %[t3], 14, %[t3]\n\t"
-        "v_add_u32 %[t0], s66, %[t0]\n\t"
-        "v_add_u32 %[t1], s70, %[t1]\n\t"
-        "v_add_u32 %[t2], s74, %[t2]\n\t"
-        "v_add_u32 %[t3], s78, %[t3]\n\t"
-        "ds_read_b32 %[t0], %[t0]\n\t"
-        "ds_read_b32 %[t1], %[t1]\n\t"
-        "ds_read_b32 %[t2], %[t2]\n\t"
-        "ds_read_b32 %[t3], %[t3]\n\t"
-        ".Lq_a%=:\n\t"
-        "s_add_u32 %[n], %[n], 1\n\t"
-        "s_cbranch_scc1 .Lq_tail_a%=\n\t"
-        "s_load_dwordx16 s[80:95], %[rb], %[ro]\n\t"
-        "s_add_u32 %[ro], %[ro], 64\n\t"
-        "s_waitcnt lgkmcnt(0)\n\t"
-        "s_cmp_lt_i32 %[m], -1\n\t"
-        "s_cselect_b64 exec, %[lo], %[hi]\n\t"
-        "s_set_gpr_idx_on s80, gpr_idx(SRC0)\n\t"
-        "v_perm_b32 %[t4], v48, 0, s80\n\t"
-        "s_set_gpr_idx_idx s84\n\t"
-        "v_perm_b32 %[t5], v48, 0, s84\n\t"
-        "s_set_gpr_idx_idx s88\n\t"
-        "v_perm_b32 %[t6], v48, 0, s88\n\t"
-        "s_set_gpr_idx_idx s92\n\t"
-        "v_perm_b32 %[t7], v48, 0, s92\n\t"
-        "s_set_gpr_idx_off\n\t"
-        "v_lshrrev_b32 %[t4], 14, %[t4]\n\t"
-        "v_lshrrev_b32 %[t5], 14, %[t5]\n\t"
-        "v_lshrrev_b32 %[t6], 14, %[t6]\n\t"
-        "v_lshrrev_b32 %[t7], 14, %[t7]\n\t"
-        "v_add_u32 %[t4], s82, %[t4]\n\t"
-        "v_add_u32 %[t5], s86, %[t5]\n\t"
-        "v_add_u32 %[t6], s90, %[t6]\n\t"
-        "v_add_u32 %[t7], s94, %[t7]\n\t"
-        "ds_read_b32 %[t4], %[t4]\n\t"
-        "ds_read_b32 %[t5], %[t5]\n\t"
-        "ds_read_b32 %[t6], %[t6]\n\t"
-        "ds_read_b32 %[t7], %[t7]\n\t"
-        "s_cmp_lt_i32 %[m], 0\n\t"
-        "s_cselect_b64 exec, %[lo], %[hi]\n\t"
-        "s_set_gpr_idx_on s65, gpr_idx(SRC2,DST)\n\t"
-        "v_fma_f32 v64, %[t0], s67, v64\n\t"
-        "s_set_gpr_idx_idx s69\n\t"
-        "v_fma_f32 v64, %[t1], s71, v64\n\t"
-        "s_set_gpr_idx_idx s73\n\t"
-        "v_fma_f32 v64, %[t2], s75, v64\n\t"
-        "s_set_gpr_idx_idx s77\n\t"
-        "v_fma_f32 v64, %[t3], s79, v64\n\t"
-        "s_set_gpr_idx_off\n\t"
-        "s_add_u32 %[m], %[m], 1\n\t"
-        "s_add_u32 %[n], %[n], 1\n\t"
-        "s_cbranch_scc1 .Lq_tail_b%=\n\t"
-        "s_load_dwordx16 s[64:79], %[rb], %[ro]\n\t"
-        "s_add_u32 %[ro], %[ro], 64\n\t"
-        "s_waitcnt lgkmcnt(0)\n\t"
-        "s_cmp_lt_i32 %[m], -1\n\t"
-        "s_cselect_b64 exec, %[lo], %[hi]\n\t"
-        "s_set_gpr_idx_on s64, gpr_idx(SRC0)\n\t"
-        "v_perm_b32 %[t0], v48, 0, s64\n\t"
-        "s_set_gpr_idx_idx s68\n\t"
-        "v_perm_b32 %[t1], v48, 0, s68\n\t"
-        "s_set_gpr_idx_idx s72\n\t"
-        "v_perm_b32 %[t2], v48, 0, s72\n\t"
-        "s_set_gpr_idx_idx s76\n\t"
-        "v_perm_b32 %[t3], v48, 0, s76\n\t"
-        "s_set_gpr_idx_off\n\t"
-        "v_lshrrev_b32 %[t0], 14, %[t0]\n\t"
-        "v_lshrrev_b32 %[t1], 14, %[t1]\n\t"
-        "v_lshrrev_b32 %[t2], 14, %[t2]\n\t"
-        "v_lshrrev_b32 %[t3], 14, %[t3]\n\t"
-        "v_add_u32 %[t0], s66, %[t0]\n\t"
-        "v_add_u32 %[t1], s70, %[t1]\n\t"
-        "v_add_u32 %[t2], s74, %[t2]\n\t"
-        "v_add_u32 %[t3], s78, %[t3]\n\t"
-        "ds_read_b32 %[t0], %[t0]\n\t"
-        "ds_read_b32 %[t1], %[t1]\n\t"
-        "ds_read_b32 %[t2], %[t2]\n\t"
-        "ds_read_b32 %[t3], %[t3]\n\t"
-        "s_cmp_lt_i32 %[m], 0\n\t"
-        "s_cselect_b64 exec, %[lo], %[hi]\n\t"
-        "s_set_gpr_idx_on s81, gpr_idx(SRC2,DST)\n\t"
-        "v_fma_f32 v64, %[t4], s83, v64\n\t"
-        "s_set_gpr_idx_idx s85\n\t"
-        "v_fma_f32 v64, %[t5], s87, v64\n\t"
-        "s_set_gpr_idx_idx s89\n\t"
-        "v_fma_f32 v64, %[t6], s91, v64\n\t"
-        "s_set_gpr_idx_idx s93\n\t"
-        "v_fma_f32 v64, %[t7], s95, v64\n\t"
-        "s_set_gpr_idx_off\n\t"
-        "s_add_u32 %[m], %[m], 1\n\t"
-        "s_branch .Lq_a%=\n\t"
-        ".Lq_tail_a%=:\n\t"
-        "s_waitcnt lgkmcnt(0)\n\t"
-        "s_cmp_lt_i32 %[m], 0\n\t"
-        "s_cselect_b64 exec, %[lo], %[hi]\n\t"
-        "s_set_gpr_idx_on s65, gpr_idx(SRC2,DST)\n\t"
-        "v_fma_f32 v64, %[t0], s67, v64\n\t"
-        "s_set_gpr_idx_idx s69\n\t"
-        "v_fma_f32 v64, %[t1], s71, v64\n\t"
-        "s_set_gpr_idx_idx s73\n\t"
-        "v_fma_f32 v64, %[t2], s75, v64\n\t"
-        "s_set_gpr_idx_idx s77\n\t"
-        "v_fma_f32 v64, %[t3], s79, v64\n\t"
-        "s_set_gpr_idx_off\n\t"
-        "s_add_u32 %[m], %[m], 1\n\t"
-        "s_branch .Lq_end%=\n\t"
-        ".Lq_tail_b%=:\n\t"
-        "s_waitcnt lgkmcnt(0)\n\t"
-        "s_cmp_lt_i32 %[m], 0\n\t"
-        "s_cselect_b64 exec, %[lo], %[hi]\n\t"
-        "s_set_gpr_idx_on s81, gpr_idx(SRC2,DST)\n\t"
-        "v_fma_f32 v64, %[t4], s83, v64\n\t"
-        "s_set_gpr_idx_idx s85\n\t"
-        "v_fma_f32 v64, %[t5], s87, v64\n\t"
-        "s_set_gpr_idx_idx s89\n\t"
-        "v_fma_f32 v64, %[t6], s91, v64\n\t"
-        "s_set_gpr_idx_idx s93\n\t"
-        "v_fma_f32 v64, %[t7], s95, v64\n\t"
-        "s_set_gpr_idx_off\n\t"
-        "s_add_u32 %[m], %[m], 1\n\t"
-        ".Lq_end%=:\n\t"
-        "s_mov_b64 exec, %[ex]\n\t"
-        ".Lq_done%=:\n\t"
-        : [t0] "=&v"(t0), [t1] "=&v"(t1), [t2] "=&v"(t2), [t3] "=&v"(t3), [t4] "=&v"(t4),
-          [t5] "=&v"(t5), [t6] "=&v"(t6), [t7] "=&v"(t7), [ex] "=&s"(ex), [ro] "+s"(ro),
-          [n] "+s"(n), [m] "+s"(m), "+{v[48:63]}"(selv), "+{v[64:95]}"(acc0), "+{v[96:127]}"(acc1)
-        : [rb] "s"(rb), [lo] "s"(lo), [hi] "s"(hi)
-        : "memory", "scc", "s64", "s65", "s66", "s67", "s68", "s69", "s70", "s71", "s72", "s73",
-          "s74", "s75", "s76", "s77", "s78", "s79", "s80", "s81", "s82", "s83", "s84", "s85",
-          "s86", "s87", "s88", "s89", "s90", "s91", "s92", "s93", "s94", "s95");
-}
-
 // the groups after the two loaded before the barrier (four-word records): s_load
 // into s[64:79] / s[80:95] alternately, the next group in flight
 __device__ __forceinline__ void tile_group_loop_r16(const uint32_t *rb, uint32_t ro, uint32_t &n,
@@ -2964,9 +2800,6 @@ __global__ __launch_bounds__(kTileWaves * kWave) void bwd_tile_kernel(
 #ifndef TILE_PF_AHEAD
 #define TILE_PF_AHEAD 128  // dwords: the window starts 512 B past the chunk's records
 #endif
-#ifndef TILE_LOOP2
-#define TILE_LOOP2 0  // rolling-pipeline loop for the groups after the first two
-#endif
 #ifndef TILE_KPF
 // record groups 3 and 4 pulled into the scalar cache with the first two (0 or 2; 4
 // measured no better): Reddit k=32 2.81 -> 2.78 ms
@@ -3072,11 +2905,7 @@ __global__ __launch_bounds__(kTileWaves * kWave) void bwd_tile_kernel(
             asm volatile("s_waitcnt lgkmcnt(0)" : "+{s[64:79]}"(pa), "+{s[80:95]}"(pb)::"memory");
 #endif
             tile_groups2_r16(pa, pb, n, m, lo, hi, selv, acc0, acc1);
-#if TILE_LOOP2
-            tile_group_loop2_r16(rb, ro + 128, n, m, lo, hi, selv, acc0, acc1);
-#else
             tile_group_loop_r16(rb, ro + 128, n, m, lo, hi, selv, acc0, acc1);
-#endif
             ro += 64 * gn;
             return;
         }
