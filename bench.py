@@ -800,7 +800,8 @@ def main():
         result["config"]["halo_nodes_rank0"] = p.num_halo
         result["config"]["own_nodes_rank0"] = p.num_own
         result["config"]["overlap"] = model.overlap
-        result["config"]["halo_mode"] = model.halo_mode
+        # the all-gather table path exists only with the own | halo split
+        result["config"]["halo_mode"] = model.halo_mode if model.overlap else "records"
         result["config"]["halo_bytes_rank0"] = model.halo_bytes(k)
         # per-call timing on each rank (HIP events on the launch stream; the
         # calls include their halo all-to-all-v), max over ranks
