@@ -338,6 +338,29 @@ int maxk_sspmm_backward_local_rel8(const int32_t *seg_edge_off, int num_segments
                                    int num_rows, int dim_origin, int dim_k, float *dxs,
                                    void *stream);
 
+/* Multi-relation STAGED backward (the backward of maxk_spgemm_forward_multi;
+ * config 5, ogbn-proteins R = 8): dxs[c,l] = sum_q sum_e val[e,q] *
+ * grad[q, row(e), sel[c,l]] with values fp32[E, num_rel] and grad
+ * fp32[num_rel, num_rows, dim_origin] as the forward's (both 16-B aligned).
+ * The relations are summed per edge inside phase 1, which writes one staging
+ * row per edge; phase 2 is the single-relation segmented sum.  algo
+ * MAXK_BWD_STAGED (or AUTO): rows in CSC order, csc_pos = maxk_csc_build's;
+ * MAXK_BWD_EDGE_GATHER: rows in edge order, csc_pos = the CSC slot -> edge
+ * permutation (maxk_csc_perm_build).  Selectors are always the node CBSR
+ * selectors here.  num_rel in {4, 8, 16}; dim_k in {8, 16, 32, 64};
+ * dim_origin % 4 == 0.  Workspace: maxk_backward_workspace_bytes(algo, ...).
+ * No counterpart in the reference (its proteins model makes one SSpMM call
+ * per relation); equals the sum of num_rel maxk_sspmm_backward calls up to
+ * fp32 summation order.  Writes every element of dxs. */
+int maxk_sspmm_backward_multi(int algo, const int32_t *sched, int64_t num_panels,
+                              const int32_t *indptr, const int32_t *indices, const float *values,
+                              int num_rel, const float *grad, const uint8_t *cbsr_sel,
+                              int num_rows, int num_cols, int64_t num_edges, int dim_origin,
+                              int dim_k, float *dxs, const int32_t *csc_pos,
+                              const int32_t *csc_sched, int64_t csc_num_panels,
+                              const int32_t *csc_indptr, void *workspace, size_t workspace_bytes,
+                              void *stream);
+
 /* ---------------------------------------------------------------------------
  * Backward SSpMM, TILE algorithm (dim_k = 32 or 64, dim_origin = 256): every
  * gradient row is read once per CU into an LDS ring instead of being

@@ -32,6 +32,10 @@ MAXK_BWD_STAGED_EDGE = 5
 MAXK_BWD_EDGE_GATHER = 6
 MAXK_BWD_BINNED = 7
 MAXK_BWD_BINNED_EDGE = 8
+# backward_multi only (Python level; the C entry is maxk_sspmm_backward_multi with
+# MAXK_BWD_STAGED / MAXK_BWD_EDGE_GATHER): relations summed per edge in phase 1
+MAXK_BWD_MULTI_STAGED = 16
+MAXK_BWD_MULTI_EDGE_GATHER = 17
 MAXK_BIN_DESTS = 255
 MAXK_BIN_WINDOW = 64
 MAXK_TOPK_ORDER_COLUMN = 0
@@ -66,6 +70,8 @@ SIGNATURES = {
     "maxk_grad_interleave": (_I, [_P, _I, _I, _I, _P, _P]),
     "maxk_sspmm_backward_local_rel8": (_I, [_P, _I, _P, _I, _I, _P, _P, _P, _P, _I, _I, _I, _P,
                                             _P]),
+    "maxk_sspmm_backward_multi": (_I, [_I, _P, _L, _P, _P, _P, _I, _P, _P, _I, _I, _L, _I, _I, _P,
+                                       _P, _P, _L, _P, _P, _S, _P]),
     "maxk_sspmm_backward_tile": (_I, [_P, _P, _P, _P, _P, _I, _I, _I, _P, _P, _P, _I, _I, _I, _I,
                                       _P, _P, _P]),
     "maxk_tile_format": (_I, [ctypes.POINTER(_I), ctypes.POINTER(_I)]),

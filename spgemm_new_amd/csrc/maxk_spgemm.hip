@@ -1312,6 +1312,165 @@ __global__ __launch_bounds__(kBlock) void bwd_panel_kernel(
     }
 }
 
+// ---------------------------------------------------------------------------
+// Multi-relation STAGED backward (config 5, ogbn-proteins R = 8; the backward
+// of maxk_spgemm_forward_multi):
+//   dXs[c,l] = sum_q sum_{e: idx[e]=c} val[e,q] * G_q[row(e), sel[c,l]].
+// dXs has no relation axis, so the relation sum is taken per EDGE, in
+// registers, before anything leaves the CU: phase 1 stages the R gradient rows
+// of a source row in LDS relation-innermost and writes one product row per
+// edge, P[e, l] = sum_q val[e,q] * G_q[r, sel[c,l]] -- the staging row of the
+// single-relation STAGED (PM = kPmCsc) or EDGE_GATHER (kPmEdge) backward -- so
+// phase 2 is that backward's segmented sum.  Per edge: R*4 B of values, 4 B
+// index, a k-byte selector piece (the V*k table is cache-resident on
+// proteins) and one staging row out and back; the R gradient rows of a source
+// row are read once per panel.  (The composed backward makes R such passes;
+// LOCAL rel8 gathers 32 B of interleaved gradient per selected entry.)
+//
+// LDS: per wave one 256-column row of R floats per column = R/4 16-B slots
+// per column.  A 256-B bank row holds 64/R columns, so the ds_read_b128 of
+// slot s at random columns would use only 16/(R/4) slot positions of the
+// bank row; slot s of column j is stored at s ^ ((j / (64/R)) % (R/4)), so
+// over j the reads of one logical slot cover all 16 positions.
+// ---------------------------------------------------------------------------
+template <int R>
+struct RelLds {
+    static constexpr int NS = R / 4;    // 16-B slots per column
+    static constexpr int CPB = 64 / R;  // columns per 256-B bank row
+    static __device__ __forceinline__ uint32_t off(uint32_t j, int s)
+    {
+        return j * (R * 4) + (((uint32_t)s ^ ((j / CPB) % NS)) << 4);
+    }
+};
+
+// G_q[r, 0:dim] for q < R into the wave's LDS row (columns >= dim read as 0,
+// the rule of stage_row).  dim % 4 == 0.
+template <int R>
+__device__ __forceinline__ void stage_rel_rows(char *gs, const float *__restrict__ grad,
+                                               int64_t plane, int r, int dim)
+{
+    wave_sync_lds();
+    const int j0 = lane_id() * 4;  // 64 lanes x 4 columns
+    const float *g0 = grad + (size_t)r * dim + j0;
+#pragma unroll
+    for (int s = 0; s < R / 4; ++s) {
+        f4 g[4];
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+            g[i] = j0 < dim ? *reinterpret_cast<const f4 *>(g0 + (size_t)(4 * s + i) * plane)
+                            : f4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int c = 0; c < 4; ++c)
+            *reinterpret_cast<f4 *>(gs + RelLds<R>::off(j0 + c, s)) =
+                f4{g[0][c], g[1][c], g[2][c], g[3][c]};
+    }
+    wave_sync_lds();
+}
+
+// One source row's edge range [e0, e1): KP/4 lanes per edge, 4 selected
+// columns per lane (as bwd_edges_stage_vec), the edge's R values loaded once
+// by the lane that owns the edge and shuffled to the edge's lanes.
+template <int K, int R, int PM>
+__device__ __forceinline__ void bwd_multi_edges(int e0, int e1, const int32_t *__restrict__ idx,
+                                                const float *__restrict__ val,
+                                                const int32_t *__restrict__ csc_pos,
+                                                const uint8_t *__restrict__ sel, const char *gs,
+                                                float *__restrict__ P)
+{
+    constexpr bool CSRP = PM == kPmEdge;
+    constexpr int KP = PM == kPmCsc ? PRow<K>::KP : K;
+    constexpr int LPE = KP / 4;
+    constexpr int EPS = kWave / LPE;
+    constexpr int STEPS = kWave / EPS;
+    constexpr int U = STEPS < 8 ? STEPS : 8;
+    constexpr int NS = R / 4;
+    const int lane = lane_id();
+    const int sub = lane % LPE;
+    const int slot = lane / LPE;
+    for (int base = e0; base < e1; base += kWave) {
+        const int n = (e1 - base) < kWave ? (e1 - base) : kWave;
+        int my_c = 0, my_p = 0;
+        f4 my_v[NS];
+#pragma unroll
+        for (int s = 0; s < NS; ++s) my_v[s] = f4{0.f, 0.f, 0.f, 0.f};
+        if (lane < n) {
+            my_c = __builtin_nontemporal_load(idx + base + lane);
+            my_p = CSRP ? base + lane : __builtin_nontemporal_load(csc_pos + base + lane);
+            const f4 *vp = reinterpret_cast<const f4 *>(val + (size_t)(base + lane) * R);
+#pragma unroll
+            for (int s = 0; s < NS; ++s) my_v[s] = __builtin_nontemporal_load(vp + s);
+        }
+#pragma unroll
+        for (int s0 = 0; s0 < STEPS; s0 += U) {
+            if (s0 * EPS >= n) break;
+            uint32_t sb[U];
+#pragma unroll
+            for (int u = 0; u < U; ++u) {
+                const int t = (s0 + u) * EPS + slot;
+                const int c = __shfl(my_c, t);
+                sb[u] = t < n && sub * 4 < K
+                            ? *reinterpret_cast<const uint32_t *>(sel + (size_t)c * K + sub * 4)
+                            : 0u;
+            }
+#pragma unroll
+            for (int u = 0; u < U; ++u) {
+                const int t = (s0 + u) * EPS + slot;
+                const int p = __shfl(my_p, t);
+                f4 v[NS];
+#pragma unroll
+                for (int s = 0; s < NS; ++s)
+                    v[s] = f4{__shfl(my_v[s].x, t), __shfl(my_v[s].y, t), __shfl(my_v[s].z, t),
+                              __shfl(my_v[s].w, t)};
+                if (t < n) {
+                    f4 o = f4{0.f, 0.f, 0.f, 0.f};
+                    if (sub * 4 < K) {
+#pragma unroll
+                        for (int i = 0; i < 4; ++i) {
+                            const uint32_t j = (sb[u] >> (8 * i)) & 0xffu;
+                            float acc = 0.f;
+#pragma unroll
+                            for (int s = 0; s < NS; ++s) {
+                                const f4 g = *reinterpret_cast<const f4 *>(gs + RelLds<R>::off(j, s));
+                                acc = fmaf(v[s].x, g.x, acc);
+                                acc = fmaf(v[s].y, g.y, acc);
+                                acc = fmaf(v[s].z, g.z, acc);
+                                acc = fmaf(v[s].w, g.w, acc);
+                            }
+                            o[i] = acc;
+                        }
+                    }
+                    __builtin_nontemporal_store(
+                        o, reinterpret_cast<f4 *>(P + (size_t)p * KP + sub * 4));
+                }
+            }
+        }
+    }
+}
+
+template <int K, int R, int PM>
+__global__ __launch_bounds__(kBlock) void bwd_multi_stage_kernel(
+    const int2 *__restrict__ sched, int64_t num_panels, const int32_t *__restrict__ indptr,
+    const int32_t *__restrict__ idx, const float *__restrict__ val,
+    const float *__restrict__ grad, int64_t plane, const uint8_t *__restrict__ sel,
+    const int32_t *__restrict__ csc_pos, int num_rows, int dim, float *__restrict__ P)
+{
+    extern __shared__ __attribute__((aligned(16))) float lds[];
+    char *gs = reinterpret_cast<char *>(lds + (threadIdx.x / kWave) * (kMaxDim * R));
+    const int64_t w = (int64_t)blockIdx.x * kWavesPerBlock + threadIdx.x / kWave;
+    if (w >= num_panels) return;
+    const int2 a = sched[w], b = sched[w + 1];
+    const int i0 = a.x, j0 = a.y, i1 = b.x, j1 = b.y;
+    const int rlast = i1 < num_rows ? i1 : num_rows - 1;
+    for (int r = i0; r <= rlast; ++r) {
+        const int rb = indptr[r], re = indptr[r + 1];
+        const int eb = rb > j0 ? rb : j0;
+        const int ee = re < j1 ? re : j1;
+        if (eb >= ee) continue;
+        stage_rel_rows<R>(gs, grad, plane, r, dim);
+        bwd_multi_edges<K, R, PM>(eb, ee, idx, val, csc_pos, sel, gs, P);
+    }
+}
+
 // STAGED phase 2: dxs[c, :] = sum of P rows [csc_indptr[c], csc_indptr[c+1]),
 // merge-path panels over the CSC ranges, register accumulation + cross-slot
 // reduction; split destinations go through the carry fixup.
@@ -3409,6 +3568,48 @@ struct BwdSegsum {
     }
 };
 
+// Phase 1 of the multi-relation STAGED backward (R in {4, 8, 16}, k in {8, 16,
+// 32, 64}); phase 2 is BwdSegsum.
+template <int K>
+struct BwdMultiStage {
+    template <int R>
+    static int launch(bool edge_order, const int2 *sc, int64_t P, const int32_t *indptr,
+                      const int32_t *idx, const float *val, const float *grad, int64_t plane,
+                      const uint8_t *sel, const int32_t *csc_pos, int V, int dim, float *Pbuf,
+                      hipStream_t st)
+    {
+        const unsigned blocks = (unsigned)ceil_div(P, kWavesPerBlock);
+        const size_t lds = (size_t)kWavesPerBlock * kMaxDim * R * sizeof(float);
+        if (edge_order)
+            hipLaunchKernelGGL((bwd_multi_stage_kernel<K, R, kPmEdge>), dim3(blocks), dim3(kBlock),
+                               lds, st, sc, P, indptr, idx, val, grad, plane, sel, csc_pos, V, dim,
+                               Pbuf);
+        else
+            hipLaunchKernelGGL((bwd_multi_stage_kernel<K, R, kPmCsc>), dim3(blocks), dim3(kBlock),
+                               lds, st, sc, P, indptr, idx, val, grad, plane, sel, csc_pos, V, dim,
+                               Pbuf);
+        return launch_status();
+    }
+
+    static int run(int R, bool edge_order, const int32_t *sched, int64_t P, const int32_t *indptr,
+                   const int32_t *idx, const float *val, const float *grad, int64_t plane,
+                   const uint8_t *sel, const int32_t *csc_pos, int V, int dim, float *Pbuf,
+                   hipStream_t st)
+    {
+        if constexpr (K != 8 && K != 16 && K != 32 && K != 64) {
+            return MAXK_E_DIM;
+        } else {
+            const int2 *sc = reinterpret_cast<const int2 *>(sched);
+            switch (R) {
+            case 4: return launch<4>(edge_order, sc, P, indptr, idx, val, grad, plane, sel, csc_pos, V, dim, Pbuf, st);
+            case 8: return launch<8>(edge_order, sc, P, indptr, idx, val, grad, plane, sel, csc_pos, V, dim, Pbuf, st);
+            case 16: return launch<16>(edge_order, sc, P, indptr, idx, val, grad, plane, sel, csc_pos, V, dim, Pbuf, st);
+            default: return MAXK_E_ARG;
+            }
+        }
+    }
+};
+
 template <int K>
 struct BwdLocal {
     static int run(const int32_t *seg_off, int NS, const int32_t *dstart, int W, int dmax,
@@ -3855,6 +4056,51 @@ int maxk_sspmm_backward(int algo, const int32_t *sched, int64_t num_panels,
     int rc = dispatch_k<BwdPanel>(dim_k, true, sched, num_panels, indptr, indices, values, grad,
                                   cbsr_sel, csc_pos, num_rows, dim_origin, dim_k, dxs, Pbuf, st,
                                   esel, gather ? kPmEdge : kPmCsc);
+    if (rc) return rc;
+    return dispatch_k<BwdSegsum>(dim_k, csc_sched, csc_num_panels, csc_indptr, Pbuf, num_cols,
+                                 dim_k, dxs, carry, carry_row, st,
+                                 gather ? csc_pos : (const int32_t *)nullptr);
+}
+
+int maxk_sspmm_backward_multi(int algo, const int32_t *sched, int64_t num_panels,
+                              const int32_t *indptr, const int32_t *indices, const float *values,
+                              int num_rel, const float *grad, const uint8_t *cbsr_sel,
+                              int num_rows, int num_cols, int64_t num_edges, int dim_origin,
+                              int dim_k, float *dxs, const int32_t *csc_pos,
+                              const int32_t *csc_sched, int64_t csc_num_panels,
+                              const int32_t *csc_indptr, void *workspace, size_t workspace_bytes,
+                              void *stream)
+{
+    if (!sched || !indptr || !dxs || num_panels < 1 || num_rows < 0 || num_cols < 0 ||
+        num_edges < 0)
+        return MAXK_E_ARG;
+    if (num_rel != 4 && num_rel != 8 && num_rel != 16) return MAXK_E_ARG;
+    if (!dims_ok(dim_origin, dim_k) || (dim_origin & 3) ||
+        (dim_k != 8 && dim_k != 16 && dim_k != 32 && dim_k != 64))
+        return MAXK_E_DIM;
+    if (algo == MAXK_BWD_AUTO) algo = MAXK_BWD_STAGED;
+    if (algo != MAXK_BWD_STAGED && algo != MAXK_BWD_EDGE_GATHER) return MAXK_E_ARG;
+    hipStream_t st = as_stream(stream);
+    if (num_cols == 0) return MAXK_OK;
+    if (num_rows == 0 || num_edges == 0) return zero_floats(dxs, (size_t)num_cols * dim_k, st);
+    if (!indices || !values || !grad || !cbsr_sel || !csc_pos || !csc_sched || !csc_indptr ||
+        csc_num_panels < 1 || !workspace)
+        return MAXK_E_ARG;
+    if ((reinterpret_cast<uintptr_t>(values) | reinterpret_cast<uintptr_t>(grad)) & 15)
+        return MAXK_E_ARG;
+    const bool gather = algo == MAXK_BWD_EDGE_GATHER;
+    if (workspace_bytes < maxk_backward_workspace_bytes(algo, num_edges, dim_k, csc_num_panels))
+        return MAXK_E_WORKSPACE;
+    const int kp = dim_k == 8 && !gather ? 16 : dim_k;
+    const size_t pbytes = align_up((size_t)num_edges * kp * sizeof(float), 256);
+    const size_t carry_bytes = align_up((size_t)csc_num_panels * dim_k * sizeof(float), 256);
+    float *Pbuf = static_cast<float *>(workspace);
+    float *carry = reinterpret_cast<float *>(static_cast<char *>(workspace) + pbytes);
+    int32_t *carry_row = reinterpret_cast<int32_t *>(static_cast<char *>(workspace) + pbytes +
+                                                     carry_bytes);
+    int rc = dispatch_k<BwdMultiStage>(dim_k, num_rel, gather, sched, num_panels, indptr, indices,
+                                       values, grad, (int64_t)num_rows * dim_origin, cbsr_sel,
+                                       csc_pos, num_rows, dim_origin, Pbuf, st);
     if (rc) return rc;
     return dispatch_k<BwdSegsum>(dim_k, csc_sched, csc_num_panels, csc_indptr, Pbuf, num_cols,
                                  dim_k, dxs, carry, carry_row, st,

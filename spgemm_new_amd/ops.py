@@ -240,6 +240,7 @@ class MaxKGraph:
         self.tile_splits = tile_splits
         self._ws = {}
         self._bwd_choice = {}
+        self._multi_timings = {}  # ((multi key), algo) -> ms, AUTO's backward_multi timings
         self._bwd_alt = {}        # AUTO's best algorithm other than STAGED_EDGE, per key
         self._esel_on = set()     # (k, h): forwards write edge selectors (AUTO chose STAGED_EDGE)
         self._esel = []           # [(sel key, sel, uint8 buffer[E * k], pinned)], most recent last
@@ -713,10 +714,14 @@ class MaxKGraph:
                        out: torch.Tensor | None = None, algo: int = _lib.MAXK_BWD_AUTO):
         """Backward of forward_multi: dXs = sum_q (A_q^T G_q) sampled at sel,
         with grad fp32[R, V, h] and values fp32[E, R].  Returns fp32[V, k].
-        Composed from R single-relation backward calls (per-relation value
-        columns cached), summed on the device; for R a multiple of 8 and k = 32
-        (ogbn-proteins: R = 8) one LOCAL pass per 8 relations over the gradient
-        interleaved by relation instead (algo AUTO or LOCAL)."""
+        Algorithms: MAXK_BWD_MULTI_STAGED / MULTI_EDGE_GATHER -- one staged pass
+        that sums the R relations per edge in phase 1 (maxk_sspmm_backward_multi;
+        R in {4, 8, 16}, k in {8, 16, 32, 64}); LOCAL -- for R a multiple of 8
+        and k = 32, one LOCAL pass per 8 relations over the gradient interleaved
+        by relation; any single-relation algorithm -- composed from R
+        single-relation calls (per-relation value columns cached), summed on the
+        device.  AUTO times the fused candidates once per (k, h, R) (MAXK_AUTO=
+        fixed: MULTI_STAGED when it applies, then LOCAL rel8, else composed)."""
         check_tensor(grad, "grad_output", torch.float32, dim=3)
         check_tensor(values, "values", torch.float32, dim=2)
         R = values.shape[1]
@@ -729,29 +734,74 @@ class MaxKGraph:
         k = cbsr_sel.shape[1]
         if out is None:
             out = torch.empty((self.num_cols, k), dtype=torch.float32, device=self.device)
-        rel8_ok = (R % 8 == 0 and k == 32 and self.num_edges > 0 and self.local_plan(k) is not None)
-        if algo == _lib.MAXK_BWD_AUTO and rel8_ok:
-            # measured once per (h, R): the interleaved pass vs R composed calls
+        staged_ok = (R in (4, 8, 16) and k in (8, 16, 32, 64) and grad.shape[2] % 4 == 0
+                     and self.num_edges > 0 and values.data_ptr() % 16 == 0
+                     and grad.data_ptr() % 16 == 0)
+        if algo == _lib.MAXK_BWD_AUTO:
+            # the same lazily built plans the candidates need; rel8 last (its
+            # LOCAL plan costs the most to build)
+            fused = []
+            if staged_ok:
+                fused += [_lib.MAXK_BWD_MULTI_STAGED, _lib.MAXK_BWD_MULTI_EDGE_GATHER]
+            if R % 8 == 0 and k == 32 and self.num_edges > 0 and self.local_plan(k) is not None:
+                fused.append(_lib.MAXK_BWD_LOCAL)
             key = ("multi", k, grad.shape[2], R)
-            if key not in self._bwd_choice and not torch.cuda.is_current_stream_capturing():
-                ms = []
-                for fn in (lambda: self._backward_rel8(grad, cbsr_sel, values, out),
-                           lambda: self._backward_composed(grad, cbsr_sel, values, out,
-                                                           _lib.MAXK_BWD_AUTO)):
-                    fn()
-                    e0 = torch.cuda.Event(enable_timing=True)
-                    e1 = torch.cuda.Event(enable_timing=True)
-                    e0.record()
-                    fn()
-                    e1.record()
-                    e1.synchronize()
-                    ms.append(e0.elapsed_time(e1))
-                self._bwd_choice[key] = "rel8" if ms[0] <= ms[1] else "composed"
-            if self._bwd_choice.get(key, "rel8") == "rel8":
-                algo = _lib.MAXK_BWD_LOCAL
-        if algo == _lib.MAXK_BWD_LOCAL and rel8_ok:
+            if key in self._bwd_choice:
+                algo = self._bwd_choice[key]
+            elif not fused:
+                algo = _lib.MAXK_BWD_AUTO   # composed, each call its own AUTO
+            elif AUTO_MODE == "fixed" or len(fused) == 1 or \
+                    torch.cuda.is_current_stream_capturing():
+                algo = self._bwd_choice[key] = fused[0]
+            else:
+                # measured once per (k, h, R): each fused candidate run once, then
+                # timed AUTOTUNE_REPS times, the minimum kept
+                best = None
+                for a in fused:
+                    self.backward_multi(grad, cbsr_sel, values, out, a)
+                    t = float("inf")
+                    for _ in range(AUTOTUNE_REPS):
+                        e0 = torch.cuda.Event(enable_timing=True)
+                        e1 = torch.cuda.Event(enable_timing=True)
+                        e0.record()
+                        self.backward_multi(grad, cbsr_sel, values, out, a)
+                        e1.record()
+                        e1.synchronize()
+                        t = min(t, e0.elapsed_time(e1))
+                    self._multi_timings[(key, a)] = t
+                    if best is None or t < best[0]:
+                        best = (t, a)
+                algo = self._bwd_choice[key] = best[1]
+        if algo in (_lib.MAXK_BWD_MULTI_STAGED, _lib.MAXK_BWD_MULTI_EDGE_GATHER):
+            if not staged_ok:
+                raise RuntimeError("multi-relation STAGED backward needs R in {4, 8, 16}, k in "
+                                   "{8, 16, 32, 64}, h % 4 == 0 and 16-B aligned grad/values")
+            return self._backward_multi_staged(grad, cbsr_sel, values, out,
+                                               algo == _lib.MAXK_BWD_MULTI_EDGE_GATHER)
+        if algo == _lib.MAXK_BWD_LOCAL and R % 8 == 0 and k == 32 and self.num_edges > 0 \
+                and self.local_plan(k) is not None:
             return self._backward_rel8(grad, cbsr_sel, values, out)
         return self._backward_composed(grad, cbsr_sel, values, out, algo)
+
+    def _backward_multi_staged(self, grad, sel, values, out, edge_order: bool):
+        """One pass for all R relations (maxk_sspmm_backward_multi): phase 1 writes
+        per edge sum_q val[e,q] * G_q[row, sel[c, :]], phase 2 the CSC segmented sum
+        (edge_order: rows in edge order, gathered through the CSC permutation)."""
+        L = _lib.load()
+        k, h, R = sel.shape[1], grad.shape[2], values.shape[1]
+        cabi = _lib.MAXK_BWD_EDGE_GATHER if edge_order else _lib.MAXK_BWD_STAGED
+        csc_pos, csc_indptr, csc_sched, CP = self.csc()
+        if edge_order:
+            csc_pos = self.csc_perm()
+        ws = self._workspace(("bwd", k), L.maxk_backward_workspace_bytes(cabi, self.num_edges, k, CP))
+        _lib.check(L.maxk_sspmm_backward_multi(
+            cabi, self.bwd_sched.data_ptr(), self.bwd_num_panels, self.indptr.data_ptr(),
+            self.indices.data_ptr(), values.data_ptr(), R, grad.data_ptr(), sel.data_ptr(),
+            self.num_rows, self.num_cols, self.num_edges, h, k, out.data_ptr(), csc_pos.data_ptr(),
+            csc_sched.data_ptr(), CP, csc_indptr.data_ptr(), ws.data_ptr(), ws.numel(),
+            _stream(out)), "maxk_sspmm_backward_multi")
+        self.last_bwd_algo = "multi_edge_gather" if edge_order else "multi_staged"
+        return out
 
     def _backward_composed(self, grad, cbsr_sel, values, out, algo):
         R = values.shape[1]
