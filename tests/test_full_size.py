@@ -138,6 +138,15 @@ def test_full_size_proteins_multi_relation(dev):
     assert abs(lhs - rhs) / abs(lhs) <= 1e-6
     comp = g.backward_multi(Gr, sel, vals, algo=_lib.MAXK_BWD_STAGED)
     assert _rel(dx, comp) <= TOL
+    del comp
+    for algo in (_lib.MAXK_BWD_MULTI_STAGED, _lib.MAXK_BWD_MULTI_EDGE_GATHER):
+        dm = g.backward_multi(Gr, sel, vals, algo=algo)
+        assert _rel(dx, dm) <= TOL, algo
+        rhs = float((data.double() * dm.double()).sum())
+        assert abs(lhs - rhs) / abs(lhs) <= 1e-6, algo
+        dm2 = g.backward_multi(Gr, sel, vals, algo=algo)
+        assert torch.equal(dm, dm2), algo          # no atomics: bitwise repeatable
+        del dm, dm2
 
 
 def test_flickr_config1_full(dev, oracle):
