@@ -743,11 +743,23 @@ class MaxKGraph:
             fused = []
             if staged_ok:
                 fused += [_lib.MAXK_BWD_MULTI_STAGED, _lib.MAXK_BWD_MULTI_EDGE_GATHER]
-            if R % 8 == 0 and k == 32 and self.num_edges > 0 and self.local_plan(k) is not None:
-                fused.append(_lib.MAXK_BWD_LOCAL)
             key = ("multi", k, grad.shape[2], R)
+            # the LOCAL plan (the costliest to build) only when rel8 will be timed or is
+            # the only fused form
+            want_rel8 = key not in self._bwd_choice and (
+                not staged_ok or (AUTO_MODE != "fixed" and
+                                  not torch.cuda.is_current_stream_capturing()))
+            if want_rel8 and R % 8 == 0 and k == 32 and self.num_edges > 0 and \
+                    self.local_plan(k) is not None:
+                fused.append(_lib.MAXK_BWD_LOCAL)
             if key in self._bwd_choice:
                 algo = self._bwd_choice[key]
+                if algo in (_lib.MAXK_BWD_MULTI_STAGED, _lib.MAXK_BWD_MULTI_EDGE_GATHER) and \
+                        not staged_ok:
+                    # e.g. misaligned values: rel8, else composed (each call its own AUTO)
+                    algo = _lib.MAXK_BWD_LOCAL if (R % 8 == 0 and k == 32 and
+                                                   self.local_plan(k) is not None) \
+                        else _lib.MAXK_BWD_AUTO
             elif not fused:
                 algo = _lib.MAXK_BWD_AUTO   # composed, each call its own AUTO
             elif AUTO_MODE == "fixed" or len(fused) == 1 or \

@@ -152,3 +152,25 @@ def test_multi_staged_abi_rejects(dev):
     assert call(h=254) == _lib.MAXK_E_DIM
     assert call(algo=_lib.MAXK_BWD_ATOMIC) == _lib.MAXK_E_ARG
     assert call(vptr=vals.data_ptr() + 4) == _lib.MAXK_E_ARG
+
+
+def test_multi_auto_misaligned_values_fall_back(dev):
+    """AUTO's cached choice is the relation-summing kernel (16-B aligned inputs);
+    a later call whose values are a contiguous but misaligned view takes rel8 /
+    composed instead of failing, with the same result."""
+    indptr, indices = small_csr(600, seed=14)
+    v, e, R, k = len(indptr) - 1, len(indices), 8, 32
+    rng = np.random.default_rng(6)
+    vals = rng.random((e, R), dtype=np.float32)
+    _, sel = random_cbsr(v, k, 256, seed=4)
+    grad = T(rng.random((R, v, 256), dtype=np.float32), dev)
+    g = S.MaxKGraph(T(indptr, dev), T(indices, dev), panel_cost=256)
+    a = g.backward_multi(grad, T(sel, dev), T(vals, dev)).clone()
+    flat = torch.empty(e * R + 1, device=dev)
+    flat[1:] = T(vals, dev).reshape(-1)
+    mis = flat[1:].view(e, R)
+    assert mis.is_contiguous() and mis.data_ptr() % 16 != 0
+    b = g.backward_multi(grad, T(sel, dev), mis)
+    assert g.last_bwd_algo not in ("multi_staged", "multi_edge_gather")
+    err = ((a - b).abs() / b.abs().clamp_min(1)).max().item()
+    assert err <= TOL
