@@ -790,6 +790,9 @@ __device__ __forceinline__ void flush_multi(float *acc, int R, float *__restrict
 // edges per step with private row copies when L < 64, else L/64 passes.
 // Lanes of one step write distinct words (an edge's selected columns are
 // distinct; different edges use different copies).
+#ifndef FWD_REL8_SWZ
+#define FWD_REL8_SWZ 1   // R = 8: 8-float column records, quads XOR-swizzled (0: 12-float records)
+#endif
 template <int K, int R4>
 struct Rel4 {
     static_assert((R4 & (R4 - 1)) == 0, "R4 must be a power of two");
@@ -800,10 +803,20 @@ struct Rel4 {
     static constexpr int U = PASSES >= 8 ? 1 : 8 / PASSES;
     // floats per column record: an odd number of float4 quads, so the 4-bank
     // group of a b128 access (= col * S/4 mod 16) takes all 16 values; with
-    // S = 8 (R = 8) only 8 groups were used: 19 conflict cycles per
-    // ds_*_b128 measured on proteins (SQ_LDS_BANK_CONFLICT / SQ_INSTS_LDS)
-    static constexpr int S = (R4 & 1) ? R : R + 4;
+    // plain S = 8 (R = 8) only 8 groups were used: 19 conflict cycles per
+    // ds_*_b128 measured on proteins (SQ_LDS_BANK_CONFLICT / SQ_INSTS_LDS).
+    // R = 8 now keeps S = 8 with the two quads of column col swapped when bit 3
+    // of col is set (SWZ): quad 0's 16-B unit 2*col + (col >> 3 & 1) again
+    // takes all 16 values mod 16, and the record is 8 KB per copy instead of
+    // 12 (proteins forward 5.32 -> 5.12 ms, same sums bit for bit)
+    static constexpr bool SWZ = FWD_REL8_SWZ && R4 == 2;
+    static constexpr int S = (R4 & 1) || SWZ ? R : R + 4;
     static constexpr int ROW = kMaxDim * S;  // floats per accumulator copy
+    // word offset of relation quad rq of column col
+    static __device__ __forceinline__ uint32_t off(uint32_t col, int rq)
+    {
+        return col * S + 4 * (SWZ ? ((uint32_t)rq ^ ((col >> 3) & 1u)) : (uint32_t)rq);
+    }
 };
 
 // One round of U edges (EPS == 1: every lane works on the same edge): the
@@ -845,7 +858,7 @@ __device__ __forceinline__ void rel4_round_uniform(int my_c, int base, int s0, i
 #pragma unroll
         for (int p = 0; p < PASSES; ++p) {
             const int rq = (lane + p * kWave) / K;
-            f4 *a = reinterpret_cast<f4 *>(my + col[u][p] * C::S + 4 * rq);
+            f4 *a = reinterpret_cast<f4 *>(my + C::off(col[u][p], rq));
             *a += d[u][p] * v[u][p];
         }
     }
@@ -899,7 +912,7 @@ __device__ __forceinline__ void fwd_rel4_edges(int e0, int e1, const int32_t *__
 #pragma unroll
                     for (int p = 0; p < PASSES; ++p) {
                         const int rq = (lane % L) / K;
-                        f4 *a = reinterpret_cast<f4 *>(my + col[u][p] * C::S + 4 * rq);
+                        f4 *a = reinterpret_cast<f4 *>(my + C::off(col[u][p], rq));
                         *a += d[u][p] * v[u][p];
                     }
                 }
@@ -923,10 +936,12 @@ __device__ __forceinline__ void flush_rel4(float *acc, float *__restrict__ dst, 
         const int q = i / d4, c4 = i - q * d4;
         f4 s = f4{0.f, 0.f, 0.f, 0.f};
         for (int cp = 0; cp < C::EPS; ++cp) {
-            constexpr int S = C::S;
-            float *b = acc + cp * C::ROW + (4 * c4) * S + q;
-            s.x += b[0]; s.y += b[S]; s.z += b[2 * S]; s.w += b[3 * S];
-            b[0] = 0.f; b[S] = 0.f; b[2 * S] = 0.f; b[3 * S] = 0.f;
+            float *b = acc + cp * C::ROW + (q & 3);
+            const int c0 = 4 * c4;
+            float *b0 = b + C::off(c0, q >> 2), *b1 = b + C::off(c0 + 1, q >> 2);
+            float *b2 = b + C::off(c0 + 2, q >> 2), *b3 = b + C::off(c0 + 3, q >> 2);
+            s.x += *b0; s.y += *b1; s.z += *b2; s.w += *b3;
+            *b0 = 0.f; *b1 = 0.f; *b2 = 0.f; *b3 = 0.f;
         }
         float *o = dst + q * rel_stride + 4 * c4;
         if ((dim & 3) == 0) {
@@ -1998,7 +2013,9 @@ __global__ __launch_bounds__(kBlock) void cbsr_bank_order_kernel(const float *__
         const bool on = lane < k;
         const int c = on ? sel[r * k + lane] : 0;
         const float d = on ? data[r * k + lane] : 0.f;
-        const int res = c & 7;
+        // the 16-B unit of quad 0 mod 8: 3c with S = 12 (c mod 8), 2c + (c >> 3 & 1)
+        // with the swizzled 8-float records
+        const int res = FWD_REL8_SWZ ? (c & 3) | (((c >> 3) & 1) << 2) : c & 7;
         uint64_t mine = 0;
         int cnt[8];
 #pragma unroll

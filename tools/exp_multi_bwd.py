@@ -35,6 +35,7 @@ def main():
     ap.add_argument("--k", type=int, default=32)
     ap.add_argument("--R", type=int, default=8)
     ap.add_argument("--algos", default="rel8,multi_staged,multi_edge_gather")
+    ap.add_argument("--fwd", action="store_true", help="also time forward_multi")
     a = ap.parse_args()
     dev = torch.device("cuda:0")
     V, E, h, R, k = 132534, 79122504, 256, a.R, a.k
@@ -59,6 +60,10 @@ def main():
         res[name] = out
         print(f"{name}: min {mn:.3f} ms  median {md:.3f} ms  ({g.last_bwd_algo})", flush=True)
     y = g.forward_multi(data, sel, vals, h)
+    if a.fwd:
+        mn, md = timed(lambda: g.forward_multi(data, sel, vals, h, out=y), a.reps)
+        print(f"forward_multi: min {mn:.3f} ms  median {md:.3f} ms  checksum "
+              f"{float(y.double().sum()):.6e}", flush=True)
     lhs = float((y.double() * G.double()).sum())
     del y
     for name, dx in res.items():
