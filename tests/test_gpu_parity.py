@@ -801,14 +801,23 @@ def test_forward_records_errors(dev, g_small):
     assert rc == _lib.MAXK_E_ARG
 
 
+def _store_class(cols):
+    """The R = 8 accumulator's 16-B unit of quad 0 mod 8 (8-float records, quads
+    swapped when bit 3 of the column is set: unit 2c + (c >> 3 & 1)), as a class
+    0..7: (c & 3) | (c >> 3 & 1) << 2."""
+    cols = np.asarray(cols, dtype=int)
+    return (cols & 3) | (((cols >> 3) & 1) << 2)
+
+
 def _lds_conflicts(cols):
     """Extra LDS cycles of the relation-vector kernel's accesses for one row's entry
-    order: ds_write_b128 groups of 8 contiguous entries (bank unit = col mod 8) and
-    ds_read_b128 16-lane groups (col mod 16) -- S / 4 is odd, so col residues decide."""
+    order: ds_write_b128 groups of 8 contiguous entries (bank unit class
+    _store_class) and ds_read_b128 16-lane groups (unit mod 16, a bijection of
+    col mod 16)."""
     cols = np.asarray(cols, dtype=int)
     extra = 0
     for g0 in range(0, len(cols) - len(cols) % 8, 8):
-        extra += np.bincount(cols[g0:g0 + 8] % 8, minlength=8).max() - 1
+        extra += np.bincount(_store_class(cols[g0:g0 + 8]), minlength=8).max() - 1
     rg = [list(range(0, 4)) + list(range(12, 16)) + list(range(20, 28)),
           list(range(4, 12)) + list(range(16, 20)) + list(range(28, 32))]
     for b in range(0, len(cols) - len(cols) % 32, 32):
@@ -821,14 +830,14 @@ def _lds_conflicts(cols):
 def test_cbsr_bank_order(dev, k):
     """maxk_cbsr_bank_order permutes each row's (value, column) pairs (same set) and
     lowers the LDS conflicts of the fused multi-relation forward's accesses; a row
-    with four columns per residue mod 8 (k = 32) has conflict-free store groups."""
+    with four columns per store class (k = 32) has conflict-free store groups."""
     v, h = 500, 256
     data, sel = random_cbsr(v, k, h, seed=k)
-    if k == 32:   # a few rows balanced mod 8
+    if k == 32:   # a few rows balanced over the 8 store classes
         for r in range(0, 40):
             rng = np.random.default_rng(r)
-            sel[r] = np.array([q + 8 * b for q in range(8)
-                               for b in rng.choice(32, 4, replace=False)], dtype=np.uint8)
+            sel[r] = np.array([(q & 3) | ((q >> 2) << 3) | (b << 4) for q in range(8)
+                               for b in rng.choice(16, 4, replace=False)], dtype=np.uint8)
     L = _lib.load()
     od = torch.empty((v, k), device=dev)
     os_ = torch.empty((v, k), dtype=torch.uint8, device=dev)
@@ -844,7 +853,7 @@ def test_cbsr_bank_order(dev, k):
         after += _lds_conflicts(os_[r])
         if k == 32 and r < 40:
             for g0 in range(0, 32, 8):
-                assert len(set(os_[r][g0:g0 + 8] % 8)) == 8
+                assert len(set(_store_class(os_[r][g0:g0 + 8]))) == 8
     assert after <= before, (before, after)
     if k >= 16:   # (k = 8: one store group, its set of columns is fixed)
         assert after < before, (before, after)
