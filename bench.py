@@ -347,6 +347,45 @@ def vendor_baseline(g, indptr, indices, values, X, sel, y, fwd_ms, ev_ms):
     return out
 
 
+def vendor_backward_reference(indptr, indices, values, grad, sel, num_cols=None):
+    """An independent per-element reference of the backward SSpMM at any size
+    (VERDICT r3): dXs_ref = (A^T . G) gathered at sel, with A^T built by torch
+    (COO transpose + coalesce) and the product by rocSPARSE fp32 SpMM through
+    torch.sparse.mm -- no code of this repository on the path.  Matches the
+    reference kernel's math (kernels/spmm_maxk_backward.cu:15-115: dXs[c, l] =
+    sum over in-edges e of c of val[e] * G[row(e), sel[c, l]])."""
+    V = indptr.numel() - 1
+    C = V if num_cols is None else num_cols
+    e0, e1 = int(indptr[0]), int(indptr[-1])
+    rows = torch.repeat_interleave(torch.arange(V, device=indptr.device),
+                                   (indptr[1:] - indptr[:-1]).long(), output_size=e1 - e0)
+    idx = torch.stack([indices[e0:e1].long(), rows])
+    del rows
+    at = torch.sparse_coo_tensor(idx, values[e0:e1], (C, V)).coalesce().to_sparse_csr()
+    del idx
+    full = torch.sparse.mm(at, grad)
+    del at
+    ref = torch.gather(full, 1, sel.long())
+    del full
+    return ref
+
+
+def bwd_check(dx, ref, y, grad, data, staged=None):
+    """The timed dx against the rocSPARSE reference (per element, |d| / max(1,
+    |ref|)), the exact adjoint identity <A.X^, G> = <X^_s, dXs> (fp64 sums) and,
+    when given, STAGED (another algorithm of this repository)."""
+    lhs = float((y.double() * grad.double()).sum())
+    rhs = float((data.double() * dx.double()).sum())
+    out = {"vs": "rocsparse",
+           "ref": "torch.sparse.mm(A^T, G) gathered at sel (rocSPARSE fp32 SpMM, A^T by torch)",
+           "max_rel_diff": float(((dx - ref).abs() / ref.abs().clamp_min(1)).max()),
+           "adjoint_rel_err": abs(lhs - rhs) / max(abs(lhs), 1e-30)}
+    if staged is not None:
+        out["vs_staged_max_rel_diff"] = float(((dx - staged).abs()
+                                               / staged.abs().clamp_min(1)).max())
+    return out
+
+
 def bench_multi_partitioned(args, indptr, indices, vals, data, sel, V, E, h, k, R, dev, world,
                             rank, dist, gen, b_fused):
     """Config 5 on N GPUs: rows partitioned as in the single-relation path, one
@@ -432,7 +471,53 @@ def _ms_stats(xs):
             "min": round(min(xs), 4)}
 
 
-SWEEP_ENTRIES = ("products_k8", "products_k16", "products_k32", "products_k64", "proteins_r8")
+SWEEP_ENTRIES = ("flickr_cpu", "products_k8", "products_k16", "products_k32", "products_k64",
+                 "proteins_r8")
+
+
+def flickr_config1(args, dev):
+    """BASELINE config 1: Flickr (89,250 nodes, 899,756 edges + self-loops, as
+    scripts_train/flickr_maxk.sh:15 --selfloop; values 1), h=64, k=16 -- the
+    reference's CPU aggregation path (utils/models.py:281-287: torch.sparse.mm
+    sum and mean forms, and the backward A^T G * mask) timed on the host cores
+    over the WHOLE graph, ms and GB/s; our GPU forward + backward of the same
+    shape beside it."""
+    import spgemm_new_amd as S
+    from spgemm_new_amd.graphs import CONFIGS, synthetic_columns, synthetic_indptr
+    from spgemm_new_amd.ops import topk_cbsr
+    V, E = CONFIGS["flickr"]
+    h, k = 64, 16
+    indptr = synthetic_indptr(V, E, seed=args.seed, device=dev)
+    indices = synthetic_columns(indptr, seed=args.seed, self_loops=True)
+    values = torch.ones(indices.numel(), device=dev)
+    gen = torch.Generator(device=dev)
+    gen.manual_seed(args.seed + 1)
+    X = torch.rand((V, h), generator=gen, device=dev)
+    G = torch.rand((V, h), generator=gen, device=dev)
+    data, sel = topk_cbsr(X, k)
+    mask = torch.zeros((V, h), device=dev).scatter_(1, sel.long(), 1.0)
+    cpu = cpu_baseline(indptr, indices, values, (X * mask).cpu(), G.cpu(), mask.cpu(), k, h,
+                       budget_s=max(args.cpu_seconds, 20.0))
+    g = S.MaxKGraph(indptr, indices, values)
+    y = torch.empty((V, h), device=dev)
+    dx = torch.empty((V, k), device=dev)
+    g.backward(G, sel, out=dx)
+    fw, bw = _timed_calls([lambda: g.forward(data, sel, h, out=y, edge_sel="auto"),
+                           lambda: g.backward(G, sel, out=dx)], max(args.steps, 20),
+                          max(args.warmup, 5))
+    b = g.nbytes_fwd(k, h)
+    cpu_fwd_ms = cpu["fwd_ms_sample"] * cpu["ms_per_step_full_graph"] / max(cpu["ms_per_step_sample"],
+                                                                              1e-9)
+    return {"graph": "flickr (self-loops)", "num_nodes": V, "num_edges": E, "hidden": h, "k": k,
+            "algorithmic_bytes_per_call": b,
+            "cpu_reference": cpu,
+            "cpu_fwd_sum_form_ms": round(cpu_fwd_ms, 3),
+            "cpu_fwd_sum_form_GBs": round(b / (cpu_fwd_ms / 1e3) / 1e9, 3),
+            "cpu_fwd_mean_form_ms": cpu["mean_form_fwd_ms_sample"],
+            "cpu_fwd_mean_form_GBs": cpu["mean_form_GBs"],
+            "gpu_fwd_ms": _ms_stats(fw), "gpu_bwd_ms": _ms_stats(bw),
+            "gpu_bwd_algo": g.last_bwd_algo,
+            "gpu_step_GBs": round(2 * b / ((sum(fw) + sum(bw)) / len(fw) / 1e3) / 1e9, 1)}
 
 
 def config_sweep(args, dev, only=None):
@@ -456,6 +541,13 @@ def config_sweep(args, dev, only=None):
                        "synthetic generator as the headline (seed 123)"}
     want = set(only) if only else set(SWEEP_ENTRIES)
     t_all = time.time()
+    if "flickr_cpu" in want:
+        t0 = time.time()
+        out["flickr_cpu"] = flickr_config1(args, dev)
+        out["flickr_cpu"]["wall_s"] = round(time.time() - t0, 1)
+        log(f"[bench] sweep flickr (config 1): CPU fwd {out['flickr_cpu']['cpu_fwd_sum_form_ms']} ms "
+            f"in {time.time() - t0:.1f}s")
+        torch.cuda.empty_cache()
     ks = [k for k in (8, 16, 32, 64) if f"products_k{k}" in want]
     if ks:
         V, E = CONFIGS["products"]
@@ -481,9 +573,9 @@ def config_sweep(args, dev, only=None):
             nb = g._fwd_blocks.get((k, h), 0)
             b = g.nbytes_fwd(k, h)
             torch.cuda.synchronize()
-            dx_ref = g.backward(G, sel, algo=_lib.MAXK_BWD_STAGED)
-            lhs = float((y.double() * G.double()).sum())
-            rhs = float((data.double() * dx.double()).sum())
+            dx_st = g.backward(G, sel, algo=_lib.MAXK_BWD_STAGED)
+            chk = bwd_check(dx, vendor_backward_reference(indptr, indices, values, G, sel), y, G,
+                            data, dx_st)
             fs, bs = _ms_stats(fw), _ms_stats(bw)
             st = [a + c for a, c in zip(fw, bw)]
             out[f"products_k{k}"] = {
@@ -497,14 +589,11 @@ def config_sweep(args, dev, only=None):
                 "bwd_candidates_ms": getattr(g, "bwd_candidates", {}).get((k, h, True)),
                 "fwd_form": (f"column-blocked nb={nb}" if nb else
                                                "packed CBSR records" if k <= 16 else "plain"),
-                "bwd_check": {"vs": "staged",
-                              "max_rel_diff": float(((dx - dx_ref).abs()
-                                                     / dx_ref.abs().clamp_min(1)).max()),
-                              "adjoint_rel_err": abs(lhs - rhs) / max(abs(lhs), 1e-30)},
+                "bwd_check": chk,
                 "wall_s": round(time.time() - t0, 1)}
             log(f"[bench] sweep products k={k}: fwd {fs['mean']:.3f} bwd {bs['mean']:.3f} ms "
                 f"({algo}) in {time.time() - t0:.1f}s")
-            del data, sel, dx, dx_ref
+            del data, sel, dx, dx_st
             # drop the per-k plans and buffers before the next k
             g._ws.clear()
             g._esel.clear()
@@ -539,6 +628,21 @@ def config_sweep(args, dev, only=None):
         fwd_err = float(((y[0] - y0).abs() / y0.abs().clamp_min(1)).max())
         lhs = float((y.double() * G.double()).sum())
         rhs = float((data.double() * dx.double()).sum())
+        # independent per-element references (rocSPARSE through torch.sparse.mm): every
+        # relation's forward A_q . X^ and the backward sum_q (A_q^T G_q) gathered at sel
+        xm = torch.zeros((V, h), device=dev).scatter_(1, sel.long(), data)
+        fwd_vendor, ref = 0.0, None
+        for q in range(R):
+            vq = vals[:, q].contiguous()
+            a = torch.sparse_csr_tensor(indptr.long(), indices.long(), vq, size=(V, V))
+            yq = torch.sparse.mm(a, xm)
+            fwd_vendor = max(fwd_vendor, float(((y[q] - yq).abs() / yq.abs().clamp_min(1)).max()))
+            del a, yq
+            rq = vendor_backward_reference(indptr, indices, vq, G[q], sel)
+            ref = rq if ref is None else ref.add_(rq)
+            del rq, vq
+        bwd_vendor = float(((dx - ref).abs() / ref.abs().clamp_min(1)).max())
+        del xm, ref
         b = E * (4 + 4 * R + 5 * k) + R * 4 * h * V
         fs, bs = _ms_stats(fw), _ms_stats(bw)
         out["proteins_r8"] = {
@@ -550,6 +654,10 @@ def config_sweep(args, dev, only=None):
             "bwd_frac": round(b / (bs["mean"] / 1e3) / 1e9 / HBM_PEAK_GBS, 4),
             "bwd_algo": g.last_bwd_algo,
             "check": {"fwd_rel0_vs_single_max_rel_diff": fwd_err,
+                      "fwd_vs_rocsparse_max_rel_diff": fwd_vendor,
+                      "bwd_vs_rocsparse_max_rel_diff": bwd_vendor,
+                      "ref": "per relation torch.sparse.mm(A_q, X^) and sum_q torch.sparse.mm"
+                             "(A_q^T, G_q) gathered at sel (rocSPARSE fp32)",
                       "adjoint_rel_err": abs(lhs - rhs) / max(abs(lhs), 1e-30)},
             "wall_s": round(time.time() - t0, 1)}
         log(f"[bench] sweep proteins R=8: fwd {fs['mean']:.3f} bwd {bs['mean']:.3f} ms "
@@ -650,8 +758,71 @@ def bench_multi(args, S, indptr, indices, data, sel, V, E, h, k, dev, world, ran
     print(json.dumps(result), flush=True)
 
 
+def _free_port() -> int:
+    import socket
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def launch_ranks(args) -> int:
+    """`python bench.py --gpus N` (N > 1) without an outside launcher: this process
+    makes NO GPU call (torch.cuda.device_count() does not initialise the device on
+    this image); it starts N ranks as ONE child `python -m torch.distributed.run
+    --nproc-per-node N` with the same arguments, relays rank 0's JSON line and
+    returns non-zero when N exceeds the visible devices (RCCL: one GPU per rank),
+    when any rank fails, or when the line's n_gpus is not N.  BENCH_BACKEND=gloo
+    (a rehearsal of the N > 1 logic) may share GPUs between ranks."""
+    import subprocess
+    n = args.gpus
+    backend = os.environ.get("BENCH_BACKEND", "nccl")
+    visible = torch.cuda.device_count()
+    if backend == "nccl" and n > visible:
+        log(f"[bench] --gpus {n} but {visible} GPU(s) visible: refusing (one GPU per rank)")
+        return 3
+    if visible < 1:
+        log("[bench] no GPU visible")
+        return 3
+    port = os.environ.get("MASTER_PORT") or str(_free_port())
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
+           "--master-addr", "127.0.0.1", "--master-port", port, os.path.abspath(__file__),
+           *sys.argv[1:]]
+    log(f"[bench] launching {n} ranks: {' '.join(cmd)}")
+    env = dict(os.environ, MASTER_ADDR="127.0.0.1", MASTER_PORT=port)
+    proc = subprocess.run(cmd, stdout=subprocess.PIPE, env=env, text=True)
+    lines = [ln for ln in proc.stdout.splitlines() if ln.startswith("{")]
+    for ln in proc.stdout.splitlines():
+        if not ln.startswith("{"):
+            log(ln)
+    if proc.returncode != 0:
+        log(f"[bench] a rank failed (torch.distributed.run rc={proc.returncode})")
+        return proc.returncode or 1
+    if len(lines) != 1:
+        log(f"[bench] expected one JSON line from rank 0, got {len(lines)}")
+        return 4
+    try:
+        d = json.loads(lines[0])
+    except ValueError:
+        log("[bench] rank 0's line is not JSON")
+        return 4
+    if d.get("n_gpus") != n:
+        log(f"[bench] rank 0 reports n_gpus={d.get('n_gpus')} for --gpus {n}")
+        return 5
+    print(lines[0], flush=True)
+    return 0
+
+
 def main():
     args = parse()
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        sys.exit(launch_ranks(args))
+    world_env = int(os.environ.get("WORLD_SIZE", "1"))
+    if world_env != args.gpus:
+        # a launcher that started another number of ranks than --gpus asks for
+        log(f"[bench] WORLD_SIZE={world_env} but --gpus {args.gpus}: refusing")
+        sys.exit(6)
     # the algorithm choices (forward column blocks, backward algorithm): by rule of the
     # shape (default; the same choices, summation order and bits on every box) or timed
     os.environ.setdefault("MAXK_AUTO", args.auto)
@@ -664,8 +835,6 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
-    if world != args.gpus and world > 1:
-        log(f"warning: WORLD_SIZE={world} but --gpus {args.gpus}")
     # one GPU per rank; ranks beyond the visible GPUs share them (only for the
     # BENCH_BACKEND=gloo rehearsal of the N>1 path on a one-GPU box)
     dev_index = local_rank % max(1, torch.cuda.device_count())
@@ -838,6 +1007,18 @@ def main():
                               "algorithmic_bytes_per_launch": int(b_max)}
         result["fwd_ms"] = round(fms, 4)
         result["bwd_ms"] = round(bms, 4)
+        # each exchange alone on the wire (HIP events around the synchronous
+        # collective, step-sized messages), max over ranks; the step overlaps them
+        # with compute where it can
+        ex = model.exchange_ms(k)
+        names = sorted(kk for kk in ex if kk.endswith("_ms"))
+        t = torch.tensor([ex[kk] for kk in names], device=dev, dtype=torch.float64)
+        if dist:
+            dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        result["exchange_ms_max_over_ranks"] = {kk: round(float(v), 4) for kk, v in zip(names, t)}
+        result["exchange_bytes_rank0"] = {kk: v for kk, v in ex.items() if not kk.endswith("_ms")}
+        result["local_bwd_algo_rank0"] = model.local.last_bwd_algo if not model.overlap else \
+            {"own": model.local_own.last_bwd_algo, "halo": model.local_halo.last_bwd_algo}
     if not partitioned:
         # per-call timing with HIP events on the launch stream (the current stream)
         st = torch.cuda.current_stream()
@@ -893,17 +1074,13 @@ def main():
         result["bwd_ms_median"] = round(_median(bw), 4)
         result["config"]["bwd_algo"] = g.last_bwd_algo
         # untimed parity check of the timed outputs: dx of the timed algorithm vs
-        # STAGED (an independent algorithm), and the exact adjoint identity
-        # <A.X^, G> = <X^_s, dXs> (fp64 sums) for the timed y and dx
+        # rocSPARSE's A^T G gathered at sel (independent of this repository), vs
+        # STAGED, and the exact adjoint identity <A.X^, G> = <X^_s, dXs> (fp64 sums)
         torch.cuda.synchronize()
-        dx_ref = g.backward(G, sel, algo=_lib.MAXK_BWD_STAGED)
-        lhs = float((y.double() * G.double()).sum())
-        rhs = float((data.double() * dx.double()).sum())
-        result["bwd_check"] = {
-            "vs": "staged",
-            "max_rel_diff": float(((dx - dx_ref).abs() / dx_ref.abs().clamp_min(1)).max()),
-            "adjoint_rel_err": abs(lhs - rhs) / max(abs(lhs), 1e-30)}
-        del dx_ref
+        dx_st = g.backward(G, sel, algo=_lib.MAXK_BWD_STAGED)
+        result["bwd_check"] = bwd_check(dx, vendor_backward_reference(indptr, indices, values, G,
+                                                                      sel), y, G, data, dx_st)
+        del dx_st
         result["fwd_ms"] = round(fms, 4)
         result["bwd_ms"] = round(bms, 4)
         result["fwd_GBs"] = round(b_call / fms / 1e6, 1)

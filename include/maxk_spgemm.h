@@ -254,11 +254,12 @@ int maxk_spmm_dense_forward(const int32_t *sched, int64_t num_panels, const int3
  * ------------------------------------------------------------------------- */
 size_t maxk_forward_multi_workspace_bytes(int64_t num_panels, int dim_origin, int num_rel);
 /* The same CBSR with each row's entries in bank-aware order for the fused
- * forward (its LDS stores go 8 entries at a time; columns that differ mod 8
- * do not conflict).  Any order is a valid CBSR and the forward's result is
- * bit-identical; dim_k <= 64.  out_data / out_sel: num_rows x dim_k. */
+ * forward over num_rel relations (its LDS stores go 8 entries at a time; the
+ * store classes follow the num_rel record layout).  Any order is a valid CBSR
+ * and the forward's result is bit-identical; dim_k <= 64, 1 <= num_rel <= 16.
+ * out_data / out_sel: num_rows x dim_k. */
 int maxk_cbsr_bank_order(const float *cbsr_data, const uint8_t *cbsr_sel, int num_rows,
-                         int dim_k, float *out_data, uint8_t *out_sel, void *stream);
+                         int dim_k, int num_rel, float *out_data, uint8_t *out_sel, void *stream);
 int maxk_spgemm_forward_multi(const int32_t *sched, int64_t num_panels, const int32_t *indptr,
                               const int32_t *indices, const float *values, int num_rel,
                               const float *cbsr_data, const uint8_t *cbsr_sel, int num_rows,

@@ -105,7 +105,7 @@ SIGNATURES = {
     "maxk_records_sel_gather": (_I, [_P, _I, _P, _L, _P, _P]),
     "maxk_cbsr_gather_records": (_I, [_P, _P, _P, _L, _I, _P, _P]),
     "maxk_spgemm_forward_records": (_I, [_P, _L, _P, _P, _P, _P, _I, _I, _I, _I, _P, _P, _S, _P]),
-    "maxk_cbsr_bank_order": (_I, [_P, _P, _I, _I, _P, _P, _P]),
+    "maxk_cbsr_bank_order": (_I, [_P, _P, _I, _I, _I, _P, _P, _P]),
     "maxk_segment_rows_add": (_I, [_P, _I, _P, _P, _P, _L, _P, _P]),
     "maxk_topk_cbsr": (_I, [_P, _I, _I, _L, _I, _I, _P, _P, _P, _P]),
     "maxk_cbsr_scatter": (_I, [_P, _P, _I, _I, _I, _P, _P]),

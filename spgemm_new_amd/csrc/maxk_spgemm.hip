@@ -2001,7 +2001,7 @@ __global__ __launch_bounds__(kBlock) void bwd_local_kernel(
 // One wave per row, k <= 64.
 __global__ __launch_bounds__(kBlock) void cbsr_bank_order_kernel(const float *__restrict__ data,
                                                                  const uint8_t *__restrict__ sel,
-                                                                 int num_rows, int k,
+                                                                 int num_rows, int k, int swz,
                                                                  float *__restrict__ odata,
                                                                  uint8_t *__restrict__ osel)
 {
@@ -2013,9 +2013,9 @@ __global__ __launch_bounds__(kBlock) void cbsr_bank_order_kernel(const float *__
         const bool on = lane < k;
         const int c = on ? sel[r * k + lane] : 0;
         const float d = on ? data[r * k + lane] : 0.f;
-        // the 16-B unit of quad 0 mod 8: 3c with S = 12 (c mod 8), 2c + (c >> 3 & 1)
-        // with the swizzled 8-float records
-        const int res = FWD_REL8_SWZ ? (c & 3) | (((c >> 3) & 1) << 2) : c & 7;
+        // the 16-B unit of quad 0 mod 8: (S / 4) c with odd S / 4 (R = 4, 12, 16
+        // records: c mod 8), 2c + (c >> 3 & 1) with the swizzled 8-float R = 8 records
+        const int res = swz ? (c & 3) | (((c >> 3) & 1) << 2) : c & 7;
         uint64_t mine = 0;
         int cnt[8];
 #pragma unroll
@@ -3971,16 +3971,19 @@ int maxk_spgemm_forward_records(const int32_t *sched, int64_t num_panels, const 
 }
 
 int maxk_cbsr_bank_order(const float *cbsr_data, const uint8_t *cbsr_sel, int num_rows,
-                         int dim_k, float *out_data, uint8_t *out_sel, void *stream)
+                         int dim_k, int num_rel, float *out_data, uint8_t *out_sel, void *stream)
 {
     if (dim_k < 1 || dim_k > kWave) return MAXK_E_DIM;
+    if (num_rel < 1 || num_rel > 16) return MAXK_E_ARG;
+    // the store classes follow the record layout maxk_spgemm_forward_multi uses for num_rel
+    const int swz = (FWD_REL8_SWZ && num_rel == 8) ? 1 : 0;
     if (num_rows < 0 || (num_rows > 0 && (!cbsr_data || !cbsr_sel || !out_data || !out_sel)))
         return MAXK_E_ARG;
     if (num_rows == 0) return MAXK_OK;
     const int64_t blocks = ceil_div(num_rows, kWavesPerBlock);
     hipLaunchKernelGGL(cbsr_bank_order_kernel, dim3((unsigned)(blocks < 4096 ? blocks : 4096)),
                        dim3(kBlock), 0, as_stream(stream), cbsr_data, cbsr_sel, num_rows, dim_k,
-                       out_data, out_sel);
+                       swz, out_data, out_sel);
     return launch_status();
 }
 

@@ -135,6 +135,16 @@ class HaloPlan:
         return self.num_halo * 5
 
 
+def _train_fwd(eng, data, sel, dim_origin):
+    """A training forward of a local block: its backward follows with the same
+    selector tensor, so a MaxKGraph engine writes the edge selectors when its
+    AUTO backward chose an edge-selector algorithm (edge_sel="auto", as
+    SpGEMMFunction does)."""
+    if isinstance(eng, MaxKGraph):
+        return eng.forward(data, sel, dim_origin, edge_sel="auto")
+    return eng.forward(data, sel, dim_origin)
+
+
 def _default_engine(local_indptr, local_indices, local_values, num_cols, **kw):
     return MaxKGraph(local_indptr, local_indices, local_values, num_cols=num_cols, **kw)
 
@@ -231,8 +241,12 @@ class PartitionedMaxK:
             # of compute per step on Reddit blocks (two engines, their own launches
             # and partials: N=2/4/8 step 3.10/1.84/1.04 ms split vs 2.72/1.57/0.89
             # single, tools/exp_rank_step.py) against 19-33 MB of halo records, a
-            # few tenths of that over 7 xGMI links; products' 200-340 MB are not
-            overlap = p.num_halo * OVERLAP_BYTES_PER_HALO_NODE >= OVERLAP_MIN_HALO_BYTES
+            # few tenths of that over 7 xGMI links; products' 200-340 MB are not.
+            # Decided on the LARGEST halo over the ranks (one all-reduce), so every
+            # rank takes the same decision (a per-rank choice let split
+            # and unsplit ranks call different collectives in all-gather mode)
+            overlap = self._max_over_ranks(float(p.num_halo)) * OVERLAP_BYTES_PER_HALO_NODE \
+                >= OVERLAP_MIN_HALO_BYTES
         elif not isinstance(overlap, bool):
             raise RuntimeError("overlap must be True, False or 'auto'")
         self.overlap = overlap and p.num_halo > 0
@@ -267,23 +281,46 @@ class PartitionedMaxK:
             else bool(overlap_backward and self.overlap)
         self._bufs = {}
         self._fwd_sel = None     # sel_own of the last forward
+        self._fwd_block_sel = None   # the single-block forward's own + halo selectors
         self._halo_part = None   # its halo selectors: [num_halo, k] (view of records or rows)
 
     # --------------------------------------------------------------- helpers
+    def _max_over_ranks(self, *xs: float) -> list[float] | float:
+        """Element-wise MAX of the given floats over all ranks (one all-reduce;
+        the values themselves at world 1)."""
+        if self.world == 1:
+            return xs[0] if len(xs) == 1 else list(xs)
+        t = torch.tensor(xs, dtype=torch.float64)
+        if dist.get_backend() != "gloo":
+            t = t.to(self.device)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        out = t.cpu().tolist()
+        return out[0] if len(xs) == 1 else out
+
     def _pick_halo_mode(self, mode: str) -> str:
+        """Decided collectively: the all-gather path needs the own | halo split on
+        EVERY rank (a rank without it -- overlap off, or no halo at all -- would
+        call the all-to-all-v of gather_halo_cbsr while the others all-gather),
+        so one all-reduce carries the largest halo fraction and whether any rank
+        is unsplit; "allgather" is only taken when no rank is."""
         if mode not in ("auto", "records", "allgather"):
             raise RuntimeError("halo_mode must be 'auto', 'records' or 'allgather'")
-        if mode != "auto" or self.world == 1:
+        if self.world == 1:
             return "records" if mode == "auto" else mode
+        if mode == "records":
+            return mode
         p = self.plan
         V = self.bounds[-1]
-        frac = torch.tensor([p.num_halo / max(1, V)], dtype=torch.float64)
-        if dist.get_backend() != "gloo":
-            frac = frac.to(self.device)
-        dist.all_reduce(frac, op=dist.ReduceOp.MAX)
-        return "allgather" if float(frac) > HALO_ALLGATHER_FRAC else "records"
+        frac, unsplit = self._max_over_ranks(p.num_halo / max(1, V), 0.0 if self.overlap else 1.0)
+        if unsplit > 0:
+            return "records"
+        if mode == "allgather":
+            return mode
+        return "allgather" if frac > HALO_ALLGATHER_FRAC else "records"
 
     def _allgather_ok(self, k: int) -> bool:
+        # halo_mode == "allgather" implies every rank is split (_pick_halo_mode); k is
+        # the same on every rank, so the records test agrees too
         return (self.halo_mode == "allgather" and self.overlap and self.world > 1
                 and self._use_records(k, self.local_halo))
 
@@ -362,6 +399,7 @@ class PartitionedMaxK:
         data[p.num_own:] = (hd if (5 * k) % 4 == 0 else hd.contiguous()).view(torch.float32)
         sel[p.num_own:] = recv[:, 4 * k:]
         self._fwd_sel, self._halo_part = sel_own, sel[p.num_own:]
+        self._fwd_block_sel = sel
         return data, sel
 
     def forward(self, data_own: torch.Tensor, sel_own: torch.Tensor, dim_origin: int = 256):
@@ -372,7 +410,7 @@ class PartitionedMaxK:
             # of whole 160-B records read in place measured slower than data +
             # selector rows at full size: 3.63 vs 3.31 ms, tools/exp_rank_step.py)
             data, sel = self.gather_halo_cbsr(data_own, sel_own)
-            return self.local.forward(data, sel, dim_origin)
+            return _train_fwd(self.local, data, sel, dim_origin)
         if not self._use_records(k, self.local_halo):
             return self._forward_overlap_rows(data_own, sel_own, dim_origin)
         if self._allgather_ok(k):
@@ -380,7 +418,7 @@ class PartitionedMaxK:
         recv = self._buf(("recv", k), (p.num_halo, 5 * k), torch.uint8)
         work = a2a(recv, self._pack(data_own, sel_own), p.recv_counts, p.send_counts,
                    async_op=True)
-        y = self.local_own.forward(data_own, sel_own, dim_origin)   # overlaps the exchange
+        y = _train_fwd(self.local_own, data_own, sel_own, dim_origin)   # overlaps the exchange
         work.wait()
         # the halo block reads the received records in place and adds onto y
         self.local_halo.forward_records(recv, k, dim_origin, out=y, accumulate=True)
@@ -407,7 +445,7 @@ class PartitionedMaxK:
             mine[: p.num_own, 4 * k:] = sel_own
         table = self._buf(("ag_table", k), (self.world * max_own, 5 * k), torch.uint8)
         work = ag(table, mine, async_op=True)
-        y = self.local_own.forward(data_own, sel_own, dim_origin)   # overlaps the all-gather
+        y = _train_fwd(self.local_own, data_own, sel_own, dim_origin)   # overlaps the all-gather
         work.wait()
         eng.forward_records(table, k, dim_origin, out=y, accumulate=True)
         self._fwd_sel = sel_own
@@ -434,13 +472,60 @@ class PartitionedMaxK:
                 "allgather_fwd": (self.world - 1) * max_own * 5 * k,
                 "reverse_bwd": p.num_halo * 4 * k}
 
+    def exchange_ms(self, k: int, reps: int = 10) -> dict:
+        """Wire time of this rank's exchanges, each run alone (not overlapped) with
+        the step's message sizes: the forward's all-to-all-v of halo records (or
+        the all-gather of the CBSR table in that mode) and the backward's reverse
+        all-to-all-v of partial sums.  HIP events on the current stream around
+        synchronous collectives (the current stream waits for RCCL's), mean of
+        `reps` after one warm-up.  Every rank must call it (same order)."""
+        p = self.plan
+        dev = self.device
+
+        def ev_ms(fn):
+            fn()
+            if dev.type != "cuda":
+                import time
+                t0 = time.perf_counter()
+                for _ in range(reps):
+                    fn()
+                return (time.perf_counter() - t0) / reps * 1e3
+            st = torch.cuda.current_stream(dev)
+            a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            a.record(st)
+            for _ in range(reps):
+                fn()
+            b.record(st)
+            b.synchronize()
+            return a.elapsed_time(b) / reps
+
+        out = {}
+        if self._allgather_ok(k):
+            max_own = max(self.bounds[i + 1] - self.bounds[i] for i in range(self.world))
+            mine = torch.zeros((max_own, 5 * k), dtype=torch.uint8, device=dev)
+            table = torch.empty((self.world * max_own, 5 * k), dtype=torch.uint8, device=dev)
+            out["fwd_allgather_ms"] = ev_ms(lambda: ag(table, mine))
+            out["fwd_bytes_in"] = (self.world - 1) * max_own * 5 * k
+            del mine, table
+        else:
+            send = torch.zeros((self.send_rows.numel(), 5 * k), dtype=torch.uint8, device=dev)
+            recv = torch.empty((p.num_halo, 5 * k), dtype=torch.uint8, device=dev)
+            out["fwd_a2a_ms"] = ev_ms(lambda: a2a(recv, send, p.recv_counts, p.send_counts))
+            out["fwd_bytes_in"] = p.num_halo * 5 * k
+            del send, recv
+        dh = torch.zeros((p.num_halo, k), dtype=torch.float32, device=dev)
+        back = torch.empty((sum(p.send_counts), k), dtype=torch.float32, device=dev)
+        out["bwd_a2a_ms"] = ev_ms(lambda: a2a(back, dh, p.send_counts, p.recv_counts))
+        out["bwd_bytes_out"] = p.num_halo * 4 * k
+        return out
+
     def _forward_overlap_rows(self, data_own, sel_own, dim_origin):
         p = self.plan
         k = data_own.shape[1]
         recv = torch.empty((p.num_halo, 5 * k), dtype=torch.uint8, device=self.device)
         work = a2a(recv, self._pack(data_own, sel_own), p.recv_counts, p.send_counts,
                    async_op=True)
-        y = self.local_own.forward(data_own, sel_own, dim_origin)   # overlaps the exchange
+        y = _train_fwd(self.local_own, data_own, sel_own, dim_origin)   # overlaps the exchange
         work.wait()
         h_data, h_sel = self._unpack(recv, k)
         h_sel = h_sel.contiguous()
@@ -505,7 +590,13 @@ class PartitionedMaxK:
         when sel_own is its tensor (or None), else exchanged again.  With
         overlap_backward the halo columns go first and their partial sums
         travel while the own columns are computed."""
-        sel = self._block_sel(sel_own, halo_sel)
+        last = halo_sel is None and (sel_own is None or sel_own is self._fwd_sel)
+        if last and not self.overlap and self._fwd_block_sel is not None:
+            # the single-block forward's own selector tensor (own + halo rows as it
+            # read them): the engine finds the edge selectors that forward wrote
+            sel = self._fwd_block_sel
+        else:
+            sel = self._block_sel(sel_own, halo_sel)
         if not self.overlap_backward:
             return self._return_halo(self._local_bwd(self.local, grad_own, sel))
         p = self.plan
@@ -513,7 +604,9 @@ class PartitionedMaxK:
         dh = self._local_bwd(self.local_halo, grad_own, sel[p.num_own:])
         back = self._buf(("back", k), (sum(p.send_counts), k), torch.float32)
         work = a2a(back, dh, p.send_counts, p.recv_counts, async_op=True)
-        own = self._local_bwd(self.local_own, grad_own, sel[: p.num_own])   # overlaps the exchange
+        # the own part: the forward's selector tensor itself when it is the last one
+        own_sel = self._fwd_sel if last else sel[: p.num_own]
+        own = self._local_bwd(self.local_own, grad_own, own_sel)   # overlaps the exchange
         work.wait()
         return self._add_returns(back, own)
 

@@ -1035,9 +1035,11 @@ def _fwd_blocks(g: MaxKGraph, data, sel, dim_origin: int, out, values) -> int:
         return 0
     if AUTO_MODE == "fixed":
         # the measured best on Reddit at k = 32 and 64, when its partial
-        # outputs fit comfortably
-        free, _ = torch.cuda.mem_get_info(g.device)
-        nb = 4 if 4 * 4 * g.num_rows * dim_origin + 16 * g.num_edges <= free // 4 else 0
+        # outputs fit comfortably.  A rule of the shape and the device's TOTAL memory
+        # only, so the choice (and the fp32 summation order with it) does not depend
+        # on how much memory happens to be free at the first call
+        total = torch.cuda.get_device_properties(g.device).total_memory
+        nb = 4 if 4 * 4 * g.num_rows * dim_origin + 16 * g.num_edges <= total // 8 else 0
         g._fwd_blocks[key] = nb
         return nb
     if torch.cuda.is_current_stream_capturing():
@@ -1157,7 +1159,7 @@ def spgemm_forward_multi(g: MaxKGraph, data, sel, values, dim_origin: int = 256,
         od = g._workspace(("bank_data", k), g.num_cols * k * 4).view(torch.float32)
         os_ = g._workspace(("bank_sel", k), g.num_cols * k)
         od, os_ = od[: g.num_cols * k].view(g.num_cols, k), os_[: g.num_cols * k].view(g.num_cols, k)
-        _lib.check(L.maxk_cbsr_bank_order(data.data_ptr(), sel.data_ptr(), g.num_cols, k,
+        _lib.check(L.maxk_cbsr_bank_order(data.data_ptr(), sel.data_ptr(), g.num_cols, k, R,
                                           od.data_ptr(), os_.data_ptr(), _stream(out)),
                    "maxk_cbsr_bank_order")
         data, sel = od, os_

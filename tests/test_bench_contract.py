@@ -74,3 +74,34 @@ def test_bench_two_ranks_multi_relation_rehearsal():
     d = json.loads(out.stdout.strip().splitlines()[-1])
     assert d["n_gpus"] == 2 and d["config"]["parallelism"] == "rowpart2"
     assert d["config"]["relations"] == 8 and d["value"] > 0 and d["bwd_multi_ms"] > 0
+
+
+@pytest.mark.gpu
+def test_bench_launches_its_own_ranks():
+    """`python bench.py --gpus 2` with no outside launcher: the
+    parent makes no GPU call, starts 2 ranks itself (gloo stands in for RCCL, both
+    ranks on the one GPU) and relays rank 0's line, which reports n_gpus 2, the
+    row partition and the per-exchange wire times."""
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK",
+                                                            "MASTER_PORT")}
+    env["BENCH_BACKEND"] = "gloo"
+    cmd = [sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--steps", "2",
+           "--warmup", "1", "--graph", "flickr", "--h", "64", "--k", "16"]
+    out = subprocess.run(cmd, cwd=ROOT, capture_output=True, text=True, timeout=600, env=env)
+    assert out.returncode == 0, out.stderr[-3000:]
+    lines = out.stdout.strip().splitlines()
+    assert len(lines) == 1
+    d = json.loads(lines[0])
+    assert d["n_gpus"] == 2 and d["config"]["parallelism"] == "rowpart2"
+    ex = d["exchange_ms_max_over_ranks"]
+    assert ex["bwd_a2a_ms"] > 0 and ("fwd_a2a_ms" in ex or "fwd_allgather_ms" in ex)
+
+
+@pytest.mark.gpu
+def test_bench_more_gpus_than_visible_fails():
+    """--gpus 9 on a one-GPU box (RCCL: one GPU per rank) exits non-zero, prints no line."""
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK",
+                                                            "BENCH_BACKEND")}
+    out = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "9"],
+                         cwd=ROOT, capture_output=True, text=True, timeout=300, env=env)
+    assert out.returncode != 0 and out.stdout.strip() == ""

@@ -82,3 +82,54 @@ def test_workload_key():
 def test_median():
     assert bench._median([3.0, 1.0, 2.0]) == 2.0
     assert bench._median([4.0, 1.0, 2.0, 3.0]) == 2.5
+
+
+def test_gpus_beyond_visible_devices_fails_loudly():
+    """`bench.py --gpus N` without a launcher starts its own ranks; when N exceeds
+    the visible GPUs (none in this container) it exits non-zero before any GPU
+    call instead of measuring one GPU and reporting it as N."""
+    import subprocess
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
+    out = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "9"],
+                         cwd=ROOT, capture_output=True, text=True, timeout=300, env=env)
+    assert out.returncode != 0
+    assert out.stdout.strip() == ""
+    assert "refusing" in out.stderr or "no GPU" in out.stderr
+
+
+def test_world_size_mismatch_fails_loudly():
+    """A launcher that started another number of ranks than --gpus names: refused."""
+    import subprocess
+    env = dict(os.environ, WORLD_SIZE="2", RANK="0", LOCAL_RANK="0")
+    out = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "4"],
+                         cwd=ROOT, capture_output=True, text=True, timeout=300, env=env)
+    assert out.returncode == 6 and out.stdout.strip() == ""
+
+
+def test_vendor_backward_reference_matches_oracle():
+    """bench.vendor_backward_reference (the full-size backward check: A^T by torch,
+    torch.sparse.mm, gathered at sel) equals the fp64 oracle on a small graph
+    (CPU torch here; rocSPARSE on the GPU), also for a row block (indptr[0] != 0
+    views are not used; a rectangular block with more columns than rows is)."""
+    import numpy as np
+    import torch
+    from oracle import oracle as O
+    from spgemm_new_amd.graphs import random_cbsr, small_csr
+    indptr, indices = small_csr(700, seed=3)
+    v, h, k = len(indptr) - 1, 64, 8
+    values = np.random.default_rng(1).random(len(indices), dtype=np.float32)
+    grad = np.random.default_rng(2).random((v, h), dtype=np.float32)
+    _, sel = random_cbsr(v, k, h, seed=4)
+    ref = bench.vendor_backward_reference(torch.from_numpy(indptr), torch.from_numpy(indices),
+                                          torch.from_numpy(values), torch.from_numpy(grad),
+                                          torch.from_numpy(sel))
+    want = O.np_backward(indptr, indices, values, grad, sel)
+    assert O.parity_error(ref.numpy(), want) <= 1e-4
+    # rectangular: the first 300 rows, all 700 columns
+    r = 300
+    ip = indptr[: r + 1]
+    ref = bench.vendor_backward_reference(torch.from_numpy(ip), torch.from_numpy(indices),
+                                          torch.from_numpy(values), torch.from_numpy(grad[:r]),
+                                          torch.from_numpy(sel), num_cols=v)
+    want = O.np_backward(ip, indices[: ip[-1]], values[: ip[-1]], grad[:r], sel)
+    assert O.parity_error(ref.numpy(), want) <= 1e-4

@@ -563,6 +563,97 @@ def test_allgather_halo_mode_bitwise_equals_records(world):
         assert nbytes["allgather_fwd"] >= nbytes["records_fwd"] > 0
 
 
+def _mixed_worker(rank, world, port, q, isolated):
+    """Ranks with different halo sizes (and, with `isolated`, rank 0 without any
+    halo) under overlap="auto" + halo_mode "allgather"/"auto": the choices must be
+    the same on every rank, the collectives must match (no hang) and the result
+    must equal the oracle."""
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        import spgemm_new_amd.distributed as Dm
+        from spgemm_new_amd.distributed import PartitionedMaxK, row_partition
+        indptr, indices = small_csr(900, seed=4)
+        v, h, k = len(indptr) - 1, 64, 8
+        if isolated:
+            # rank 0's rows reference only rank 0's own columns: its halo is empty
+            b = row_partition(torch.from_numpy(indptr), world)
+            rng = np.random.default_rng(11)
+            indices = indices.copy()
+            for r in range(b[0], b[1]):
+                e0, e1 = indptr[r], indptr[r + 1]
+                indices[e0:e1] = np.sort(rng.integers(b[0], b[1], e1 - e0))
+        values = np.random.default_rng(1).random(len(indices), dtype=np.float32)
+        data, sel = random_cbsr(v, k, h, seed=2)
+        grad = np.random.default_rng(3).random((v, h), dtype=np.float32)
+        args = (torch.from_numpy(indptr), torch.from_numpy(indices), torch.from_numpy(values),
+                rank, world, "cpu")
+        probe = PartitionedMaxK(*args, engine=OracleEngine, overlap=False, halo_mode="records")
+        halos = [None] * world
+        dist.all_gather_object(halos, probe.plan.num_halo)
+        saved = Dm.OVERLAP_MIN_HALO_BYTES
+        # between the smallest and the largest rank's halo records
+        Dm.OVERLAP_MIN_HALO_BYTES = (min(halos) + max(halos)) // 2 * Dm.OVERLAP_BYTES_PER_HALO_NODE
+        try:
+            res = []
+            for mode in ("allgather", "auto"):
+                m = PartitionedMaxK(*args, engine=OracleEngine, overlap="auto", halo_mode=mode)
+                d_l = m.local_rows(torch.from_numpy(data))
+                s_l = m.local_rows(torch.from_numpy(sel))
+                y = m.forward(d_l, s_l, h)
+                dx = m.backward(m.local_rows(torch.from_numpy(grad)), s_l)
+                res.append((y.numpy(), dx.numpy(), m.overlap, m.halo_mode, m.plan.num_halo))
+        finally:
+            Dm.OVERLAP_MIN_HALO_BYTES = saved
+        allres = [None] * world
+        dist.all_gather_object(allres, res)
+        if rank == 0:
+            from oracle import oracle as O
+            yr = O.np_forward(indptr, indices, values, data, sel, h)
+            dr = O.np_backward(indptr, indices, values, grad, sel)
+            errs = []
+            for i in range(2):
+                errs.append((O.parity_error(np.concatenate([a[i][0] for a in allres]), yr),
+                             O.parity_error(np.concatenate([a[i][1] for a in allres]), dr)))
+            q.put((errs, [[(r[2], r[3], r[4]) for r in a] for a in allres], halos))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world,isolated", [(3, False), (3, True), (4, True)])
+def test_overlap_and_halo_mode_decided_collectively(world, isolated):
+    """OVERLAP_MIN_HALO_BYTES between two ranks' halo sizes, halo_mode "allgather"
+    and "auto": every rank takes the same split decision (on the largest halo)
+    and the same collective; a rank with no halo at all (isolated) cannot be
+    split, so the all-gather mode falls back to records on every rank."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_mixed_worker, args=(r, world, port, q, isolated))
+             for r in range(world)]
+    for p in procs:
+        p.start()
+    for p in procs:
+        p.join(timeout=240)
+    assert all(p.exitcode == 0 for p in procs), [p.exitcode for p in procs]
+    errs, flags, halos = q.get(timeout=5)
+    assert all(ey <= 1e-4 and ed <= 1e-4 for ey, ed in errs), errs
+    if isolated:
+        assert halos[0] == 0 and max(halos) > 0
+    else:
+        assert min(halos) < max(halos)
+    for i in range(2):
+        modes = {r[i][1] for r in flags}
+        assert len(modes) == 1, flags              # one collective on every rank
+        # the split decision is the same wherever a rank has a halo to split off
+        assert len({r[i][0] for r in flags if r[i][2] > 0}) == 1, flags
+        if isolated:
+            assert modes == {"records"}, flags
+    if not isolated:
+        assert flags[0][0][1] == "allgather"
+
+
 @pytest.mark.gpu
 @pytest.mark.parametrize("k", [4, 8, 16, 32, 64])
 def test_records_sel_gather(k):

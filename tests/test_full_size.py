@@ -6,9 +6,13 @@ reference on the same device:
 
 * forward vs rocSPARSE SpMM (torch.sparse.mm on the densified masked input),
   per element |got - ref| / max(1, |ref|) <= 1e-4;
-* backward via the exact adjoint identity <A . X^, G> = <X^_s, dXs> (both
-  sides summed in fp64), every backward algorithm (ATOMIC, STAGED, LOCAL, TILE)
-  agreeing with STAGED within 1e-4, bit-exact linearity of the deterministic
+* backward per element against an independent reference, (A^T . G) gathered
+  at sel with rocSPARSE fp32 SpMM (bench.vendor_backward_reference: A^T built
+  by torch, no code of this repository), every algorithm within 1e-4 --
+  TILE with the bench's 2-range plan included; plus the exact adjoint identity
+  <A . X^, G> = <X^_s, dXs> (both sides summed in fp64), every backward
+  algorithm (ATOMIC, STAGED, LOCAL, TILE, ...) agreeing with STAGED within 1e-4,
+  bit-exact linearity of the deterministic
   LOCAL path (dXs(2G) == 2 dXs(G)), TILE run-to-run identical and equal to
   LOCAL bit for bit where its plan has one source range (Reddit k = 64);
 * config 5 (proteins, R = 8): fused forward vs 8 single calls, the
@@ -21,6 +25,7 @@ import pytest
 import torch
 
 import spgemm_new_amd as S
+from bench import vendor_backward_reference
 from spgemm_new_amd import _lib
 from spgemm_new_amd.graphs import CONFIGS, synthetic_csr_gpu
 
@@ -68,12 +73,15 @@ def test_full_size_properties(dev, graph, k):
         assert tile_plan is not None   # the benched backward must be covered here
     lhs = float((y.double() * Gr.double()).sum())
     ref = g.backward(Gr, sel, algo=_lib.MAXK_BWD_STAGED)
+    vref = vendor_backward_reference(indptr, indices, values, Gr, sel)
+    assert _rel(ref, vref) <= TOL
     outs = {}
     for a_ in algos:
         dx = g.backward(Gr, sel, algo=a_)
         rhs = float((data.double() * dx.double()).sum())
         assert abs(lhs - rhs) / abs(lhs) <= 1e-6, (a_, lhs, rhs)
         assert _rel(dx, ref) <= TOL, a_
+        assert _rel(dx, vref) <= TOL, a_          # independent per-element reference
         if a_ in (_lib.MAXK_BWD_LOCAL, _lib.MAXK_BWD_TILE):
             outs[a_] = dx
         else:
@@ -132,16 +140,24 @@ def test_full_size_proteins_multi_relation(dev):
     Gr = torch.rand((R, V, h), generator=gen, device=dev)
     lhs = float((y.double() * Gr.double()).sum())
     del y
+    # independent per-element reference: sum_q (A_q^T G_q) gathered at sel (rocSPARSE)
+    vref = None
+    for q in range(R):
+        rq = vendor_backward_reference(indptr, indices, vals[:, q].contiguous(), Gr[q], sel)
+        vref = rq if vref is None else vref.add_(rq)
+        del rq
     dx = g.backward_multi(Gr, sel, vals, algo=_lib.MAXK_BWD_LOCAL)
     assert g.last_bwd_algo == "local_rel8"
     rhs = float((data.double() * dx.double()).sum())
     assert abs(lhs - rhs) / abs(lhs) <= 1e-6
+    assert _rel(dx, vref) <= TOL
     comp = g.backward_multi(Gr, sel, vals, algo=_lib.MAXK_BWD_STAGED)
     assert _rel(dx, comp) <= TOL
     del comp
     for algo in (_lib.MAXK_BWD_MULTI_STAGED, _lib.MAXK_BWD_MULTI_EDGE_GATHER):
         dm = g.backward_multi(Gr, sel, vals, algo=algo)
         assert _rel(dx, dm) <= TOL, algo
+        assert _rel(dm, vref) <= TOL, algo
         rhs = float((data.double() * dm.double()).sum())
         assert abs(lhs - rhs) / abs(lhs) <= 1e-6, algo
         dm2 = g.backward_multi(Gr, sel, vals, algo=algo)

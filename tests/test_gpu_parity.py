@@ -833,6 +833,31 @@ def test_cbsr_bank_order(dev, k):
     with four columns per store class (k = 32) has conflict-free store groups."""
     v, h = 500, 256
     data, sel = random_cbsr(v, k, h, seed=k)
+    _bank_order_case(dev, k, v, data, sel)
+
+
+@pytest.mark.parametrize("R", [4, 12, 16])
+def test_cbsr_bank_order_odd_records(dev, R):
+    """R != 8 (odd 16-B quads per column record): the store classes are c mod 8, so
+    the first 8 entries of a row with a column of every residue are conflict-free
+    (the R = 8 swizzled classes were applied to every R)."""
+    v, k, h = 300, 32, 256
+    data, sel = random_cbsr(v, k, h, seed=R)
+    L = _lib.load()
+    od = torch.empty((v, k), device=dev)
+    os_ = torch.empty((v, k), dtype=torch.uint8, device=dev)
+    td, ts = T(data, dev), T(sel, dev)
+    _lib.check(L.maxk_cbsr_bank_order(td.data_ptr(), ts.data_ptr(), v, k, R, od.data_ptr(),
+                                      os_.data_ptr(), None), "bank_order")
+    torch.cuda.synchronize()
+    od, os_ = od.cpu().numpy(), os_.cpu().numpy()
+    for r in range(v):
+        assert sorted(zip(os_[r], od[r])) == sorted(zip(sel[r], data[r]))
+        present = len(set(int(c) & 7 for c in sel[r]))
+        assert len(set(int(c) & 7 for c in os_[r][:8])) == min(8, present)
+
+
+def _bank_order_case(dev, k, v, data, sel):
     if k == 32:   # a few rows balanced over the 8 store classes
         for r in range(0, 40):
             rng = np.random.default_rng(r)
@@ -842,7 +867,7 @@ def test_cbsr_bank_order(dev, k):
     od = torch.empty((v, k), device=dev)
     os_ = torch.empty((v, k), dtype=torch.uint8, device=dev)
     td, ts = T(data, dev), T(sel, dev)   # held: the call reads them asynchronously
-    _lib.check(L.maxk_cbsr_bank_order(td.data_ptr(), ts.data_ptr(), v, k, od.data_ptr(),
+    _lib.check(L.maxk_cbsr_bank_order(td.data_ptr(), ts.data_ptr(), v, k, 8, od.data_ptr(),
                                       os_.data_ptr(), None), "bank_order")
     torch.cuda.synchronize()
     od, os_ = od.cpu().numpy(), os_.cpu().numpy()

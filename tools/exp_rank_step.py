@@ -145,8 +145,15 @@ def main():
                   f"bwd {tb:.3f} step {ts:.3f} ms (no wire time) | halo fwd "
                   f"{pl.num_halo * 5 * k / 1e6:.1f} MB in, {m.send_rows.numel() * 5 * k / 1e6:.1f}"
                   f" MB out; bwd algo {m.local.last_bwd_algo}; halo mode {m.halo_mode}", flush=True)
-            for nm in ("local_own", "local_halo"):
+            for nm in ("local", "local_own", "local_halo"):
                 e = getattr(m, nm, None)
+                if e is not None and hasattr(e, "_tile"):
+                    tp = {kk: (None if v is None else (v["num_groups"], v["group_size"],
+                                                       v["splits"]))
+                          for kk, v in e._tile.items()}
+                    print(f"   {nm}: rows {e.num_rows} cols {e.num_cols} edges {e.num_edges} "
+                          f"tile plans {tp} bwd choice {e._bwd_choice} "
+                          f"cands {getattr(e, 'bwd_candidates', None)}", flush=True)
                 if e is not None:
                     print(f"   {nm}: bwd {getattr(e, 'last_bwd_algo', None)}, fwd blocks "
                           f"{getattr(e, '_fwd_blocks', {})}", flush=True)
@@ -154,6 +161,48 @@ def main():
             torch.cuda.empty_cache()
 
 
+
+
+def breakdown_single(graph="reddit", k=32, world=8, rank=0):
+    """Per-component times of one rank's single-block step (overlap off: the
+    bench's choice on Reddit), loopback exchange."""
+    dev = torch.device("cuda:0")
+    V, E = CONFIGS[graph]
+    h = 256
+    indptr, indices = synthetic_csr_gpu(V, E, device=dev)
+    gen = torch.Generator(device=dev)
+    gen.manual_seed(5)
+    values = torch.rand(E, generator=gen, device=dev)
+    X = torch.rand((V, h), generator=gen, device=dev)
+    G = torch.rand((V, h), generator=gen, device=dev)
+    data, sel = topk_cbsr(X, k)
+    bounds = D.row_partition(indptr, world)
+    lb = Loopback(indptr, indices, bounds, rank, data, sel)
+    D.a2a = lb
+    m = D.PartitionedMaxK(indptr, indices, values, rank, world, dev, halo_mode="records",
+                          overlap=False)
+    d_l, s_l, g_l = m.local_rows(data), m.local_rows(sel), m.local_rows(G)
+    m.forward(d_l, s_l, h)
+    m.backward(g_l, s_l)
+    p = m.plan
+    dall, sall = m.gather_halo_cbsr(d_l, s_l)
+    dx = m.local.backward(g_l, sall)
+    rows = {
+        "pack": lambda: m._pack(d_l, s_l),
+        "gather_halo_cbsr (pack+exchange+copies)": lambda: m.gather_halo_cbsr(d_l, s_l),
+        "local forward": lambda: m.local.forward(dall, sall, h),
+        "local backward": lambda: m.local.backward(g_l, sall),
+        "return halo (exchange + add)": lambda: m._return_halo(dx),
+        "whole forward": lambda: m.forward(d_l, s_l, h),
+        "whole backward": lambda: m.backward(g_l, s_l),
+        "whole step": lambda: (m.forward(d_l, s_l, h), m.backward(g_l, s_l)),
+    }
+    e = m.local
+    print(f"{graph} k={k} world={world} rank={rank} single block: own={p.num_own} "
+          f"halo={p.num_halo} edges={e.num_edges} bwd {e.last_bwd_algo} fwd blocks "
+          f"{e._fwd_blocks} tile {[(kk, None if v is None else (v['num_groups'], v['group_size'], v['splits'])) for kk, v in e._tile.items()]}")
+    for name, fn in rows.items():
+        print(f"  {name:40s} {timed(fn, reps=20):.3f} ms", flush=True)
 
 
 def breakdown(graph="products", k=32, world=8, rank=0):
@@ -206,5 +255,8 @@ def breakdown(graph="products", k=32, world=8, rank=0):
 if __name__ == "__main__":
     if len(sys.argv) > 1 and sys.argv[1] == "breakdown":
         breakdown(*(sys.argv[2:3] or ["products"]))
+    elif len(sys.argv) > 1 and sys.argv[1] == "single":
+        for w in [int(x) for x in (sys.argv[3] if len(sys.argv) > 3 else "2,4,8").split(",")]:
+            breakdown_single(sys.argv[2] if len(sys.argv) > 2 else "reddit", 32, w, 0)
     else:
         main()
