@@ -624,6 +624,7 @@ def config_sweep(args, dev, only=None):
         fw, bw = _timed_calls([lambda: g.forward_multi(data, sel, vals, h, out=y),
                                lambda: g.backward_multi(G, sel, vals, out=dx)], steps, warmup)
         torch.cuda.synchronize()
+        algo_b = g.last_bwd_algo
         y0 = g.forward(data, sel, h, values=vals[:, 0].contiguous())
         fwd_err = float(((y[0] - y0).abs() / y0.abs().clamp_min(1)).max())
         lhs = float((y.double() * G.double()).sum())
@@ -643,6 +644,23 @@ def config_sweep(args, dev, only=None):
             del rq, vq
         bwd_vendor = float(((dx - ref).abs() / ref.abs().clamp_min(1)).max())
         del xm, ref
+        # every candidate form, timed the same way (min of 3 after one call): the
+        # forward's two kernels and the backward's fused forms + the composed one
+        from spgemm_new_amd.ops import _min_ms, multi_gather_ok
+        cand_f = {"lds": round(_min_ms(lambda: g.forward_multi(data, sel, vals, h, out=y,
+                                                               form="lds")), 4)}
+        if multi_gather_ok(R, k, h):
+            cand_f["gather"] = round(_min_ms(lambda: g.forward_multi(data, sel, vals, h, out=y,
+                                                                     form="gather")), 4)
+        cand_b = {}
+        for nm, a in (("multi_staged", _lib.MAXK_BWD_MULTI_STAGED),
+                      ("multi_edge_gather", _lib.MAXK_BWD_MULTI_EDGE_GATHER),
+                      ("local_rel8", _lib.MAXK_BWD_LOCAL)):
+            cand_b[nm] = round(_min_ms(lambda: g.backward_multi(G, sel, vals, out=dx, algo=a)), 4)
+        cand_b["composed"] = round(_min_ms(lambda: g._backward_composed(G, sel, vals, dx,
+                                                                        _lib.MAXK_BWD_AUTO)), 4)
+        g.forward_multi(data, sel, vals, h, out=y)
+        g.backward_multi(G, sel, vals, out=dx)
         b = E * (4 + 4 * R + 5 * k) + R * 4 * h * V
         fs, bs = _ms_stats(fw), _ms_stats(bw)
         out["proteins_r8"] = {
@@ -652,7 +670,9 @@ def config_sweep(args, dev, only=None):
             "bytes_formula": "E*(4 + 4R + 5k) + R*4hV (SURVEY.md §8d, fused)",
             "fwd_frac": round(b / (fs["mean"] / 1e3) / 1e9 / HBM_PEAK_GBS, 4),
             "bwd_frac": round(b / (bs["mean"] / 1e3) / 1e9 / HBM_PEAK_GBS, 4),
-            "bwd_algo": g.last_bwd_algo,
+            "bwd_algo": algo_b,
+            "fwd_form": "gather" if multi_gather_ok(R, k, h) and S.ops.MULTI_GATHER else "lds",
+            "fwd_candidates_ms": cand_f, "bwd_candidates_ms": cand_b,
             "check": {"fwd_rel0_vs_single_max_rel_diff": fwd_err,
                       "fwd_vs_rocsparse_max_rel_diff": fwd_vendor,
                       "bwd_vs_rocsparse_max_rel_diff": bwd_vendor,

@@ -265,6 +265,23 @@ int maxk_spgemm_forward_multi(const int32_t *sched, int64_t num_panels, const in
                               const float *cbsr_data, const uint8_t *cbsr_sel, int num_rows,
                               int dim_origin, int dim_k, float *out, void *workspace,
                               size_t workspace_bytes, void *stream);
+/* Register-accumulator form of the fused forward for num_rel = 8, dim_origin =
+ * 256, dim_k in {4, 8, 16, 32} (the proteins shape): each destination row's 8 x
+ * 256 sums stay in registers and an edge's CBSR values reach them by a gather
+ * over the source's column bitmask.  Needs the CBSR in the form
+ * maxk_cbsr_colmask writes: sorted_data fp32[V, k] (each row's values in
+ * ascending column order) and mask_rec uint32[V, 16] (per 32-column word: the
+ * bitmask of selected columns, then the number selected below it; 8-B aligned).
+ * Same result as maxk_spgemm_forward_multi, bit for bit (same FMAs in the same
+ * edge order), same schedule and workspace size. */
+int maxk_cbsr_colmask(const float *cbsr_data, const uint8_t *cbsr_sel, int num_rows, int dim_k,
+                      float *sorted_data, uint32_t *mask_rec, void *stream);
+int maxk_spgemm_forward_multi_gather(const int32_t *sched, int64_t num_panels,
+                                     const int32_t *indptr, const int32_t *indices,
+                                     const float *values, int num_rel, const float *sorted_data,
+                                     const uint32_t *mask_rec, int num_rows, int dim_origin,
+                                     int dim_k, float *out, void *workspace,
+                                     size_t workspace_bytes, void *stream);
 
 /* ---------------------------------------------------------------------------
  * Backward SSpMM  dXs[c,l] = sum_{e: idx[e]=c} val[e] * G[row(e), sel[c,l]]

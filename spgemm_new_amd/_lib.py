@@ -102,6 +102,9 @@ SIGNATURES = {
     "maxk_spmm_dense_forward": (_I, [_P, _L, _P, _P, _P, _P, _I, _I, _P, _P, _S, _P]),
     "maxk_forward_multi_workspace_bytes": (_S, [_L, _I, _I]),
     "maxk_spgemm_forward_multi": (_I, [_P, _L, _P, _P, _P, _I, _P, _P, _I, _I, _I, _P, _P, _S, _P]),
+    "maxk_cbsr_colmask": (_I, [_P, _P, _I, _I, _P, _P, _P]),
+    "maxk_spgemm_forward_multi_gather": (_I, [_P, _L, _P, _P, _P, _I, _P, _P, _I, _I, _I, _P, _P,
+                                              _S, _P]),
     "maxk_records_sel_gather": (_I, [_P, _I, _P, _L, _P, _P]),
     "maxk_cbsr_gather_records": (_I, [_P, _P, _P, _L, _I, _P, _P]),
     "maxk_spgemm_forward_records": (_I, [_P, _L, _P, _P, _P, _P, _I, _I, _I, _I, _P, _P, _S, _P]),

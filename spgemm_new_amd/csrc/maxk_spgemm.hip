@@ -994,6 +994,205 @@ __global__ __launch_bounds__(kBlock) void fwd_rel4_panel_kernel(
     }
 }
 
+// ---------------------------------------------------------------------------
+// Register-accumulator form of the fused R = 8 forward (h = 256, k <= 32):
+// the destination row's 8 x 256 sums live in registers, lane l owning columns
+// 4l .. 4l+3 of every relation (8 x f4 = 32 VGPRs), so the per-edge LDS
+// read-modify-write of the relation-vector kernel (ds_read_b128 + ds_write_b128,
+// 17 LDS cycles per edge plus bank conflicts) goes away.  An edge reaches a
+// lane's columns as a GATHER, not a scatter: the source's CBSR row is kept
+// column-sorted (cbsr_colmask_kernel), with a 256-bit column bitmask and the
+// number of selected columns below each 32-column word; lane l tests its four
+// bits, their ranks in the row are base + popcount of the lower bits, and
+// ds_bpermute fetches the values from the lanes holding the (sorted) CBSR row;
+// a column the source did not select reads a lane of the zero half.  Then
+// 2 x 8 v_pk_fma_f32 with the edge's 8 values (wave-uniform, scalar loads).
+// Per element the FMAs happen in edge order with the same operands as the
+// relation-vector kernel (fma(x, v_q, acc); an unselected column adds 0 * v_q),
+// so the two kernels give the same bits.
+// ---------------------------------------------------------------------------
+typedef float f2 __attribute__((ext_vector_type(2)));
+
+// Column-sorted CBSR + column bitmask records: one wave per row; entry j's rank
+// = the number of the row's distinct columns below it; duplicate columns (not a
+// valid CBSR, handled anyway) are summed in entry order into one rank.  mrec[r*8 + w]
+// = {bits of columns 32w .. 32w+31, selected columns below 32w}.
+template <int K>
+__global__ __launch_bounds__(kBlock) void cbsr_colmask_kernel(const float *__restrict__ data,
+                                                              const uint8_t *__restrict__ sel,
+                                                              int num_rows,
+                                                              float *__restrict__ sdata,
+                                                              uint2 *__restrict__ mrec)
+{
+    const int lane = lane_id();
+    const int64_t nwaves = (int64_t)gridDim.x * kWavesPerBlock;
+    for (int64_t r = (int64_t)blockIdx.x * kWavesPerBlock + threadIdx.x / kWave; r < num_rows;
+         r += nwaves) {
+        const bool on = lane < K;
+        const int c = on ? (int)sel[r * K + lane] : 1024;
+        const float d = on ? data[r * K + lane] : 0.f;
+        int rank = 0;
+        float dsum = 0.f;
+        bool first = on;
+#pragma unroll
+        for (int i = 0; i < K; ++i) {
+            const int ci = __shfl(c, i);
+            const float di = __shfl(d, i);
+            rank += ci < c;
+            if (ci == c) {
+                dsum += di;
+                if (i < lane) first = false;
+            }
+        }
+        if (first) sdata[r * K + rank] = dsum;
+        const int myw = c >> 5;
+        uint32_t mw = 0, pw = 0;
+#pragma unroll
+        for (int w = 0; w < 8; ++w) {
+            uint32_t b = (on && myw == w) ? (1u << (c & 31)) : 0u;
+            b |= __shfl_xor(b, 1);
+            b |= __shfl_xor(b, 2);
+            b |= __shfl_xor(b, 4);
+            b |= __shfl_xor(b, 8);
+            b |= __shfl_xor(b, 16);
+            b |= __shfl_xor(b, 32);
+            const uint32_t below = (uint32_t)__builtin_popcountll(__ballot(first && myw < w));
+            if (lane == w) {
+                mw = b;
+                pw = below;
+            }
+        }
+        if (lane < 8) mrec[r * 8 + lane] = make_uint2(mw, pw);
+    }
+}
+
+// One round of U edges of a destination row (FULL: all U exist).  Per edge:
+// the bitmask word of the lane's columns and the rank base (one 8-B load per
+// lane from the source's 64-B record), the source's sorted CBSR row in lanes
+// 0 .. K-1 (lanes K .. 63 hold zeros), the 8 values by scalar loads.
+template <int K, int U, bool FULL>
+__device__ __forceinline__ void rel8g_round(int my_c, int ebase, int s0, int n,
+                                            const float *__restrict__ val,
+                                            const float *__restrict__ sdata,
+                                            const uint2 *__restrict__ mrec, f2 (&a)[8][2])
+{
+    const int lane = lane_id();
+    const int wd = lane >> 3;
+    const uint32_t sh = (uint32_t)(lane & 7) * 4u;
+    const uint32_t low = (1u << sh) - 1u;
+    uint2 mr[U];
+    float dv[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+        if (!FULL && s0 + u >= n) break;
+        const int c = __builtin_amdgcn_readlane(my_c, s0 + u);
+        const uint2 *mp = mrec + (size_t)c * 8;      // wave-uniform row pointers
+        const float *dp = sdata + (size_t)c * K;
+        mr[u] = mp[wd];
+        const float x = dp[lane & (K - 1)];
+        dv[u] = lane < K ? x : 0.f;
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+        if (!FULL && s0 + u >= n) break;
+        // the edge's 8 values: a uniform address, so scalar loads and SGPR operands
+        const int eu = __builtin_amdgcn_readfirstlane(ebase + s0 + u);
+        const float *vr = val + (size_t)eu * 8;
+        const uint32_t nib = (mr[u].x >> sh) & 15u;
+        const uint32_t base = (uint32_t)__builtin_popcount(mr[u].x & low) + mr[u].y;
+        // rank of column 4l + i among the source's selected columns (x4: a byte
+        // address for ds_bpermute), or lane 63 (a zero) when column 4l + i is not
+        // selected: bfi(-hit, rank * 4, 252)
+        uint32_t ad[4];
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            const uint32_t p = (uint32_t)__builtin_popcount(nib & ((1u << i) - 1u)) + base;
+            const uint32_t hit = (uint32_t)(((int32_t)(nib << (31 - i))) >> 31);
+            ad[i] = ((p << 2) & hit) | (((uint32_t)(kWave - 1) << 2) & ~hit);
+        }
+        const int xb = __float_as_int(dv[u]);
+        f2 x01, x23;
+        x01.x = __int_as_float(__builtin_amdgcn_ds_bpermute((int)ad[0], xb));
+        x01.y = __int_as_float(__builtin_amdgcn_ds_bpermute((int)ad[1], xb));
+        x23.x = __int_as_float(__builtin_amdgcn_ds_bpermute((int)ad[2], xb));
+        x23.y = __int_as_float(__builtin_amdgcn_ds_bpermute((int)ad[3], xb));
+#pragma unroll
+        for (int q = 0; q < 8; ++q) {
+            const float v = vr[q];
+            const f2 vv = {v, v};
+            a[q][0] = __builtin_elementwise_fma(x01, vv, a[q][0]);
+            a[q][1] = __builtin_elementwise_fma(x23, vv, a[q][1]);
+        }
+    }
+}
+
+template <int K>
+__device__ __forceinline__ void rel8g_edges(int e0, int e1, const int32_t *__restrict__ idx,
+                                            const float *__restrict__ val,
+                                            const float *__restrict__ sdata,
+                                            const uint2 *__restrict__ mrec, f2 (&a)[8][2])
+{
+    constexpr int U = 8;
+    const int lane = lane_id();
+    for (int base = e0; base < e1; base += kWave) {
+        const int n = __builtin_amdgcn_readfirstlane((e1 - base) < kWave ? (e1 - base) : kWave);
+        const int my_c = lane < n ? __builtin_nontemporal_load(idx + base + lane) : 0;
+        int s0 = 0;
+        for (; s0 + U <= n; s0 += U) rel8g_round<K, U, true>(my_c, base, s0, n, val, sdata, mrec, a);
+        if (s0 < n) rel8g_round<K, U, false>(my_c, base, s0, n, val, sdata, mrec, a);
+    }
+}
+
+__device__ __forceinline__ void rel8g_store(f2 (&a)[8][2], float *__restrict__ dst, size_t rel_stride)
+{
+    const int lane = lane_id();
+#pragma unroll
+    for (int q = 0; q < 8; ++q) {
+        const f4 s = {a[q][0].x, a[q][0].y, a[q][1].x, a[q][1].y};
+        *reinterpret_cast<f4 *>(dst + q * rel_stride + 4 * lane) = s;
+        a[q][0] = f2{0.f, 0.f};
+        a[q][1] = f2{0.f, 0.f};
+    }
+}
+
+template <int K>
+__global__ __launch_bounds__(kBlock) void fwd_rel8_gather_kernel(
+    const int2 *__restrict__ sched, int64_t num_panels, const int32_t *__restrict__ indptr,
+    const int32_t *__restrict__ idx, const float *__restrict__ val,
+    const float *__restrict__ sdata, const uint2 *__restrict__ mrec, int num_rows,
+    float *__restrict__ out, float *__restrict__ carry, int32_t *__restrict__ carry_row)
+{
+    const int64_t w = (int64_t)blockIdx.x * kWavesPerBlock + threadIdx.x / kWave;
+    if (w >= num_panels) return;
+    f2 a[8][2];
+#pragma unroll
+    for (int q = 0; q < 8; ++q) a[q][0] = a[q][1] = f2{0.f, 0.f};
+    const size_t rs = (size_t)num_rows * kMaxDim;
+    const int2 s0 = sched[w], s1 = sched[w + 1];
+    const int i0 = s0.x, j0 = s0.y, i1 = s1.x, j1 = s1.y;
+    int e = j0;
+    for (int r = i0; r < i1; ++r) {
+        const int re = indptr[r + 1];
+        if (e < re) rel8g_edges<K>(e, re, idx, val, sdata, mrec, a);
+        rel8g_store(a, out + (size_t)r * kMaxDim, rs);
+        e = re;
+    }
+    int has_carry = 0;
+    if (i1 < num_rows) {
+        const int eb = e > indptr[i1] ? e : indptr[i1];
+        if (eb < j1) {
+            rel8g_edges<K>(eb, j1, idx, val, sdata, mrec, a);
+            has_carry = 1;
+        }
+    }
+    if (has_carry) {
+        rel8g_store(a, carry + (size_t)w * 8 * kMaxDim, kMaxDim);
+        if (lane_id() == 0) carry_row[w] = i1;
+    } else if (lane_id() == 0) {
+        carry_row[w] = -1;
+    }
+}
+
 template <int K>
 __global__ __launch_bounds__(kBlock) void fwd_multi_panel_kernel(
     const int2 *__restrict__ sched, int64_t num_panels, const int32_t *__restrict__ indptr,
@@ -3488,6 +3687,45 @@ struct FwdMulti {
     }
 };
 
+// the register-accumulator R = 8 forward (h = 256) and its CBSR preparation, k <= 32
+template <int K>
+struct CbsrColmask {
+    static int run(const float *data, const uint8_t *sel, int V, float *sdata, uint2 *mrec,
+                   hipStream_t st)
+    {
+        if constexpr (K == 0 || K > 32) {
+            return MAXK_E_DIM;
+        } else {
+            const int64_t blocks = ceil_div(V, kWavesPerBlock);
+            hipLaunchKernelGGL(cbsr_colmask_kernel<K>, dim3((unsigned)(blocks < 8192 ? blocks : 8192)),
+                               dim3(kBlock), 0, st, data, sel, V, sdata, mrec);
+            return launch_status();
+        }
+    }
+};
+
+template <int K>
+struct FwdRel8Gather {
+    static int run(const int32_t *sched, int64_t P, const int32_t *indptr, const int32_t *idx,
+                   const float *val, const float *sdata, const uint2 *mrec, int V, float *out,
+                   float *carry, int32_t *carry_row, hipStream_t st)
+    {
+        if constexpr (K == 0 || K > 32) {
+            return MAXK_E_DIM;
+        } else {
+            const int64_t blocks = ceil_div(P, kWavesPerBlock);
+            hipLaunchKernelGGL(fwd_rel8_gather_kernel<K>, dim3((unsigned)blocks), dim3(kBlock), 0, st,
+                               reinterpret_cast<const int2 *>(sched), P, indptr, idx, val, sdata,
+                               mrec, V, out, carry, carry_row);
+            int rc = launch_status();
+            if (rc) return rc;
+            hipLaunchKernelGGL(carry_fixup_kernel, dim3((unsigned)blocks), dim3(kBlock), 0, st, P,
+                               carry, carry_row, out, kMaxDim, kMaxDim, 8, (size_t)V * kMaxDim);
+            return launch_status();
+        }
+    }
+};
+
 template <int K>
 struct FwdWarp4 {
     static int run(const int32_t *warp4, int W, const int32_t *idx, const float *val,
@@ -4016,6 +4254,44 @@ int maxk_spgemm_forward_multi(const int32_t *sched, int64_t num_panels, const in
     return dispatch_k<FwdMulti>(dim_k, sched, num_panels, indptr, indices, values, num_rel,
                                 cbsr_data, cbsr_sel, num_rows, dim_origin, out, carry, carry_row,
                                 as_stream(stream));
+}
+
+int maxk_cbsr_colmask(const float *cbsr_data, const uint8_t *cbsr_sel, int num_rows, int dim_k,
+                      float *sorted_data, uint32_t *mask_rec, void *stream)
+{
+    if (dim_k < 4 || dim_k > 32 || (dim_k & (dim_k - 1))) return MAXK_E_DIM;
+    if (num_rows < 0 || (num_rows > 0 && (!cbsr_data || !cbsr_sel || !sorted_data || !mask_rec)))
+        return MAXK_E_ARG;
+    if (reinterpret_cast<uintptr_t>(mask_rec) & 7) return MAXK_E_ARG;
+    if (num_rows == 0) return MAXK_OK;
+    return dispatch_k<CbsrColmask>(dim_k, cbsr_data, cbsr_sel, num_rows, sorted_data,
+                                   reinterpret_cast<uint2 *>(mask_rec), as_stream(stream));
+}
+
+int maxk_spgemm_forward_multi_gather(const int32_t *sched, int64_t num_panels,
+                                     const int32_t *indptr, const int32_t *indices,
+                                     const float *values, int num_rel, const float *sorted_data,
+                                     const uint32_t *mask_rec, int num_rows, int dim_origin,
+                                     int dim_k, float *out, void *workspace,
+                                     size_t workspace_bytes, void *stream)
+{
+    if (!sched || !indptr || !out || num_panels < 1 || num_rows < 0) return MAXK_E_ARG;
+    if (num_rel != 8 || dim_origin != kMaxDim) return MAXK_E_DIM;
+    if (dim_k < 4 || dim_k > 32 || (dim_k & (dim_k - 1))) return MAXK_E_DIM;
+    if (num_rows == 0) return MAXK_OK;
+    if (!indices || !values || !sorted_data || !mask_rec) return MAXK_E_ARG;
+    if ((reinterpret_cast<uintptr_t>(mask_rec) & 7) || (reinterpret_cast<uintptr_t>(out) & 15))
+        return MAXK_E_ARG;
+    if (!workspace ||
+        workspace_bytes < maxk_forward_multi_workspace_bytes(num_panels, dim_origin, num_rel))
+        return MAXK_E_WORKSPACE;
+    float *carry = static_cast<float *>(workspace);
+    int32_t *carry_row = reinterpret_cast<int32_t *>(
+        static_cast<char *>(workspace) +
+        align_up((size_t)num_panels * num_rel * kMaxDim * sizeof(float), 256));
+    return dispatch_k<FwdRel8Gather>(dim_k, sched, num_panels, indptr, indices, values, sorted_data,
+                                     reinterpret_cast<const uint2 *>(mask_rec), num_rows, out, carry,
+                                     carry_row, as_stream(stream));
 }
 
 size_t maxk_backward_workspace_bytes(int algo, int64_t num_edges, int dim_k,

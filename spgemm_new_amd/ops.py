@@ -96,6 +96,13 @@ FWD_BLOCKED_MIN_DEGREE = 128
 FWD_BLOCKED_CANDIDATES = (3, 4, 6, 8)  # Reddit: 4 best at k = 32 and 64
 # fused multi-relation forward: reorder CBSR entries against LDS store conflicts
 MULTI_BANK_ORDER = os.environ.get("MAXK_MULTI_BANK_ORDER", "1") != "0"
+# fused R = 8 forward at h = 256, k <= 32: the register-accumulator (gather) kernel
+# instead of the LDS relation-vector one (same bits; MAXK_MULTI_GATHER=0 disables)
+MULTI_GATHER = os.environ.get("MAXK_MULTI_GATHER", "0") != "0"
+
+
+def multi_gather_ok(R: int, k: int, dim_origin: int) -> bool:
+    return R == 8 and dim_origin == 256 and k in (4, 8, 16, 32)
 
 
 def _build_schedule(indptr: torch.Tensor, num_rows: int, num_edges: int, panel_cost: int,
@@ -221,7 +228,15 @@ class MaxKGraph:
             # small graph): the own-column block of a Reddit rank at N=8 took
             # 0.137 ms with 2048-cost panels, 0.089 ms with >= 16 K panels
             cost = self.num_edges + row_cost * self.num_rows
-            panel_cost = int(min(_lib.DEFAULT_PANEL_COST, max(256, cost // max(MIN_PANELS, 1))))
+            want = max(1, cost // max(MIN_PANELS, 1))
+            # rounded to the NEAREST power of two: rank blocks of Reddit measured
+            # slower at the in-between costs (N=4: 1805 -> 0.77 ms vs 2048 -> 0.65 ms
+            # column-blocked forward; N=8: 903 -> 0.42 ms vs 1024 -> 0.35 ms;
+            # tools/exp_rank_fwd.py, round 4)
+            p2 = 1 << max(0, want.bit_length() - 1)
+            if want - p2 > 2 * p2 - want:
+                p2 *= 2
+            panel_cost = int(min(_lib.DEFAULT_PANEL_COST, max(256, p2)))
         self.panel_cost, self.row_cost = panel_cost, row_cost
         self.sched, self.num_panels = _build_schedule(indptr, self.num_rows, self.num_edges,
                                                       panel_cost, row_cost)
@@ -703,12 +718,14 @@ class MaxKGraph:
 
     def forward_multi(self, cbsr_data: torch.Tensor, cbsr_sel: torch.Tensor,
                       values: torch.Tensor, dim_origin: int = 256,
-                      out: torch.Tensor | None = None) -> torch.Tensor:
+                      out: torch.Tensor | None = None, form: str = "auto") -> torch.Tensor:
         """Fused multi-relation forward (BASELINE config 5, ogbn-proteins):
         Y[q] = A_q . scatter(CBSR) with A_q's values = values[:, q]
         (fp32[E, R], R <= 16).  Returns fp32[R, V, dim_origin]; equals R
-        forward() calls with values[:, q].contiguous()."""
-        return spgemm_forward_multi(self, cbsr_data, cbsr_sel, values, dim_origin, out)
+        forward() calls with values[:, q].contiguous().  form: "gather" (the
+        register-accumulator kernel: R = 8, h = 256, k <= 32), "lds" (the
+        relation-vector LDS kernel) or "auto" (gather where it applies)."""
+        return spgemm_forward_multi(self, cbsr_data, cbsr_sel, values, dim_origin, out, form)
 
     def backward_multi(self, grad: torch.Tensor, cbsr_sel: torch.Tensor, values: torch.Tensor,
                        out: torch.Tensor | None = None, algo: int = _lib.MAXK_BWD_AUTO):
@@ -739,7 +756,12 @@ class MaxKGraph:
                      and grad.data_ptr() % 16 == 0)
         if algo == _lib.MAXK_BWD_AUTO:
             # the same lazily built plans the candidates need; rel8 last (its
-            # LOCAL plan costs the most to build)
+            # LOCAL plan costs the most to build).  Measure mode also times the
+            # composed form (R single-relation calls, each its own AUTO) against
+            # them (a shape where no fused form pays must be able to
+            # fall back); fixed mode takes MULTI_STAGED where it applies -- measured
+            # best on proteins R = 8, k = 32 and the only fused form
+            # that serves R in {4, 16} at other k
             fused = []
             if staged_ok:
                 fused += [_lib.MAXK_BWD_MULTI_STAGED, _lib.MAXK_BWD_MULTI_EDGE_GATHER]
@@ -766,17 +788,22 @@ class MaxKGraph:
                     torch.cuda.is_current_stream_capturing():
                 algo = self._bwd_choice[key] = fused[0]
             else:
-                # measured once per (k, h, R): each fused candidate run once, then
-                # timed AUTOTUNE_REPS times, the minimum kept
+                # measured once per (k, h, R): each fused candidate and the composed
+                # form run once, then timed AUTOTUNE_REPS times, the minimum kept
                 best = None
-                for a in fused:
-                    self.backward_multi(grad, cbsr_sel, values, out, a)
+                for a in fused + [_lib.MAXK_BWD_AUTO]:
+                    def run(a=a):
+                        if a == _lib.MAXK_BWD_AUTO:   # composed (not a recursive AUTO call)
+                            self._backward_composed(grad, cbsr_sel, values, out, a)
+                        else:
+                            self.backward_multi(grad, cbsr_sel, values, out, a)
+                    run()
                     t = float("inf")
                     for _ in range(AUTOTUNE_REPS):
                         e0 = torch.cuda.Event(enable_timing=True)
                         e1 = torch.cuda.Event(enable_timing=True)
                         e0.record()
-                        self.backward_multi(grad, cbsr_sel, values, out, a)
+                        run()
                         e1.record()
                         e1.synchronize()
                         t = min(t, e0.elapsed_time(e1))
@@ -1132,7 +1159,8 @@ def spgemm_forward_records(g: MaxKGraph, records: torch.Tensor, k: int, dim_orig
     return out
 
 
-def spgemm_forward_multi(g: MaxKGraph, data, sel, values, dim_origin: int = 256, out=None):
+def spgemm_forward_multi(g: MaxKGraph, data, sel, values, dim_origin: int = 256, out=None,
+                         form: str = "auto"):
     _check_cbsr(g, data, sel)
     k = data.shape[1]
     check_tensor(values, "values", torch.float32, dim=2)
@@ -1153,6 +1181,27 @@ def spgemm_forward_multi(g: MaxKGraph, data, sel, values, dim_origin: int = 256,
         _on_device(g, output=out)
     vals = values if g.num_edges > 0 else torch.zeros((1, R), device=g.device)
     L = _lib.load()
+    if form not in ("auto", "gather", "lds"):
+        raise RuntimeError("form must be 'auto', 'gather' or 'lds'")
+    gather = multi_gather_ok(R, k, dim_origin) and (form == "gather" or
+                                                    (form == "auto" and MULTI_GATHER))
+    if form == "gather" and not gather:
+        raise RuntimeError("the gather form needs R = 8, dim_origin = 256 and k in {4, 8, 16, 32}")
+    if gather:
+        # column-sorted CBSR + per-word column bitmasks (maxk_cbsr_colmask), then the
+        # register-accumulator kernel
+        sd = g._workspace(("colmask_data", k), g.num_cols * k * 4)
+        mr = g._workspace(("colmask_rec",), g.num_cols * 64)
+        _lib.check(L.maxk_cbsr_colmask(data.data_ptr(), sel.data_ptr(), g.num_cols, k, sd.data_ptr(),
+                                       mr.data_ptr(), _stream(out)), "maxk_cbsr_colmask")
+        nbytes = L.maxk_forward_multi_workspace_bytes(g.num_panels, dim_origin, R)
+        ws = g._workspace(("fwd_multi", dim_origin, R), nbytes)
+        _lib.check(L.maxk_spgemm_forward_multi_gather(
+            g.sched.data_ptr(), g.num_panels, g.indptr.data_ptr(), g.indices.data_ptr(),
+            vals.data_ptr(), R, sd.data_ptr(), mr.data_ptr(), g.num_rows, dim_origin, k,
+            out.data_ptr(), ws.data_ptr(), ws.numel(), _stream(out)),
+            "maxk_spgemm_forward_multi_gather")
+        return out
     if MULTI_BANK_ORDER and R % 4 == 0 and k % 8 == 0 and k <= 64:
         # bank-aware entry order for the relation-vector kernel's LDS stores
         # (same CBSR set, bit-identical result)

@@ -1040,3 +1040,73 @@ def test_auto_fixed_mode_is_deterministic(dev, g_small, monkeypatch):
         algos.append(g.last_bwd_algo)
     assert algos[0] == algos[1] == "local"     # short rows, small gradient: LOCAL by rule
     assert torch.equal(outs[0], outs[1])
+
+
+@pytest.mark.parametrize("k", [4, 8, 16, 32])
+@pytest.mark.parametrize("order", ["column", "value"])
+def test_cbsr_colmask(dev, k, order):
+    """maxk_cbsr_colmask: each row's values in ascending column order and, per
+    32-column word, the column bitmask and the count of selected columns below
+    it -- whatever the CBSR entry order."""
+    v, h = 700, 256
+    x = torch.rand((v, h), device=dev)
+    data, sel = S.topk_cbsr(x, k, order=order)
+    L = _lib.load()
+    sd = torch.empty((v, k), device=dev)
+    mr = torch.empty((v, 16), dtype=torch.int32, device=dev)
+    _lib.check(L.maxk_cbsr_colmask(data.data_ptr(), sel.data_ptr(), v, k, sd.data_ptr(),
+                                   mr.data_ptr(), None), "colmask")
+    torch.cuda.synchronize()
+    s_np, d_np = sel.cpu().numpy().astype(np.int64), data.cpu().numpy()
+    o = np.argsort(s_np, axis=1, kind="stable")
+    np.testing.assert_array_equal(sd.cpu().numpy(), np.take_along_axis(d_np, o, 1))
+    m = mr.cpu().numpy().view(np.uint32).reshape(v, 8, 2)
+    for r in range(0, v, 7):
+        cols = set(s_np[r].tolist())
+        for w in range(8):
+            bits = sum(1 << (c - 32 * w) for c in cols if 32 * w <= c < 32 * w + 32)
+            assert m[r, w, 0] == bits and m[r, w, 1] == sum(c < 32 * w for c in cols)
+
+
+@pytest.mark.parametrize("k", [4, 8, 16, 32])
+@pytest.mark.parametrize("panel_cost", [100, 2048])
+def test_forward_multi_gather_bitwise(dev, oracle, k, panel_cost):
+    """The register-accumulator R = 8 forward (form="gather") gives the same bits
+    as the LDS relation-vector kernel (same FMAs in the same edge order) on a
+    graph with hub rows split over many panels, empty rows and value-ordered
+    (unsorted) CBSR entries; both equal the fp64 oracle."""
+    indptr, indices = small_csr(1200, seed=31)
+    v, e, R = len(indptr) - 1, len(indices), 8
+    vals = torch.rand((e, R), device=dev)
+    x = torch.rand((v, 256), device=dev)
+    data, sel = S.topk_cbsr(x, k, order="value")
+    g = S.MaxKGraph(T(indptr, dev), T(indices, dev), panel_cost=panel_cost)
+    y_g = g.forward_multi(data, sel, vals, 256, form="gather")
+    y_l = g.forward_multi(data, sel, vals, 256, form="lds")
+    assert torch.equal(y_g, y_l)
+    dn, sn, vn = data.cpu().numpy(), sel.cpu().numpy(), vals.cpu().numpy()
+    for q in (0, 7):
+        ref = oracle.np_forward(indptr, indices, vn[:, q].copy(), dn, sn, 256)
+        assert oracle.parity_error(y_g[q].cpu().numpy(), ref) <= TOL
+
+
+def test_forward_multi_gather_edge_cases(dev, oracle):
+    """Gather form: empty edge list, a single hub row, the last row only; stale
+    NaN outputs are overwritten; unsupported shapes refuse the explicit form."""
+    for kind in ("single_row_hub", "empty_rows", "last_row_only"):
+        indptr, indices = _edge_graph(kind)
+        v, e = len(indptr) - 1, len(indices)
+        vals = torch.rand((e, 8), device=dev)
+        data, sel = random_cbsr(v, 32, 256, seed=5)
+        g = S.MaxKGraph(T(indptr, dev), T(indices, dev), panel_cost=100)
+        out = torch.full((8, v, 256), float("nan"), device=dev)
+        g.forward_multi(T(data, dev), T(sel, dev), vals, 256, out=out, form="gather")
+        for q in (0, 5):
+            ref = oracle.np_forward(indptr, indices, vals[:, q].cpu().numpy(), data, sel, 256)
+            assert oracle.parity_error(out[q].cpu().numpy(), ref) <= TOL, kind
+    indptr, indices = small_csr(50, seed=2)
+    g = S.MaxKGraph(T(indptr, dev), T(indices, dev))
+    data, sel = random_cbsr(50, 64, 256, seed=1)
+    with pytest.raises(RuntimeError, match="gather form"):
+        g.forward_multi(T(data, dev), T(sel, dev), torch.rand((len(indices), 8), device=dev),
+                        form="gather")
