@@ -653,10 +653,15 @@ def config_sweep(args, dev, only=None):
             cand_f["gather"] = round(_min_ms(lambda: g.forward_multi(data, sel, vals, h, out=y,
                                                                      form="gather")), 4)
         cand_b = {}
-        for nm, a in (("multi_staged", _lib.MAXK_BWD_MULTI_STAGED),
-                      ("multi_edge_gather", _lib.MAXK_BWD_MULTI_EDGE_GATHER),
-                      ("local_rel8", _lib.MAXK_BWD_LOCAL)):
-            cand_b[nm] = round(_min_ms(lambda: g.backward_multi(G, sel, vals, out=dx, algo=a)), 4)
+        for nm, a, fm in (("multi_staged_lds", _lib.MAXK_BWD_MULTI_STAGED, "lds"),
+                          ("multi_staged_regs", _lib.MAXK_BWD_MULTI_STAGED, "gather"),
+                          ("multi_edge_gather_lds", _lib.MAXK_BWD_MULTI_EDGE_GATHER, "lds"),
+                          ("multi_edge_gather_regs", _lib.MAXK_BWD_MULTI_EDGE_GATHER, "gather"),
+                          ("local_rel8", _lib.MAXK_BWD_LOCAL, "auto")):
+            if fm == "gather" and not multi_gather_ok(R, k, h):
+                continue
+            cand_b[nm] = round(_min_ms(lambda: g.backward_multi(G, sel, vals, out=dx, algo=a,
+                                                                form=fm)), 4)
         cand_b["composed"] = round(_min_ms(lambda: g._backward_composed(G, sel, vals, dx,
                                                                         _lib.MAXK_BWD_AUTO)), 4)
         g.forward_multi(data, sel, vals, h, out=y)

@@ -378,6 +378,19 @@ int maxk_sspmm_backward_multi(int algo, const int32_t *sched, int64_t num_panels
                               const int32_t *csc_sched, int64_t csc_num_panels,
                               const int32_t *csc_indptr, void *workspace, size_t workspace_bytes,
                               void *stream);
+/* The same with phase 1 in register form (num_rel = 8, dim_origin = 256, dim_k
+ * in {8, 16, 32}): the source row's 8 gradient rows in registers, per edge the
+ * relations folded for every column and the selected ones fetched by lane
+ * permutes -- the same FMAs in the same order, so the same bits; same
+ * arguments, workspace and phase 2. */
+int maxk_sspmm_backward_multi_gather(int algo, const int32_t *sched, int64_t num_panels,
+                                     const int32_t *indptr, const int32_t *indices,
+                                     const float *values, int num_rel, const float *grad,
+                                     const uint8_t *cbsr_sel, int num_rows, int num_cols,
+                                     int64_t num_edges, int dim_origin, int dim_k, float *dxs,
+                                     const int32_t *csc_pos, const int32_t *csc_sched,
+                                     int64_t csc_num_panels, const int32_t *csc_indptr,
+                                     void *workspace, size_t workspace_bytes, void *stream);
 
 /* ---------------------------------------------------------------------------
  * Backward SSpMM, TILE algorithm (dim_k = 32 or 64, dim_origin = 256): every

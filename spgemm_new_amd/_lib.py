@@ -72,6 +72,8 @@ SIGNATURES = {
                                             _P]),
     "maxk_sspmm_backward_multi": (_I, [_I, _P, _L, _P, _P, _P, _I, _P, _P, _I, _I, _L, _I, _I, _P,
                                        _P, _P, _L, _P, _P, _S, _P]),
+    "maxk_sspmm_backward_multi_gather": (_I, [_I, _P, _L, _P, _P, _P, _I, _P, _P, _I, _I, _L, _I,
+                                              _I, _P, _P, _P, _L, _P, _P, _S, _P]),
     "maxk_sspmm_backward_tile": (_I, [_P, _P, _P, _P, _P, _I, _I, _I, _P, _P, _P, _I, _I, _I, _I,
                                       _P, _P, _P]),
     "maxk_tile_format": (_I, [ctypes.POINTER(_I), ctypes.POINTER(_I)]),

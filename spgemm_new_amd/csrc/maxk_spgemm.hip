@@ -1685,6 +1685,90 @@ __global__ __launch_bounds__(kBlock) void bwd_multi_stage_kernel(
     }
 }
 
+// Register form of the multi-relation STAGED phase 1 for R = 8, h = 256, k <= 32
+// (proteins): the source row's 8 gradient rows stay in registers, lane l holding
+// columns 4l .. 4l+3 of every relation (8 x f4), loaded once per (row, panel).
+// Per edge the lane first folds the relations for ALL of its columns,
+// t = sum_q val[e, q] * G_q[r, 4l .. 4l+3] (8 v_pk_fma_f32 pairs, relation order,
+// so the same FMAs as the LDS kernel's per-column sum), then entry j (lane j <
+// k) fetches t at its selected column c_j by ds_bpermute from lane c_j / 4 and
+// keeps component c_j % 4.  No LDS array is touched: the LDS kernel's 2 x
+// ds_read_b128 per entry at random columns (bank conflicts ~47 % of its LDS
+// cycles) become 4 bpermutes per edge.  P rows as the LDS kernel writes them.
+template <int K, int PM>
+__global__ __launch_bounds__(kBlock) void bwd_rel8_gather_stage_kernel(
+    const int2 *__restrict__ sched, int64_t num_panels, const int32_t *__restrict__ indptr,
+    const int32_t *__restrict__ idx, const float *__restrict__ val,
+    const float *__restrict__ grad, int64_t plane, const uint8_t *__restrict__ sel,
+    const int32_t *__restrict__ csc_pos, int num_rows, float *__restrict__ P)
+{
+    constexpr bool CSRP = PM == kPmEdge;
+    constexpr int KP = PM == kPmCsc ? PRow<K>::KP : K;
+    constexpr int U = 4;
+    const int64_t w = (int64_t)blockIdx.x * kWavesPerBlock + threadIdx.x / kWave;
+    if (w >= num_panels) return;
+    const int lane = lane_id();
+    const int2 a = sched[w], b = sched[w + 1];
+    const int i0 = a.x, j0 = a.y, i1 = b.x, j1 = b.y;
+    const int rlast = i1 < num_rows ? i1 : num_rows - 1;
+    for (int r = i0; r <= rlast; ++r) {
+        const int rb = indptr[r], re = indptr[r + 1];
+        const int eb = rb > j0 ? rb : j0;
+        const int ee = re < j1 ? re : j1;
+        if (eb >= ee) continue;
+        f2 g[8][2];
+        const float *gr = grad + (size_t)r * kMaxDim + 4 * lane;
+#pragma unroll
+        for (int q = 0; q < 8; ++q) {
+            const f4 v = *reinterpret_cast<const f4 *>(gr + (size_t)q * plane);
+            g[q][0] = f2{v.x, v.y};
+            g[q][1] = f2{v.z, v.w};
+        }
+        for (int base = eb; base < ee; base += kWave) {
+            const int n = __builtin_amdgcn_readfirstlane((ee - base) < kWave ? (ee - base) : kWave);
+            int my_c = 0, my_p = 0;
+            if (lane < n) {
+                my_c = __builtin_nontemporal_load(idx + base + lane);
+                my_p = CSRP ? base + lane : __builtin_nontemporal_load(csc_pos + base + lane);
+            }
+            for (int s0 = 0; s0 < n; s0 += U) {
+                uint32_t cb[U];
+#pragma unroll
+                for (int u = 0; u < U; ++u) {
+                    const int c = __builtin_amdgcn_readlane(my_c, s0 + u < n ? s0 + u : s0);
+                    const uint8_t *sp = sel + (size_t)c * K;
+                    cb[u] = sp[lane & (K - 1)];
+                }
+#pragma unroll
+                for (int u = 0; u < U; ++u) {
+                    if (s0 + u >= n) break;
+                    const int eu = __builtin_amdgcn_readfirstlane(base + s0 + u);
+                    const float *vr = val + (size_t)eu * 8;
+                    f2 t0 = {0.f, 0.f}, t1 = {0.f, 0.f};
+#pragma unroll
+                    for (int q = 0; q < 8; ++q) {
+                        const float v = vr[q];
+                        const f2 vv = {v, v};
+                        t0 = __builtin_elementwise_fma(vv, g[q][0], t0);
+                        t1 = __builtin_elementwise_fma(vv, g[q][1], t1);
+                    }
+                    const int src = (int)(cb[u] >> 2) << 2;
+                    const float x = __int_as_float(__builtin_amdgcn_ds_bpermute(src, __float_as_int(t0.x)));
+                    const float y = __int_as_float(__builtin_amdgcn_ds_bpermute(src, __float_as_int(t0.y)));
+                    const float z = __int_as_float(__builtin_amdgcn_ds_bpermute(src, __float_as_int(t1.x)));
+                    const float ww = __int_as_float(__builtin_amdgcn_ds_bpermute(src, __float_as_int(t1.y)));
+                    const uint32_t cc = cb[u] & 3u;
+                    const float lo = (cc & 1u) ? y : x, hi = (cc & 1u) ? ww : z;
+                    const float o = (cc & 2u) ? hi : lo;
+                    const int p = __builtin_amdgcn_readlane(my_p, s0 + u);
+                    if (lane < K) __builtin_nontemporal_store(o, P + (size_t)p * KP + lane);
+                    else if (KP > K && lane < KP) __builtin_nontemporal_store(0.f, P + (size_t)p * KP + lane);
+                }
+            }
+        }
+    }
+}
+
 // STAGED phase 2: dxs[c, :] = sum of P rows [csc_indptr[c], csc_indptr[c+1]),
 // merge-path panels over the CSC ranges, register accumulation + cross-slot
 // reduction; split destinations go through the carry fixup.
@@ -3865,6 +3949,31 @@ struct BwdMultiStage {
     }
 };
 
+// register form of the multi-relation phase 1 (R = 8, h = 256, k <= 32)
+template <int K>
+struct BwdRel8Gather {
+    static int run(bool edge_order, const int32_t *sched, int64_t P, const int32_t *indptr,
+                   const int32_t *idx, const float *val, const float *grad, int64_t plane,
+                   const uint8_t *sel, const int32_t *csc_pos, int V, float *Pbuf, hipStream_t st)
+    {
+        if constexpr (K != 8 && K != 16 && K != 32) {
+            return MAXK_E_DIM;
+        } else {
+            const int2 *sc = reinterpret_cast<const int2 *>(sched);
+            const unsigned blocks = (unsigned)ceil_div(P, kWavesPerBlock);
+            if (edge_order)
+                hipLaunchKernelGGL((bwd_rel8_gather_stage_kernel<K, kPmEdge>), dim3(blocks),
+                                   dim3(kBlock), 0, st, sc, P, indptr, idx, val, grad, plane, sel,
+                                   csc_pos, V, Pbuf);
+            else
+                hipLaunchKernelGGL((bwd_rel8_gather_stage_kernel<K, kPmCsc>), dim3(blocks),
+                                   dim3(kBlock), 0, st, sc, P, indptr, idx, val, grad, plane, sel,
+                                   csc_pos, V, Pbuf);
+            return launch_status();
+        }
+    }
+};
+
 template <int K>
 struct BwdLocal {
     static int run(const int32_t *seg_off, int NS, const int32_t *dstart, int W, int dmax,
@@ -4358,15 +4467,16 @@ int maxk_sspmm_backward(int algo, const int32_t *sched, int64_t num_panels,
                                  gather ? csc_pos : (const int32_t *)nullptr);
 }
 
-int maxk_sspmm_backward_multi(int algo, const int32_t *sched, int64_t num_panels,
-                              const int32_t *indptr, const int32_t *indices, const float *values,
-                              int num_rel, const float *grad, const uint8_t *cbsr_sel,
-                              int num_rows, int num_cols, int64_t num_edges, int dim_origin,
-                              int dim_k, float *dxs, const int32_t *csc_pos,
-                              const int32_t *csc_sched, int64_t csc_num_panels,
-                              const int32_t *csc_indptr, void *workspace, size_t workspace_bytes,
-                              void *stream)
+static int sspmm_backward_multi_impl(bool regs, int algo, const int32_t *sched,
+                                     int64_t num_panels, const int32_t *indptr,
+                                     const int32_t *indices, const float *values, int num_rel,
+                                     const float *grad, const uint8_t *cbsr_sel, int num_rows,
+                                     int num_cols, int64_t num_edges, int dim_origin, int dim_k,
+                                     float *dxs, const int32_t *csc_pos, const int32_t *csc_sched,
+                                     int64_t csc_num_panels, const int32_t *csc_indptr,
+                                     void *workspace, size_t workspace_bytes, void *stream)
 {
+    if (regs && (num_rel != 8 || dim_origin != kMaxDim || dim_k > 32)) return MAXK_E_DIM;
     if (!sched || !indptr || !dxs || num_panels < 1 || num_rows < 0 || num_cols < 0 ||
         num_edges < 0)
         return MAXK_E_ARG;
@@ -4394,13 +4504,47 @@ int maxk_sspmm_backward_multi(int algo, const int32_t *sched, int64_t num_panels
     float *carry = reinterpret_cast<float *>(static_cast<char *>(workspace) + pbytes);
     int32_t *carry_row = reinterpret_cast<int32_t *>(static_cast<char *>(workspace) + pbytes +
                                                      carry_bytes);
-    int rc = dispatch_k<BwdMultiStage>(dim_k, num_rel, gather, sched, num_panels, indptr, indices,
-                                       values, grad, (int64_t)num_rows * dim_origin, cbsr_sel,
-                                       csc_pos, num_rows, dim_origin, Pbuf, st);
+    int rc = regs ? dispatch_k<BwdRel8Gather>(dim_k, gather, sched, num_panels, indptr, indices,
+                                              values, grad, (int64_t)num_rows * dim_origin,
+                                              cbsr_sel, csc_pos, num_rows, Pbuf, st)
+                  : dispatch_k<BwdMultiStage>(dim_k, num_rel, gather, sched, num_panels, indptr,
+                                              indices, values, grad,
+                                              (int64_t)num_rows * dim_origin, cbsr_sel, csc_pos,
+                                              num_rows, dim_origin, Pbuf, st);
     if (rc) return rc;
     return dispatch_k<BwdSegsum>(dim_k, csc_sched, csc_num_panels, csc_indptr, Pbuf, num_cols,
                                  dim_k, dxs, carry, carry_row, st,
                                  gather ? csc_pos : (const int32_t *)nullptr);
+}
+
+int maxk_sspmm_backward_multi(int algo, const int32_t *sched, int64_t num_panels,
+                              const int32_t *indptr, const int32_t *indices, const float *values,
+                              int num_rel, const float *grad, const uint8_t *cbsr_sel,
+                              int num_rows, int num_cols, int64_t num_edges, int dim_origin,
+                              int dim_k, float *dxs, const int32_t *csc_pos,
+                              const int32_t *csc_sched, int64_t csc_num_panels,
+                              const int32_t *csc_indptr, void *workspace, size_t workspace_bytes,
+                              void *stream)
+{
+    return sspmm_backward_multi_impl(false, algo, sched, num_panels, indptr, indices, values,
+                                     num_rel, grad, cbsr_sel, num_rows, num_cols, num_edges,
+                                     dim_origin, dim_k, dxs, csc_pos, csc_sched, csc_num_panels,
+                                     csc_indptr, workspace, workspace_bytes, stream);
+}
+
+int maxk_sspmm_backward_multi_gather(int algo, const int32_t *sched, int64_t num_panels,
+                                     const int32_t *indptr, const int32_t *indices,
+                                     const float *values, int num_rel, const float *grad,
+                                     const uint8_t *cbsr_sel, int num_rows, int num_cols,
+                                     int64_t num_edges, int dim_origin, int dim_k, float *dxs,
+                                     const int32_t *csc_pos, const int32_t *csc_sched,
+                                     int64_t csc_num_panels, const int32_t *csc_indptr,
+                                     void *workspace, size_t workspace_bytes, void *stream)
+{
+    return sspmm_backward_multi_impl(true, algo, sched, num_panels, indptr, indices, values,
+                                     num_rel, grad, cbsr_sel, num_rows, num_cols, num_edges,
+                                     dim_origin, dim_k, dxs, csc_pos, csc_sched, csc_num_panels,
+                                     csc_indptr, workspace, workspace_bytes, stream);
 }
 
 size_t maxk_backward_binned_workspace_bytes(int64_t num_slots, int dim_k)

@@ -728,7 +728,8 @@ class MaxKGraph:
         return spgemm_forward_multi(self, cbsr_data, cbsr_sel, values, dim_origin, out, form)
 
     def backward_multi(self, grad: torch.Tensor, cbsr_sel: torch.Tensor, values: torch.Tensor,
-                       out: torch.Tensor | None = None, algo: int = _lib.MAXK_BWD_AUTO):
+                       out: torch.Tensor | None = None, algo: int = _lib.MAXK_BWD_AUTO,
+                       form: str = "auto"):
         """Backward of forward_multi: dXs = sum_q (A_q^T G_q) sampled at sel,
         with grad fp32[R, V, h] and values fp32[E, R].  Returns fp32[V, k].
         Algorithms: MAXK_BWD_MULTI_STAGED / MULTI_EDGE_GATHER -- one staged pass
@@ -738,7 +739,9 @@ class MaxKGraph:
         by relation; any single-relation algorithm -- composed from R
         single-relation calls (per-relation value columns cached), summed on the
         device.  AUTO times the fused candidates once per (k, h, R) (MAXK_AUTO=
-        fixed: MULTI_STAGED when it applies, then LOCAL rel8, else composed)."""
+        fixed: MULTI_STAGED when it applies, then LOCAL rel8, else composed).  form:
+        phase 1 of the MULTI_* algorithms in register ("gather") or LDS ("lds")
+        form, "auto" = MAXK_MULTI_GATHER's choice; the same bits either way."""
         check_tensor(grad, "grad_output", torch.float32, dim=3)
         check_tensor(values, "values", torch.float32, dim=2)
         R = values.shape[1]
@@ -816,24 +819,32 @@ class MaxKGraph:
                 raise RuntimeError("multi-relation STAGED backward needs R in {4, 8, 16}, k in "
                                    "{8, 16, 32, 64}, h % 4 == 0 and 16-B aligned grad/values")
             return self._backward_multi_staged(grad, cbsr_sel, values, out,
-                                               algo == _lib.MAXK_BWD_MULTI_EDGE_GATHER)
+                                               algo == _lib.MAXK_BWD_MULTI_EDGE_GATHER, form)
         if algo == _lib.MAXK_BWD_LOCAL and R % 8 == 0 and k == 32 and self.num_edges > 0 \
                 and self.local_plan(k) is not None:
             return self._backward_rel8(grad, cbsr_sel, values, out)
         return self._backward_composed(grad, cbsr_sel, values, out, algo)
 
-    def _backward_multi_staged(self, grad, sel, values, out, edge_order: bool):
+    def _backward_multi_staged(self, grad, sel, values, out, edge_order: bool, form: str = "auto"):
         """One pass for all R relations (maxk_sspmm_backward_multi): phase 1 writes
         per edge sum_q val[e,q] * G_q[row, sel[c, :]], phase 2 the CSC segmented sum
-        (edge_order: rows in edge order, gathered through the CSC permutation)."""
+        (edge_order: rows in edge order, gathered through the CSC permutation).
+        form: "gather" (phase 1 in registers, maxk_sspmm_backward_multi_gather: R = 8,
+        h = 256, k <= 32), "lds", or "auto" (gather where it applies and
+        MAXK_MULTI_GATHER is on) -- the same bits either way."""
         L = _lib.load()
         k, h, R = sel.shape[1], grad.shape[2], values.shape[1]
+        regs = R == 8 and h == 256 and k in (8, 16, 32) and (
+            form == "gather" or (form == "auto" and MULTI_GATHER))
+        if form == "gather" and not regs:
+            raise RuntimeError("the gather form needs R = 8, h = 256 and k in {8, 16, 32}")
         cabi = _lib.MAXK_BWD_EDGE_GATHER if edge_order else _lib.MAXK_BWD_STAGED
         csc_pos, csc_indptr, csc_sched, CP = self.csc()
         if edge_order:
             csc_pos = self.csc_perm()
         ws = self._workspace(("bwd", k), L.maxk_backward_workspace_bytes(cabi, self.num_edges, k, CP))
-        _lib.check(L.maxk_sspmm_backward_multi(
+        fn = L.maxk_sspmm_backward_multi_gather if regs else L.maxk_sspmm_backward_multi
+        _lib.check(fn(
             cabi, self.bwd_sched.data_ptr(), self.bwd_num_panels, self.indptr.data_ptr(),
             self.indices.data_ptr(), values.data_ptr(), R, grad.data_ptr(), sel.data_ptr(),
             self.num_rows, self.num_cols, self.num_edges, h, k, out.data_ptr(), csc_pos.data_ptr(),

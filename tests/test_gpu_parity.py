@@ -1110,3 +1110,24 @@ def test_forward_multi_gather_edge_cases(dev, oracle):
     with pytest.raises(RuntimeError, match="gather form"):
         g.forward_multi(T(data, dev), T(sel, dev), torch.rand((len(indices), 8), device=dev),
                         form="gather")
+
+
+@pytest.mark.parametrize("k", [8, 16, 32])
+@pytest.mark.parametrize("algo", [_lib.MAXK_BWD_MULTI_STAGED, _lib.MAXK_BWD_MULTI_EDGE_GATHER])
+def test_backward_multi_gather_bitwise(dev, oracle, k, algo):
+    """Phase 1 of the multi-relation STAGED backward in register form (R = 8,
+    h = 256) writes the same staging rows as the LDS kernel (same FMAs, same
+    relation order): dXs bitwise equal, and equal to sum_q of the fp64 oracle."""
+    indptr, indices = small_csr(1100, seed=41)
+    v, e, R = len(indptr) - 1, len(indices), 8
+    vals = torch.rand((e, R), device=dev)
+    grad = torch.rand((R, v, 256), device=dev)
+    x = torch.rand((v, 256), device=dev)
+    _, sel = S.topk_cbsr(x, k, order="value")
+    g = S.MaxKGraph(T(indptr, dev), T(indices, dev), panel_cost=300)
+    d_g = g.backward_multi(grad, sel, vals, algo=algo, form="gather")
+    d_l = g.backward_multi(grad, sel, vals, algo=algo, form="lds")
+    assert torch.equal(d_g, d_l)
+    sn, vn, gn = sel.cpu().numpy(), vals.cpu().numpy(), grad.cpu().numpy()
+    ref = sum(oracle.np_backward(indptr, indices, vn[:, q].copy(), gn[q], sn) for q in range(R))
+    assert oracle.parity_error(d_g.cpu().numpy(), ref) <= TOL
