@@ -228,6 +228,15 @@ int maxk_local_plan_build(const int32_t *indptr, const int32_t *indices, const f
 int maxk_local_bands_build(const int32_t *woff, const int32_t *edge_rc, int num_waves,
                            int num_rows, int num_bands, int32_t *seg_edge_off, void *stream);
 
+/* GNNAdvisor-style SAG baseline (kernels/spmm_gnna.cu:60-140, the reference's
+ * speedup table README.md:136; not on the MaxK path): out[row] += sum over a
+ * part's neighbours of (values[e] or 1) * x[indices[e]], one wave per part of
+ * the warp4 schedule built with warp_max_nz = part size (maxk_warp4_build;
+ * the reference uses E / V, spmm_gnna.cu:149), float atomics into out (zero it
+ * first).  values NULL: unweighted as the reference.  x fp32[num_cols, dim],
+ * 16-B aligned, dim % 4 == 0, dim <= 256; warp4 16-B aligned. */
+int maxk_spmm_gnna_sag(const int32_t *warp4, int64_t num_parts, const int32_t *indices,
+                       const float *values, const float *x, int dim, float *out, void *stream);
 /* ---------------------------------------------------------------------------
  * Dense SpMM baseline: out = A . x with x fp32[num_cols, dim] dense, 4 <= dim
  * <= 256, dim % 4 == 0 (the comparison kernels of the reference's speedup
@@ -272,8 +281,10 @@ int maxk_spgemm_forward_multi(const int32_t *sched, int64_t num_panels, const in
  * maxk_cbsr_colmask writes: sorted_data fp32[V, k] (each row's values in
  * ascending column order) and mask_rec uint32[V, 16] (per 32-column word: the
  * bitmask of selected columns, then the number selected below it; 8-B aligned).
- * Same result as maxk_spgemm_forward_multi, bit for bit (same FMAs in the same
- * edge order), same schedule and workspace size. */
+ * Same result as maxk_spgemm_forward_multi -- bit for bit at dim_k = 32 (both
+ * add each element's contributions in edge order; at smaller k that kernel
+ * sums per-edge-slot copies, another fp32 order) -- same schedule and
+ * workspace size. */
 int maxk_cbsr_colmask(const float *cbsr_data, const uint8_t *cbsr_sel, int num_rows, int dim_k,
                       float *sorted_data, uint32_t *mask_rec, void *stream);
 int maxk_spgemm_forward_multi_gather(const int32_t *sched, int64_t num_panels,

@@ -102,6 +102,7 @@ SIGNATURES = {
                                    _S, _P]),
     "maxk_local_bands_build": (_I, [_P, _P, _I, _I, _I, _P, _P]),
     "maxk_spmm_dense_forward": (_I, [_P, _L, _P, _P, _P, _P, _I, _I, _P, _P, _S, _P]),
+    "maxk_spmm_gnna_sag": (_I, [_P, _L, _P, _P, _P, _I, _P, _P]),
     "maxk_forward_multi_workspace_bytes": (_S, [_L, _I, _I]),
     "maxk_spgemm_forward_multi": (_I, [_P, _L, _P, _P, _P, _I, _P, _P, _I, _I, _I, _P, _P, _S, _P]),
     "maxk_cbsr_colmask": (_I, [_P, _P, _I, _I, _P, _P, _P]),
@@ -132,6 +133,13 @@ class MaxKError(RuntimeError):
     pass
 
 
+def _missing(name):
+    def call(*_a, **_k):
+        raise MaxKError(f"{name} is not in {LIB_PATH} (built from older sources); rebuild it with "
+                        "`python -c 'import __graft_entry__ as g; g.build()'`")
+    return call
+
+
 def load():
     """Load the HIP library (raises if it has not been built)."""
     global _lib
@@ -142,7 +150,13 @@ def load():
                 "`python -c 'import __graft_entry__ as g; g.build()'` (no CPU fallback exists)")
         L = ctypes.CDLL(LIB_PATH)
         for name, (res, args) in SIGNATURES.items():
-            f = getattr(L, name)
+            try:
+                f = getattr(L, name)
+            except AttributeError:
+                # a library older than these bindings: the entry raises when called
+                # (loudly, naming it), the rest stays usable
+                setattr(L, name, _missing(name))
+                continue
             f.restype = res
             f.argtypes = args
         _lib = L

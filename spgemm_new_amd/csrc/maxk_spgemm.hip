@@ -1007,9 +1007,9 @@ __global__ __launch_bounds__(kBlock) void fwd_rel4_panel_kernel(
 // ds_bpermute fetches the values from the lanes holding the (sorted) CBSR row;
 // a column the source did not select reads a lane of the zero half.  Then
 // 2 x 8 v_pk_fma_f32 with the edge's 8 values (wave-uniform, scalar loads).
-// Per element the FMAs happen in edge order with the same operands as the
-// relation-vector kernel (fma(x, v_q, acc); an unselected column adds 0 * v_q),
-// so the two kernels give the same bits.
+// Per element the FMAs happen in edge order (fma(x, v_q, acc); an unselected
+// column adds 0 * v_q), as in the relation-vector kernel at k = 32, which then
+// gives the same bits (at k < 32 that kernel sums per-edge-slot row copies).
 // ---------------------------------------------------------------------------
 typedef float f2 __attribute__((ext_vector_type(2)));
 
@@ -1766,6 +1766,44 @@ __global__ __launch_bounds__(kBlock) void bwd_rel8_gather_stage_kernel(
                 }
             }
         }
+    }
+}
+
+// GNNAdvisor-style SAG baseline (kernels/spmm_gnna.cu:60-140, the reference's
+// speedup-table comparison; not on the MaxK path): every row's neighbours are
+// cut into parts of part_size (the warp4 chunks of maxk_warp4_build with
+// warp_max_nz = part_size, exactly build_part's cut, spmm_gnna.cu:20-56), one
+// wave per part sums its neighbours' dense rows in registers (lane: 4 columns)
+// and adds the part's partial row into the output with no-return float atomics
+// (the reference stages the partial in shared memory and adds with an atomic
+// exchange loop).  values == NULL: unweighted, as the reference (it passes no
+// degrees); else each neighbour row is scaled by its edge value.  out must be
+// zeroed.  dim % 4 == 0, dim <= 256.
+__global__ __launch_bounds__(kBlock) void gnna_sag_kernel(const int4 *__restrict__ parts,
+                                                          int64_t num_parts,
+                                                          const int32_t *__restrict__ idx,
+                                                          const float *__restrict__ val,
+                                                          const float *__restrict__ x, int dim,
+                                                          float *__restrict__ out)
+{
+    const int64_t w = (int64_t)blockIdx.x * kWavesPerBlock + threadIdx.x / kWave;
+    if (w >= num_parts) return;
+    const int lane = lane_id();
+    const int4 p = parts[w];   // (row, first edge, count, 0)
+    const int c4 = lane * 4;
+    f4 acc = {0.f, 0.f, 0.f, 0.f};
+    if (c4 < dim) {
+        for (int e = p.y; e < p.y + p.z; ++e) {
+            const int nid = idx[e];
+            const f4 v = *reinterpret_cast<const f4 *>(x + (size_t)nid * dim + c4);
+            const float a = val ? val[e] : 1.f;
+            acc += a * v;
+        }
+        float *o = out + (size_t)p.x * dim + c4;
+        gbl_add(o, acc.x);
+        gbl_add(o + 1, acc.y);
+        gbl_add(o + 2, acc.z);
+        gbl_add(o + 3, acc.w);
     }
 }
 
@@ -4151,6 +4189,20 @@ int maxk_rows_sum(const float *parts, int num_parts, int64_t n, float *out, void
     else
         hipLaunchKernelGGL(rows_sum_kernel<false>, dim3((unsigned)blocks), dim3(kBlock), 0, st,
                            parts, num_parts, n, out);
+    return launch_status();
+}
+
+int maxk_spmm_gnna_sag(const int32_t *warp4, int64_t num_parts, const int32_t *indices,
+                       const float *values, const float *x, int dim, float *out, void *stream)
+{
+    if (num_parts < 0 || (num_parts > 0 && (!warp4 || !indices || !x || !out))) return MAXK_E_ARG;
+    if (dim < 4 || dim > kMaxDim || (dim & 3)) return MAXK_E_DIM;
+    if ((reinterpret_cast<uintptr_t>(x) | reinterpret_cast<uintptr_t>(warp4)) & 15) return MAXK_E_ARG;
+    if (num_parts == 0) return MAXK_OK;
+    const int64_t blocks = ceil_div(num_parts, kWavesPerBlock);
+    hipLaunchKernelGGL(gnna_sag_kernel, dim3((unsigned)blocks), dim3(kBlock), 0, as_stream(stream),
+                       reinterpret_cast<const int4 *>(warp4), num_parts, indices, values, x, dim,
+                       out);
     return launch_status();
 }
 

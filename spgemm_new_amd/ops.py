@@ -916,6 +916,36 @@ class MaxKGraph:
         kernels/spmm_gnna.cu:60-140; cuSPARSE, cuda_kernel_bindings.cpp:253-284)."""
         return spmm_dense(self, x, out, values)
 
+    def spmm_sag(self, x: torch.Tensor, weighted: bool = True,
+                 out: torch.Tensor | None = None) -> torch.Tensor:
+        """GNNAdvisor-style SAG baseline (kernels/spmm_gnna.cu:60-140; README.md:136's
+        second comparison): neighbours cut into parts of E / V (build_part,
+        spmm_gnna.cu:20-56 -- the warp4 schedule with that chunk size), one wave
+        per part, float atomics into the output.  weighted=False sums the
+        neighbour rows as the reference does; True scales them by the edge values
+        (= A . x, comparable with forward()).  Not on the MaxK path."""
+        check_tensor(x, "input_features", torch.float32, dim=2)
+        _on_device(self, input_features=x)
+        if x.shape[0] != self.num_cols:
+            raise RuntimeError(f"input_features has {x.shape[0]} rows, graph has {self.num_cols} columns")
+        dim = x.shape[1]
+        if dim % 4 or not 4 <= dim <= 256:
+            raise RuntimeError("SAG needs 4 <= dim <= 256 and dim % 4 == 0")
+        if getattr(self, "_sag_parts", None) is None:
+            part = max(1, self.num_edges // max(self.num_rows, 1))
+            self._sag_parts = warp4_build(self.indptr, part)
+        parts = self._sag_parts
+        if out is None:
+            out = torch.zeros((self.num_rows, dim), dtype=torch.float32, device=self.device)
+        else:
+            check_tensor(out, "output", torch.float32, dim=2)
+            out.zero_()
+        L = _lib.load()
+        _lib.check(L.maxk_spmm_gnna_sag(parts.data_ptr(), parts.numel() // 4, self.indices.data_ptr(),
+                                        self.values.data_ptr() if weighted else None, x.data_ptr(),
+                                        dim, out.data_ptr(), _stream(out)), "maxk_spmm_gnna_sag")
+        return out
+
     def backward(self, grad: torch.Tensor, cbsr_sel: torch.Tensor, out: torch.Tensor | None = None,
                  values: torch.Tensor | None = None, algo: int = _lib.MAXK_BWD_AUTO) -> torch.Tensor:
         """dXs = (A^T G) sampled at sel  (spmm_maxk_backward.cu:15-115).  Returns fp32[V, k]."""

@@ -1071,10 +1071,12 @@ def test_cbsr_colmask(dev, k, order):
 @pytest.mark.parametrize("k", [4, 8, 16, 32])
 @pytest.mark.parametrize("panel_cost", [100, 2048])
 def test_forward_multi_gather_bitwise(dev, oracle, k, panel_cost):
-    """The register-accumulator R = 8 forward (form="gather") gives the same bits
-    as the LDS relation-vector kernel (same FMAs in the same edge order) on a
-    graph with hub rows split over many panels, empty rows and value-ordered
-    (unsorted) CBSR entries; both equal the fp64 oracle."""
+    """The register-accumulator R = 8 forward (form="gather") on a graph with hub
+    rows split over many panels, empty rows and value-ordered (unsorted) CBSR
+    entries equals the fp64 oracle, and gives the same bits as the LDS
+    relation-vector kernel at k = 32 (both add every element's contributions in
+    edge order; at k < 32 the LDS kernel sums per-edge-slot row copies, another
+    fp32 order, so there it agrees to rounding)."""
     indptr, indices = small_csr(1200, seed=31)
     v, e, R = len(indptr) - 1, len(indices), 8
     vals = torch.rand((e, R), device=dev)
@@ -1083,7 +1085,10 @@ def test_forward_multi_gather_bitwise(dev, oracle, k, panel_cost):
     g = S.MaxKGraph(T(indptr, dev), T(indices, dev), panel_cost=panel_cost)
     y_g = g.forward_multi(data, sel, vals, 256, form="gather")
     y_l = g.forward_multi(data, sel, vals, 256, form="lds")
-    assert torch.equal(y_g, y_l)
+    if k == 32:
+        assert torch.equal(y_g, y_l)
+    else:
+        assert torch.allclose(y_g, y_l, rtol=1e-6, atol=1e-6)
     dn, sn, vn = data.cpu().numpy(), sel.cpu().numpy(), vals.cpu().numpy()
     for q in (0, 7):
         ref = oracle.np_forward(indptr, indices, vn[:, q].copy(), dn, sn, 256)
@@ -1131,3 +1136,27 @@ def test_backward_multi_gather_bitwise(dev, oracle, k, algo):
     sn, vn, gn = sel.cpu().numpy(), vals.cpu().numpy(), grad.cpu().numpy()
     ref = sum(oracle.np_backward(indptr, indices, vn[:, q].copy(), gn[q], sn) for q in range(R))
     assert oracle.parity_error(d_g.cpu().numpy(), ref) <= TOL
+
+
+@pytest.mark.parametrize("dim", [4, 64, 100, 256])
+def test_gnna_sag_baseline(dev, dim):
+    """The GNNAdvisor-style SAG baseline (kernels/spmm_gnna.cu:60-140): parts of E/V
+    neighbours (build_part's cut = the warp4 chunks), unweighted as the reference,
+    or edge-weighted = A . x (== the dense SpMM baseline); rows split over many
+    parts (a hub row) and empty rows included."""
+    indptr, indices = small_csr(900, seed=8)
+    v, e = len(indptr) - 1, len(indices)
+    vals = np.random.default_rng(3).random(e, dtype=np.float32)
+    x = np.random.default_rng(4).random((v, dim), dtype=np.float32)
+    g = S.MaxKGraph(T(indptr, dev), T(indices, dev), T(vals, dev))
+    rows = np.repeat(np.arange(v), np.diff(indptr))
+    ref_u = np.zeros((v, dim), np.float64)
+    np.add.at(ref_u, rows, x[indices].astype(np.float64))
+    ref_w = np.zeros((v, dim), np.float64)
+    np.add.at(ref_w, rows, x[indices].astype(np.float64) * vals[:, None])
+    got_u = g.spmm_sag(T(x, dev), weighted=False).cpu().numpy()
+    got_w = g.spmm_sag(T(x, dev)).cpu().numpy()
+    assert np.abs(got_u - ref_u).max() / max(1.0, np.abs(ref_u).max()) <= 1e-5
+    assert np.abs(got_w - ref_w).max() / max(1.0, np.abs(ref_w).max()) <= 1e-5
+    parts = g._sag_parts.cpu().numpy().reshape(-1, 4)
+    assert (parts[:, 2] <= max(1, e // v)).all() and parts[:, 2].sum() == e

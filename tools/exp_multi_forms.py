@@ -1,0 +1,53 @@
+#!/usr/bin/env python3
+"""Config 5 (proteins R=8, k=32, h=256): the fused forward and the multi-relation
+STAGED backward in their LDS and register ("gather") forms, each run a few times
+so a rocprofv3 pass can attribute counters per kernel.  Development tool.
+
+usage: tools/exp_multi_forms.py [--reps 5]
+"""
+import argparse
+import os
+import sys
+
+import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+import spgemm_new_amd as S  # noqa: E402
+from spgemm_new_amd import _lib  # noqa: E402
+from spgemm_new_amd.graphs import CONFIGS, synthetic_columns, synthetic_indptr, synthetic_values  # noqa: E402
+from spgemm_new_amd.ops import _min_ms  # noqa: E402
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--reps", type=int, default=5)
+    a = ap.parse_args()
+    dev = torch.device("cuda:0")
+    V, E = CONFIGS["proteins"]
+    R, k, h = 8, 32, 256
+    indptr = synthetic_indptr(V, E, seed=123, device=dev)
+    indices = synthetic_columns(indptr, seed=123)
+    vals = torch.stack([synthetic_values(130 + q, 0, E, device=dev) for q in range(R)],
+                       dim=1).contiguous()
+    g = S.MaxKGraph(indptr, indices, vals[:, 0].contiguous())
+    gen = torch.Generator(device=dev)
+    gen.manual_seed(124)
+    X = torch.rand((V, h), generator=gen, device=dev)
+    G = torch.rand((R, V, h), generator=gen, device=dev)
+    data, sel = S.topk_cbsr(X, k)
+    y = torch.empty((R, V, h), device=dev)
+    dx = torch.empty((V, k), device=dev)
+    calls = {
+        "fwd lds": lambda: g.forward_multi(data, sel, vals, h, out=y, form="lds"),
+        "fwd gather": lambda: g.forward_multi(data, sel, vals, h, out=y, form="gather"),
+        "bwd lds": lambda: g.backward_multi(G, sel, vals, out=dx, algo=_lib.MAXK_BWD_MULTI_STAGED,
+                                            form="lds"),
+        "bwd regs": lambda: g.backward_multi(G, sel, vals, out=dx,
+                                             algo=_lib.MAXK_BWD_MULTI_STAGED, form="gather"),
+    }
+    for name, fn in calls.items():
+        print(f"{name}: {_min_ms(fn, reps=a.reps):.3f} ms", flush=True)
+
+
+if __name__ == "__main__":
+    main()

@@ -21,7 +21,8 @@ import sys
 HOT = ("bwd_tile_kernel", "tile_combine_kernel", "bwd_bin_sum_kernel", "fwd_panel_kernel", "carry_fixup_kernel", "carry_fixup_owner_kernel", "bwd_panel_kernel",
        "bwd_segsum_kernel", "bwd_local_kernel", "fwd_warp4_kernel", "bwd_warp4_kernel",
        "fwd_rel4_panel_kernel", "bwd_local_rel8_kernel", "grad_interleave_kernel",
-       "cbsr_bank_order_kernel", "rows_sum_kernel", "bwd_multi_stage_kernel")
+       "cbsr_bank_order_kernel", "rows_sum_kernel", "bwd_multi_stage_kernel",
+       "fwd_rel8_gather_kernel", "bwd_rel8_gather_stage_kernel", "cbsr_colmask_kernel")
 
 
 def main(tag: str, root: str = ".", workload: str | None = None):
