@@ -1,7 +1,8 @@
 """README-style speedup table (reference README.md:136):
 MaxK SpGEMM forward and SSpMM backward at k = 8, 16, 32, 64 against dense
 SpMM on the same graph and h = 256 -- our HIP dense SpMM (GNNAdvisor-style
-baseline) and rocSPARSE via torch.sparse.mm.  GPU only; prints one JSON line
+baseline), a GNNAdvisor SAG restatement (MaxKGraph.spmm_sag, spmm_gnna.cu:60-140)
+and rocSPARSE via torch.sparse.mm.  GPU only; prints one JSON line
 per (graph, k) and a markdown table.
 
   python tools/speedup_table.py [--graphs reddit products] [--ks 8 16 32 64]
@@ -48,6 +49,8 @@ def main():
         G = torch.rand((V, args.h), generator=gen, device=dev)
         g = S.MaxKGraph(indptr, indices, values)
         dense_ms = ev_ms(lambda: g.spmm_dense(X))
+        # GNNAdvisor's SAG restated (kernels/spmm_gnna.cu:60-140): unweighted, as the reference
+        sag_ms = ev_ms(lambda: g.spmm_sag(X, weighted=False))
         vendor_ms = None
         if not args.no_vendor:
             a = torch.sparse_csr_tensor(indptr.long(), indices.long(), values, size=(V, V))
@@ -65,7 +68,10 @@ def main():
                  "bwd_ms": round(bwd_ms, 3), "bwd_algo": g.last_bwd_algo,
                  "hip_dense_ms": round(dense_ms, 3),
                  "fwd_speedup_vs_hip_dense": round(dense_ms / fwd_ms, 2),
-                 "bwd_speedup_vs_hip_dense": round(dense_ms / bwd_ms, 2)}
+                 "bwd_speedup_vs_hip_dense": round(dense_ms / bwd_ms, 2),
+                 "gnna_sag_ms": round(sag_ms, 3),
+                 "fwd_speedup_vs_gnna_sag": round(sag_ms / fwd_ms, 2),
+                 "bwd_speedup_vs_gnna_sag": round(sag_ms / bwd_ms, 2)}
             if vendor_ms is not None:
                 r["rocsparse_ms"] = round(vendor_ms, 3)
                 r["fwd_speedup_vs_rocsparse"] = round(vendor_ms / fwd_ms, 2)
@@ -73,11 +79,13 @@ def main():
             rows.append(r)
         del g, X, G, indptr, indices, values
         torch.cuda.empty_cache()
-    print("\n| graph | k | fwd ms | bwd ms | HIP dense SpMM ms | fwd × | bwd × | rocSPARSE ms | fwd × |")
-    print("|---|---|---|---|---|---|---|---|---|")
+    print("\n| graph | k | fwd ms | bwd ms | HIP dense SpMM ms | fwd × | bwd × | GNNA SAG ms | fwd × | "
+          "bwd × | rocSPARSE ms | fwd × |")
+    print("|---|---|---|---|---|---|---|---|---|---|---|---|")
     for r in rows:
         print(f"| {r['graph']} | {r['k']} | {r['fwd_ms']} | {r['bwd_ms']} | {r['hip_dense_ms']} | "
               f"{r['fwd_speedup_vs_hip_dense']} | {r['bwd_speedup_vs_hip_dense']} | "
+              f"{r['gnna_sag_ms']} | {r['fwd_speedup_vs_gnna_sag']} | {r['bwd_speedup_vs_gnna_sag']} | "
               f"{r.get('rocsparse_ms', '-')} | {r.get('fwd_speedup_vs_rocsparse', '-')} |")
 
 
