@@ -15,6 +15,7 @@ import csv
 import glob
 import json
 import os
+import re
 import shutil
 import sys
 
@@ -25,6 +26,14 @@ HOT = ("bwd_tile_kernel", "tile_combine_kernel", "bwd_bin_sum_kernel", "fwd_pane
        "fwd_rel8_gather_kernel", "bwd_rel8_gather_stage_kernel", "cbsr_colmask_kernel")
 
 
+def kname(full: str) -> str:
+    """Kernel base name from a truncated (-T) or full rocprofv3 name."""
+    s = full.replace("(anonymous namespace)::", "")
+    if s.startswith("void "):
+        s = s[5:]
+    return re.split(r"[<(]", s)[0].split("::")[-1].strip()
+
+
 def main(tag: str, root: str = ".", workload: str | None = None):
     src = os.path.join(root, "gpurun_out", f"prof_{tag}")
     dst = os.path.join(root, "profiles")
@@ -33,7 +42,7 @@ def main(tag: str, root: str = ".", workload: str | None = None):
     shutil.copy(stats, os.path.join(dst, f"{tag}_kernel_stats.csv"))
     kern = {}
     for r in csv.DictReader(open(stats)):
-        name = r["Name"].split("(")[0].split("<")[0]
+        name = kname(r["Name"])
         if any(name.endswith(h) for h in HOT):
             kern[name] = {"calls": int(r["Calls"]), "avg_ms": float(r["AverageNs"]) / 1e6,
                           "min_ms": float(r["MinNs"]) / 1e6, "max_ms": float(r["MaxNs"]) / 1e6}
@@ -44,7 +53,7 @@ def main(tag: str, root: str = ".", workload: str | None = None):
         for r in csv.DictReader(open(f)):
             key = (r["Dispatch_Id"], r["Counter_Name"])
             per_dispatch[key] += float(r["Counter_Value"])
-            names[r["Dispatch_Id"]] = r["Kernel_Name"].split("(")[0].split("<")[0]
+            names[r["Dispatch_Id"]] = kname(r["Kernel_Name"])
         for (d, c), v in per_dispatch.items():
             n = names[d]
             if any(n.endswith(h) for h in HOT):
