@@ -66,10 +66,10 @@ def parse():
                    help="R > 1: BASELINE config 5, the fused R-relation forward "
                         "(use with --graph proteins) vs R single-relation forwards")
     p.add_argument("--no-configs", action="store_true",
-                   help="skip the BASELINE config 3 / 5 sweep appended to the N=1 line "
-                        "(products k in {8,16,32,64}, proteins R=8)")
+                   help="skip the BASELINE config 1 / 3 / 5 sweep appended to the N=1 line "
+                        "(Flickr on the CPU, products k in {8,16,32,64}, proteins R=8)")
     p.add_argument("--configs-only", default=None,
-                   help="comma list of sweep entries to run (products_k8,...,proteins_r8)")
+                   help="comma list of sweep entries to run (flickr_cpu,products_k8,...,proteins_r8)")
     return p.parse_args()
 
 
