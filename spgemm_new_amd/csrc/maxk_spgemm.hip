@@ -824,6 +824,17 @@ __device__ __forceinline__ void flush_multi(float *acc, int R, float *__restrict
 #ifndef FWD_REL8_SWZ
 #define FWD_REL8_SWZ 1   // R = 8: 8-float column records, quads XOR-swizzled (0: 12-float records)
 #endif
+// R = 8, k = 32: lane 2j + q works on (entry j, relation quad q) instead of lane
+// j + 32q.  A ds_read_b128 lane group (16 lanes) then covers 8 entries x both
+// quads, whose 16-B units 2c + (q ^ c>>3&1) are distinct mod 16 iff the 8
+// columns differ mod 8; a ds_write_b128 group (8 contiguous lanes) covers 4
+// entries, distinct mod 8 iff their columns differ mod 4 -- and the bank order
+// (cbsr_bank_order_kernel, mode 2) makes both hold wherever the row allows.
+// A bank-conflict model of the two layouts (32 random columns of 256) gives
+// 27 -> 22 LDS cycles per edge.  Same elements, same order: same bits.
+#ifndef FWD_REL8_ILV
+#define FWD_REL8_ILV 1
+#endif
 template <int K, int R4>
 struct Rel4 {
     static_assert((R4 & (R4 - 1)) == 0, "R4 must be a power of two");
@@ -841,6 +852,9 @@ struct Rel4 {
     // takes all 16 values mod 16, and the record is 8 KB per copy instead of
     // 12 (proteins forward 5.32 -> 5.12 ms, same sums bit for bit)
     static constexpr bool SWZ = FWD_REL8_SWZ && R4 == 2;
+    static constexpr bool ILV = FWD_REL8_ILV && SWZ && K == 32;   // lane = 2 * entry + quad
+    static __device__ __forceinline__ int entry(int item) { return ILV ? item >> 1 : item % K; }
+    static __device__ __forceinline__ int quad(int item) { return ILV ? item & 1 : item / K; }
     static constexpr int S = (R4 & 1) || SWZ ? R : R + 4;
     static constexpr int ROW = kMaxDim * S;  // floats per accumulator copy
     // word offset of relation quad rq of column col
@@ -877,7 +891,7 @@ __device__ __forceinline__ void rel4_round_uniform(int my_c, int base, int s0, i
 #pragma unroll
         for (int p = 0; p < PASSES; ++p) {
             const int item = lane + p * kWave;
-            const int j = item % K, rq = item / K;
+            const int j = C::entry(item), rq = C::quad(item);
             d[u][p] = drow[j];
             col[u][p] = srow[j];
             v[u][p] = vrow[rq];
@@ -888,7 +902,7 @@ __device__ __forceinline__ void rel4_round_uniform(int my_c, int base, int s0, i
         if (!FULL && s0 + u >= n) break;
 #pragma unroll
         for (int p = 0; p < PASSES; ++p) {
-            const int rq = (lane + p * kWave) / K;
+            const int rq = C::quad(lane + p * kWave);
             f4 *a = reinterpret_cast<f4 *>(my + C::off(col[u][p], rq));
             *a += d[u][p] * v[u][p];
         }
@@ -2365,6 +2379,41 @@ __global__ __launch_bounds__(kBlock) void cbsr_bank_order_kernel(const float *__
         const bool on = lane < k;
         const int c = on ? sel[r * k + lane] : 0;
         const float d = on ? data[r * k + lane] : 0.f;
+        if (swz == 2) {
+            // the interleaved R = 8, k = 32 layout (FWD_REL8_ILV): the o-th column of
+            // class c & 7 (o < 4) goes to a fixed slot of read group o (entries {0, 1,
+            // 6, 7, 10..13}, {2..5, 8, 9, 14, 15}, and the same + 16), placed so that
+            // every 4-entry write group holds classes of distinct c & 3; the columns
+            // past a class's fourth fill the remaining slots in entry order
+            const int x = c & 7;
+            uint64_t mine = 0;
+#pragma unroll
+            for (int q = 0; q < 8; ++q) {
+                const uint64_t m = __ballot(on && x == q);
+                if (q == x) mine = m;
+            }
+            const int o = __builtin_popcountll(mine & below);
+            // slot of (o, x): read group o, position by class
+            const int t0[8] = {0, 1, 6, 7, 10, 11, 12, 13};
+            const int t1[8] = {4, 5, 2, 3, 14, 15, 8, 9};
+            int slot = -1;
+            if (on && o < 4) slot = ((o & 1) ? t1[x] : t0[x]) + ((o >> 1) << 4);
+            uint32_t filled = slot >= 0 ? (1u << slot) : 0u;
+#pragma unroll
+            for (int m = 1; m < kWave; m <<= 1) filled |= (uint32_t)__shfl_xor((int)filled, m);
+            const uint64_t over = __ballot(on && o >= 4);
+            if (on && o >= 4) {
+                int rk = __builtin_popcountll(over & below);   // this overflow entry's rank
+                uint32_t holes = ~filled;
+                for (; rk > 0; --rk) holes &= holes - 1u;      // drop the rk lowest holes
+                slot = __builtin_ctz(holes);
+            }
+            if (on) {
+                odata[r * k + slot] = d;
+                osel[r * k + slot] = (uint8_t)c;
+            }
+            continue;
+        }
         // the 16-B unit of quad 0 mod 8: (S / 4) c with odd S / 4 (R = 4, 12, 16
         // records: c mod 8), 2c + (c >> 3 & 1) with the swizzled 8-float R = 8 records
         const int res = swz ? (c & 3) | (((c >> 3) & 1) << 2) : c & 7;
@@ -4406,7 +4455,7 @@ int maxk_cbsr_bank_order(const float *cbsr_data, const uint8_t *cbsr_sel, int nu
     if (dim_k < 1 || dim_k > kWave) return MAXK_E_DIM;
     if (num_rel < 1 || num_rel > 16) return MAXK_E_ARG;
     // the store classes follow the record layout maxk_spgemm_forward_multi uses for num_rel
-    const int swz = (FWD_REL8_SWZ && num_rel == 8) ? 1 : 0;
+    const int swz = (FWD_REL8_SWZ && num_rel == 8) ? ((FWD_REL8_ILV && dim_k == 32) ? 2 : 1) : 0;
     if (num_rows < 0 || (num_rows > 0 && (!cbsr_data || !cbsr_sel || !out_data || !out_sel)))
         return MAXK_E_ARG;
     if (num_rows == 0) return MAXK_OK;
