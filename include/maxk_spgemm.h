@@ -269,6 +269,13 @@ size_t maxk_forward_multi_workspace_bytes(int64_t num_panels, int dim_origin, in
  * out_data / out_sel: num_rows x dim_k. */
 int maxk_cbsr_bank_order(const float *cbsr_data, const uint8_t *cbsr_sel, int num_rows,
                          int dim_k, int num_rel, float *out_data, uint8_t *out_sel, void *stream);
+/* The same with each output optional (NULL: not written; cbsr_data may be NULL
+ * when out_data is) plus out_packed uint16[num_rows, dim_k]: the reordered
+ * selector | its ORIGINAL entry index << 8 -- the input of
+ * maxk_sspmm_backward_multi_banked. */
+int maxk_cbsr_bank_order_ex(const float *cbsr_data, const uint8_t *cbsr_sel, int num_rows,
+                            int dim_k, int num_rel, float *out_data, uint8_t *out_sel,
+                            uint16_t *out_packed, void *stream);
 int maxk_spgemm_forward_multi(const int32_t *sched, int64_t num_panels, const int32_t *indptr,
                               const int32_t *indices, const float *values, int num_rel,
                               const float *cbsr_data, const uint8_t *cbsr_sel, int num_rows,
@@ -389,6 +396,20 @@ int maxk_sspmm_backward_multi(int algo, const int32_t *sched, int64_t num_panels
                               const int32_t *csc_sched, int64_t csc_num_panels,
                               const int32_t *csc_indptr, void *workspace, size_t workspace_bytes,
                               void *stream);
+/* The same for num_rel = 8, dim_k = 32 with bank-ordered selectors
+ * (sel_banked = maxk_cbsr_bank_order_ex's out_packed of cbsr_sel, R = 8): phase
+ * 1 reads one edge per wave-instruction, lane 2p + q the quad q of its p-th
+ * column, so LDS reads of a 16-lane group cover 8 columns the bank order made
+ * distinct mod 8; products are stored at the columns' original entries.  Same
+ * FMAs in the same order as maxk_sspmm_backward_multi: the same bits. */
+int maxk_sspmm_backward_multi_banked(int algo, const int32_t *sched, int64_t num_panels,
+                                     const int32_t *indptr, const int32_t *indices,
+                                     const float *values, int num_rel, const float *grad,
+                                     const uint16_t *sel_banked, int num_rows, int num_cols,
+                                     int64_t num_edges, int dim_origin, int dim_k, float *dxs,
+                                     const int32_t *csc_pos, const int32_t *csc_sched,
+                                     int64_t csc_num_panels, const int32_t *csc_indptr,
+                                     void *workspace, size_t workspace_bytes, void *stream);
 /* The same with phase 1 in register form (num_rel = 8, dim_origin = 256, dim_k
  * in {8, 16, 32}): the source row's 8 gradient rows in registers, per edge the
  * relations folded for every column and the selected ones fetched by lane

@@ -74,6 +74,9 @@ SIGNATURES = {
                                        _P, _P, _L, _P, _P, _S, _P]),
     "maxk_sspmm_backward_multi_gather": (_I, [_I, _P, _L, _P, _P, _P, _I, _P, _P, _I, _I, _L, _I,
                                               _I, _P, _P, _P, _L, _P, _P, _S, _P]),
+    "maxk_sspmm_backward_multi_banked": (_I, [_I, _P, _L, _P, _P, _P, _I, _P, _P, _I, _I, _L, _I,
+                                              _I, _P, _P, _P, _L, _P, _P, _S, _P]),
+    "maxk_cbsr_bank_order_ex": (_I, [_P, _P, _I, _I, _I, _P, _P, _P, _P]),
     "maxk_sspmm_backward_tile": (_I, [_P, _P, _P, _P, _P, _I, _I, _I, _P, _P, _P, _I, _I, _I, _I,
                                       _P, _P, _P]),
     "maxk_tile_format": (_I, [ctypes.POINTER(_I), ctypes.POINTER(_I)]),

@@ -1706,12 +1706,108 @@ __device__ __forceinline__ void bwd_multi_edges(int e0, int e1, const int32_t *_
     }
 }
 
+// R = 8, k = 32 with bank-ordered selectors (round 4): one edge per
+// wave-instruction, lane 2p + q reads quad q of the edge's p-th (bank-ordered)
+// column -- a ds_read_b128 16-lane group then covers 8 columns x both quads,
+// conflict-free iff the 8 columns differ mod 8, which the bank order (mode 2,
+// maxk_cbsr_bank_order) arranges wherever the row allows (a conflict model:
+// 11.9 -> 7.7 LDS cycles per edge against the 8-lanes-per-edge layout above,
+// whose 16-lane groups mix four destinations' columns).  Lane 2p + 1 hands its
+// quad to lane 2p (DPP), which adds the 8 relations in order -- the same FMAs
+// as bwd_multi_edges, so the same bits -- and pushes the product to the lane of
+// the column's ORIGINAL entry (ds_permute; sp = bank-ordered selector |
+// original entry << 8), so lanes 0..31 store the row as one contiguous line.
+template <int PM>
+__device__ __forceinline__ void bwd_multi_edges_banked(int e0, int e1,
+                                                       const int32_t *__restrict__ idx,
+                                                       const float *__restrict__ val,
+                                                       const int32_t *__restrict__ csc_pos,
+                                                       const uint16_t *__restrict__ sp,
+                                                       const char *gs, float *__restrict__ P)
+{
+    constexpr bool CSRP = PM == kPmEdge;
+    constexpr int K = 32, KP = 32, U = 8;
+    const int lane = lane_id();
+    const int ent = lane >> 1, q = lane & 1;
+    for (int base = e0; base < e1; base += kWave) {
+        const int n = __builtin_amdgcn_readfirstlane((e1 - base) < kWave ? (e1 - base) : kWave);
+        int my_c = 0, my_p = 0;
+        f4 v0 = f4{0.f, 0.f, 0.f, 0.f}, v1 = v0;
+        if (lane < n) {
+            my_c = __builtin_nontemporal_load(idx + base + lane);
+            my_p = CSRP ? base + lane : __builtin_nontemporal_load(csc_pos + base + lane);
+            const f4 *vp = reinterpret_cast<const f4 *>(val + (size_t)(base + lane) * 8);
+            v0 = __builtin_nontemporal_load(vp);
+            v1 = __builtin_nontemporal_load(vp + 1);
+        }
+        // straight-line per group of U edges (the tail clamped to the last edge,
+        // its stores skipped): U selector loads, U LDS reads, then per edge its 8
+        // values by readlane (scalar loads would share the LDS reads' counter)
+        // the next group's selectors are loaded while this group computes (one
+        // gather round trip per U edges would otherwise stall the wave)
+        uint32_t wn[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const int c = __builtin_amdgcn_readlane(my_c, u < n ? u : n - 1);
+            wn[u] = sp[(size_t)c * K + ent];
+        }
+        for (int s0 = 0; s0 < n; s0 += U) {
+            uint32_t w[U];
+            f4 g[U];
+#pragma unroll
+            for (int u = 0; u < U; ++u) w[u] = wn[u];
+            if (s0 + U < n) {
+#pragma unroll
+                for (int u = 0; u < U; ++u) {
+                    const int t = s0 + U + u;
+                    const int c = __builtin_amdgcn_readlane(my_c, t < n ? t : n - 1);
+                    wn[u] = sp[(size_t)c * K + ent];
+                }
+            }
+#pragma unroll
+            for (int u = 0; u < U; ++u)
+                g[u] = *reinterpret_cast<const f4 *>(gs + RelLds<8>::off(w[u] & 0xffu, q));
+#pragma unroll
+            for (int u = 0; u < U; ++u) {
+                const int uu = s0 + u < n ? s0 + u : n - 1;
+                // quad 1 of the column from the odd lane (DPP quad_perm [1,0,3,2])
+                f4 h;
+                h.x = __uint_as_float(dpp_xor1(__float_as_uint(g[u].x)));
+                h.y = __uint_as_float(dpp_xor1(__float_as_uint(g[u].y)));
+                h.z = __uint_as_float(dpp_xor1(__float_as_uint(g[u].z)));
+                h.w = __uint_as_float(dpp_xor1(__float_as_uint(g[u].w)));
+                const auto rl = [uu](float x) {
+                    return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(x), uu));
+                };
+                float acc = 0.f;
+                acc = fmaf(rl(v0.x), g[u].x, acc);
+                acc = fmaf(rl(v0.y), g[u].y, acc);
+                acc = fmaf(rl(v0.z), g[u].z, acc);
+                acc = fmaf(rl(v0.w), g[u].w, acc);
+                acc = fmaf(rl(v1.x), h.x, acc);
+                acc = fmaf(rl(v1.y), h.y, acc);
+                acc = fmaf(rl(v1.z), h.z, acc);
+                acc = fmaf(rl(v1.w), h.w, acc);
+                // each even lane pushes its product to the lane of the column's
+                // original entry (odd lanes to the unused upper half), so lanes
+                // 0..31 store the row as one contiguous 128-B line
+                const int dst = q == 0 ? (int)(w[u] >> 8) : 32 + ent;
+                const float o = __int_as_float(__builtin_amdgcn_ds_permute(dst << 2, __float_as_int(acc)));
+                const int p = __builtin_amdgcn_readlane(my_p, uu);
+                if (lane < 32 && s0 + u < n)
+                    __builtin_nontemporal_store(o, P + (size_t)p * KP + lane);
+            }
+        }
+    }
+}
+
 template <int K, int R, int PM>
 __global__ __launch_bounds__(kBlock) void bwd_multi_stage_kernel(
     const int2 *__restrict__ sched, int64_t num_panels, const int32_t *__restrict__ indptr,
     const int32_t *__restrict__ idx, const float *__restrict__ val,
     const float *__restrict__ grad, int64_t plane, const uint8_t *__restrict__ sel,
-    const int32_t *__restrict__ csc_pos, int num_rows, int dim, float *__restrict__ P)
+    const int32_t *__restrict__ csc_pos, int num_rows, int dim, float *__restrict__ P,
+    const uint16_t *__restrict__ sp = nullptr)
 {
     extern __shared__ __attribute__((aligned(16))) float lds[];
     char *gs = reinterpret_cast<char *>(lds + (threadIdx.x / kWave) * (kMaxDim * R));
@@ -1726,6 +1822,12 @@ __global__ __launch_bounds__(kBlock) void bwd_multi_stage_kernel(
         const int ee = re < j1 ? re : j1;
         if (eb >= ee) continue;
         stage_rel_rows<R>(gs, grad, plane, r, dim);
+        if constexpr (K == 32 && R == 8) {
+            if (sp) {
+                bwd_multi_edges_banked<PM>(eb, ee, idx, val, csc_pos, sp, gs, P);
+                continue;
+            }
+        }
         bwd_multi_edges<K, R, PM>(eb, ee, idx, val, csc_pos, sel, gs, P);
     }
 }
@@ -2369,7 +2471,8 @@ __global__ __launch_bounds__(kBlock) void cbsr_bank_order_kernel(const float *__
                                                                  const uint8_t *__restrict__ sel,
                                                                  int num_rows, int k, int swz,
                                                                  float *__restrict__ odata,
-                                                                 uint8_t *__restrict__ osel)
+                                                                 uint8_t *__restrict__ osel,
+                                                                 uint16_t *__restrict__ opacked)
 {
     const int lane = lane_id();
     const int64_t nwaves = (int64_t)gridDim.x * kWavesPerBlock;
@@ -2378,7 +2481,7 @@ __global__ __launch_bounds__(kBlock) void cbsr_bank_order_kernel(const float *__
          r += nwaves) {
         const bool on = lane < k;
         const int c = on ? sel[r * k + lane] : 0;
-        const float d = on ? data[r * k + lane] : 0.f;
+        const float d = on && odata ? data[r * k + lane] : 0.f;
         if (swz == 2) {
             // the interleaved R = 8, k = 32 layout (FWD_REL8_ILV): the o-th column of
             // class c & 7 (o < 4) goes to a fixed slot of read group o (entries {0, 1,
@@ -2409,8 +2512,9 @@ __global__ __launch_bounds__(kBlock) void cbsr_bank_order_kernel(const float *__
                 slot = __builtin_ctz(holes);
             }
             if (on) {
-                odata[r * k + slot] = d;
-                osel[r * k + slot] = (uint8_t)c;
+                if (odata) odata[r * k + slot] = d;
+                if (osel) osel[r * k + slot] = (uint8_t)c;
+                if (opacked) opacked[r * k + slot] = (uint16_t)(c | (lane << 8));
             }
             continue;
         }
@@ -2432,8 +2536,9 @@ __global__ __launch_bounds__(kBlock) void cbsr_bank_order_kernel(const float *__
 #pragma unroll
         for (int q = 0; q < 8; ++q) pos += (cnt[q] < occ ? cnt[q] : occ) + (q < res && cnt[q] > occ);
         if (on) {
-            odata[r * k + pos] = d;
-            osel[r * k + pos] = (uint8_t)c;
+            if (odata) odata[r * k + pos] = d;
+            if (osel) osel[r * k + pos] = (uint8_t)c;
+            if (opacked) opacked[r * k + pos] = (uint16_t)(c | (lane << 8));
         }
     }
 }
@@ -4033,34 +4138,34 @@ struct BwdMultiStage {
     static int launch(bool edge_order, const int2 *sc, int64_t P, const int32_t *indptr,
                       const int32_t *idx, const float *val, const float *grad, int64_t plane,
                       const uint8_t *sel, const int32_t *csc_pos, int V, int dim, float *Pbuf,
-                      hipStream_t st)
+                      hipStream_t st, const uint16_t *sp)
     {
         const unsigned blocks = (unsigned)ceil_div(P, kWavesPerBlock);
         const size_t lds = (size_t)kWavesPerBlock * kMaxDim * R * sizeof(float);
         if (edge_order)
             hipLaunchKernelGGL((bwd_multi_stage_kernel<K, R, kPmEdge>), dim3(blocks), dim3(kBlock),
                                lds, st, sc, P, indptr, idx, val, grad, plane, sel, csc_pos, V, dim,
-                               Pbuf);
+                               Pbuf, sp);
         else
             hipLaunchKernelGGL((bwd_multi_stage_kernel<K, R, kPmCsc>), dim3(blocks), dim3(kBlock),
                                lds, st, sc, P, indptr, idx, val, grad, plane, sel, csc_pos, V, dim,
-                               Pbuf);
+                               Pbuf, sp);
         return launch_status();
     }
 
     static int run(int R, bool edge_order, const int32_t *sched, int64_t P, const int32_t *indptr,
                    const int32_t *idx, const float *val, const float *grad, int64_t plane,
                    const uint8_t *sel, const int32_t *csc_pos, int V, int dim, float *Pbuf,
-                   hipStream_t st)
+                   hipStream_t st, const uint16_t *sp = nullptr)
     {
         if constexpr (K != 8 && K != 16 && K != 32 && K != 64) {
             return MAXK_E_DIM;
         } else {
             const int2 *sc = reinterpret_cast<const int2 *>(sched);
             switch (R) {
-            case 4: return launch<4>(edge_order, sc, P, indptr, idx, val, grad, plane, sel, csc_pos, V, dim, Pbuf, st);
-            case 8: return launch<8>(edge_order, sc, P, indptr, idx, val, grad, plane, sel, csc_pos, V, dim, Pbuf, st);
-            case 16: return launch<16>(edge_order, sc, P, indptr, idx, val, grad, plane, sel, csc_pos, V, dim, Pbuf, st);
+            case 4: return launch<4>(edge_order, sc, P, indptr, idx, val, grad, plane, sel, csc_pos, V, dim, Pbuf, st, nullptr);
+            case 8: return launch<8>(edge_order, sc, P, indptr, idx, val, grad, plane, sel, csc_pos, V, dim, Pbuf, st, sp);
+            case 16: return launch<16>(edge_order, sc, P, indptr, idx, val, grad, plane, sel, csc_pos, V, dim, Pbuf, st, nullptr);
             default: return MAXK_E_ARG;
             }
         }
@@ -4452,17 +4557,27 @@ int maxk_spgemm_forward_records(const int32_t *sched, int64_t num_panels, const 
 int maxk_cbsr_bank_order(const float *cbsr_data, const uint8_t *cbsr_sel, int num_rows,
                          int dim_k, int num_rel, float *out_data, uint8_t *out_sel, void *stream)
 {
+    return maxk_cbsr_bank_order_ex(cbsr_data, cbsr_sel, num_rows, dim_k, num_rel, out_data, out_sel,
+                                   nullptr, stream);
+}
+
+int maxk_cbsr_bank_order_ex(const float *cbsr_data, const uint8_t *cbsr_sel, int num_rows,
+                            int dim_k, int num_rel, float *out_data, uint8_t *out_sel,
+                            uint16_t *out_packed, void *stream)
+{
     if (dim_k < 1 || dim_k > kWave) return MAXK_E_DIM;
     if (num_rel < 1 || num_rel > 16) return MAXK_E_ARG;
+    if (num_rows > 0 && !cbsr_sel) return MAXK_E_ARG;
+    if (num_rows > 0 && out_data && !cbsr_data) return MAXK_E_ARG;
+    if (num_rows > 0 && !out_data && !out_sel && !out_packed) return MAXK_E_ARG;
     // the store classes follow the record layout maxk_spgemm_forward_multi uses for num_rel
     const int swz = (FWD_REL8_SWZ && num_rel == 8) ? ((FWD_REL8_ILV && dim_k == 32) ? 2 : 1) : 0;
-    if (num_rows < 0 || (num_rows > 0 && (!cbsr_data || !cbsr_sel || !out_data || !out_sel)))
-        return MAXK_E_ARG;
+    if (num_rows < 0) return MAXK_E_ARG;
     if (num_rows == 0) return MAXK_OK;
     const int64_t blocks = ceil_div(num_rows, kWavesPerBlock);
     hipLaunchKernelGGL(cbsr_bank_order_kernel, dim3((unsigned)(blocks < 4096 ? blocks : 4096)),
                        dim3(kBlock), 0, as_stream(stream), cbsr_data, cbsr_sel, num_rows, dim_k,
-                       swz, out_data, out_sel);
+                       swz, out_data, out_sel, out_packed);
     return launch_status();
 }
 
@@ -4606,9 +4721,11 @@ static int sspmm_backward_multi_impl(bool regs, int algo, const int32_t *sched,
                                      int num_cols, int64_t num_edges, int dim_origin, int dim_k,
                                      float *dxs, const int32_t *csc_pos, const int32_t *csc_sched,
                                      int64_t csc_num_panels, const int32_t *csc_indptr,
-                                     void *workspace, size_t workspace_bytes, void *stream)
+                                     void *workspace, size_t workspace_bytes, void *stream,
+                                     const uint16_t *sel_banked = nullptr)
 {
     if (regs && (num_rel != 8 || dim_origin != kMaxDim || dim_k > 32)) return MAXK_E_DIM;
+    if (sel_banked && (num_rel != 8 || dim_k != 32)) return MAXK_E_DIM;
     if (!sched || !indptr || !dxs || num_panels < 1 || num_rows < 0 || num_cols < 0 ||
         num_edges < 0)
         return MAXK_E_ARG;
@@ -4642,7 +4759,7 @@ static int sspmm_backward_multi_impl(bool regs, int algo, const int32_t *sched,
                   : dispatch_k<BwdMultiStage>(dim_k, num_rel, gather, sched, num_panels, indptr,
                                               indices, values, grad,
                                               (int64_t)num_rows * dim_origin, cbsr_sel, csc_pos,
-                                              num_rows, dim_origin, Pbuf, st);
+                                              num_rows, dim_origin, Pbuf, st, sel_banked);
     if (rc) return rc;
     return dispatch_k<BwdSegsum>(dim_k, csc_sched, csc_num_panels, csc_indptr, Pbuf, num_cols,
                                  dim_k, dxs, carry, carry_row, st,
@@ -4662,6 +4779,24 @@ int maxk_sspmm_backward_multi(int algo, const int32_t *sched, int64_t num_panels
                                      num_rel, grad, cbsr_sel, num_rows, num_cols, num_edges,
                                      dim_origin, dim_k, dxs, csc_pos, csc_sched, csc_num_panels,
                                      csc_indptr, workspace, workspace_bytes, stream);
+}
+
+int maxk_sspmm_backward_multi_banked(int algo, const int32_t *sched, int64_t num_panels,
+                                     const int32_t *indptr, const int32_t *indices,
+                                     const float *values, int num_rel, const float *grad,
+                                     const uint16_t *sel_banked, int num_rows, int num_cols,
+                                     int64_t num_edges, int dim_origin, int dim_k, float *dxs,
+                                     const int32_t *csc_pos, const int32_t *csc_sched,
+                                     int64_t csc_num_panels, const int32_t *csc_indptr,
+                                     void *workspace, size_t workspace_bytes, void *stream)
+{
+    if (!sel_banked && num_cols > 0) return MAXK_E_ARG;
+    // cbsr_sel is only null-checked (the banked kernel reads sel_banked)
+    return sspmm_backward_multi_impl(false, algo, sched, num_panels, indptr, indices, values,
+                                     num_rel, grad, reinterpret_cast<const uint8_t *>(sel_banked),
+                                     num_rows, num_cols, num_edges, dim_origin, dim_k, dxs,
+                                     csc_pos, csc_sched, csc_num_panels, csc_indptr, workspace,
+                                     workspace_bytes, stream, sel_banked);
 }
 
 int maxk_sspmm_backward_multi_gather(int algo, const int32_t *sched, int64_t num_panels,

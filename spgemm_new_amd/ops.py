@@ -99,6 +99,9 @@ MULTI_BANK_ORDER = os.environ.get("MAXK_MULTI_BANK_ORDER", "1") != "0"
 # fused R = 8 forward at h = 256, k <= 32: the register-accumulator (gather) kernel
 # instead of the LDS relation-vector one (same bits; MAXK_MULTI_GATHER=0 disables)
 MULTI_GATHER = os.environ.get("MAXK_MULTI_GATHER", "0") != "0"
+# multi-relation STAGED backward at R = 8, k = 32: phase 1 on bank-ordered
+# selectors (maxk_sspmm_backward_multi_banked; same bits; measured slower, DESIGN §4: 1 enables)
+MULTI_BANKED = os.environ.get("MAXK_MULTI_BANKED", "0") != "0"
 
 
 def multi_gather_ok(R: int, k: int, dim_origin: int) -> bool:
@@ -830,23 +833,41 @@ class MaxKGraph:
         per edge sum_q val[e,q] * G_q[row, sel[c, :]], phase 2 the CSC segmented sum
         (edge_order: rows in edge order, gathered through the CSC permutation).
         form: "gather" (phase 1 in registers, maxk_sspmm_backward_multi_gather: R = 8,
-        h = 256, k <= 32), "lds", or "auto" (gather where it applies and
-        MAXK_MULTI_GATHER is on) -- the same bits either way."""
+        h = 256, k <= 32), "banked" (R = 8, k = 32: one edge per wave-instruction on
+        bank-ordered selectors, maxk_sspmm_backward_multi_banked), "lds", or "auto"
+        (gather where it applies and MAXK_MULTI_GATHER is on, else banked where it
+        applies and MAXK_MULTI_BANKED is on) -- the same bits in every form."""
         L = _lib.load()
         k, h, R = sel.shape[1], grad.shape[2], values.shape[1]
         regs = R == 8 and h == 256 and k in (8, 16, 32) and (
             form == "gather" or (form == "auto" and MULTI_GATHER))
         if form == "gather" and not regs:
             raise RuntimeError("the gather form needs R = 8, h = 256 and k in {8, 16, 32}")
+        banked = not regs and R == 8 and k == 32 and (
+            form == "banked" or (form == "auto" and MULTI_BANKED))
+        if form == "banked" and not banked:
+            raise RuntimeError("the banked form needs R = 8 and k = 32")
+        if form not in ("auto", "gather", "banked", "lds"):
+            raise RuntimeError(f"unknown backward_multi form {form!r}")
         cabi = _lib.MAXK_BWD_EDGE_GATHER if edge_order else _lib.MAXK_BWD_STAGED
         csc_pos, csc_indptr, csc_sched, CP = self.csc()
         if edge_order:
             csc_pos = self.csc_perm()
         ws = self._workspace(("bwd", k), L.maxk_backward_workspace_bytes(cabi, self.num_edges, k, CP))
         fn = L.maxk_sspmm_backward_multi_gather if regs else L.maxk_sspmm_backward_multi
+        sel_arg = sel
+        if banked:
+            # this call's selectors bank-ordered, each | its original entry << 8
+            # (one small pass over sel: 3 B per entry)
+            sp = self._workspace(("bwd_banked", k), self.num_cols * k * 2)
+            sp = sp[: self.num_cols * k * 2].view(torch.int16)
+            _lib.check(L.maxk_cbsr_bank_order_ex(None, sel.data_ptr(), self.num_cols, k, R, None,
+                                                 None, sp.data_ptr(), _stream(out)),
+                       "maxk_cbsr_bank_order_ex")
+            fn, sel_arg = L.maxk_sspmm_backward_multi_banked, sp
         _lib.check(fn(
             cabi, self.bwd_sched.data_ptr(), self.bwd_num_panels, self.indptr.data_ptr(),
-            self.indices.data_ptr(), values.data_ptr(), R, grad.data_ptr(), sel.data_ptr(),
+            self.indices.data_ptr(), values.data_ptr(), R, grad.data_ptr(), sel_arg.data_ptr(),
             self.num_rows, self.num_cols, self.num_edges, h, k, out.data_ptr(), csc_pos.data_ptr(),
             csc_sched.data_ptr(), CP, csc_indptr.data_ptr(), ws.data_ptr(), ws.numel(),
             _stream(out)), "maxk_sspmm_backward_multi")

@@ -1155,6 +1155,49 @@ def test_backward_multi_gather_bitwise(dev, oracle, k, algo):
     assert oracle.parity_error(d_g.cpu().numpy(), ref) <= TOL
 
 
+@pytest.mark.parametrize("h,order", [(256, "value"), (256, "column"), (64, "value"), (36, "value")])
+@pytest.mark.parametrize("algo", [_lib.MAXK_BWD_MULTI_STAGED, _lib.MAXK_BWD_MULTI_EDGE_GATHER])
+def test_backward_multi_banked_bitwise(dev, oracle, h, order, algo):
+    """R = 8, k = 32: phase 1 on bank-ordered selectors (one edge per
+    wave-instruction, products stored at the columns' original entries) gives
+    the LDS form's bits; h = 36 / 64 crowd the 32 columns into few residues mod 8
+    (the bank order's overflow path)."""
+    indptr, indices = small_csr(1300, seed=43)
+    v, e, R = len(indptr) - 1, len(indices), 8
+    vals = torch.rand((e, R), device=dev)
+    grad = torch.rand((R, v, h), device=dev)
+    x = torch.rand((v, h), device=dev)
+    _, sel = S.topk_cbsr(x, 32, order=order)
+    g = S.MaxKGraph(T(indptr, dev), T(indices, dev), panel_cost=300)
+    d_b = g.backward_multi(grad, sel, vals, algo=algo, form="banked")
+    d_l = g.backward_multi(grad, sel, vals, algo=algo, form="lds")
+    assert torch.equal(d_b, d_l)
+    sn, vn, gn = sel.cpu().numpy(), vals.cpu().numpy(), grad.cpu().numpy()
+    ref = sum(oracle.np_backward(indptr, indices, vn[:, q].copy(), gn[q], sn) for q in range(R))
+    assert oracle.parity_error(d_b.cpu().numpy(), ref) <= TOL
+
+
+def test_bank_order_packed(dev):
+    """maxk_cbsr_bank_order_ex's packed output: low byte = the reordered selector
+    (== out_sel), high byte = its original entry; a permutation per row."""
+    L = _lib.load()
+    data, sel = random_cbsr(700, 32, 256, seed=5)
+    sel[:40, :] = np.arange(0, 256, 8)[None, :]          # one residue only: all overflow
+    d, s = T(data, dev), T(sel, dev)
+    osel = torch.empty_like(s)
+    sp = torch.empty(s.shape, dtype=torch.int16, device=dev)
+    _lib.check(L.maxk_cbsr_bank_order_ex(d.data_ptr(), s.data_ptr(), 700, 32, 8, None,
+                                         osel.data_ptr(), sp.data_ptr(), None), "bank_order_ex")
+    torch.cuda.synchronize()
+    p = sp.cpu().numpy().astype(np.int64) & 0xFFFF
+    assert np.array_equal((p & 0xFF).astype(np.uint8), osel.cpu().numpy())
+    orig = p >> 8
+    assert (np.sort(orig, axis=1) == np.arange(32)[None, :]).all()
+    assert np.array_equal(np.take_along_axis(sel, orig, axis=1), osel.cpu().numpy())
+    assert L.maxk_cbsr_bank_order_ex(None, s.data_ptr(), 700, 32, 8, None, None, None,
+                                     None) == _lib.MAXK_E_ARG
+
+
 @pytest.mark.parametrize("dim", [4, 64, 100, 256])
 def test_gnna_sag_baseline(dev, dim):
     """The GNNAdvisor-style SAG baseline (kernels/spmm_gnna.cu:60-140): parts of E/V

@@ -1,6 +1,6 @@
 #!/usr/bin/env python3
 """Config 5 (proteins R=8, k=32, h=256): the fused forward and the multi-relation
-STAGED backward in their LDS and register ("gather") forms, each run a few times
+STAGED backward in their LDS, register ("gather") and bank-ordered ("banked") forms, each run a few times
 so a rocprofv3 pass can attribute counters per kernel.  Development tool.
 
 usage: tools/exp_multi_forms.py [--reps 5]
@@ -21,6 +21,7 @@ from spgemm_new_amd.ops import _min_ms  # noqa: E402
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--reps", type=int, default=5)
+    ap.add_argument("--only", default="", help="comma-separated subset of the forms' names")
     a = ap.parse_args()
     dev = torch.device("cuda:0")
     V, E = CONFIGS["proteins"]
@@ -44,8 +45,18 @@ def main():
                                             form="lds"),
         "bwd regs": lambda: g.backward_multi(G, sel, vals, out=dx,
                                              algo=_lib.MAXK_BWD_MULTI_STAGED, form="gather"),
+        "bwd banked": lambda: g.backward_multi(G, sel, vals, out=dx,
+                                               algo=_lib.MAXK_BWD_MULTI_STAGED, form="banked"),
+        "bwd eg lds": lambda: g.backward_multi(G, sel, vals, out=dx,
+                                               algo=_lib.MAXK_BWD_MULTI_EDGE_GATHER, form="lds"),
+        "bwd eg banked": lambda: g.backward_multi(G, sel, vals, out=dx,
+                                                  algo=_lib.MAXK_BWD_MULTI_EDGE_GATHER,
+                                                  form="banked"),
     }
+    only = [x.strip() for x in a.only.split(",") if x.strip()]
     for name, fn in calls.items():
+        if only and name not in only:
+            continue
         print(f"{name}: {_min_ms(fn, reps=a.reps):.3f} ms", flush=True)
 
 
