@@ -666,8 +666,11 @@ def config_sweep(args, dev, only=None):
                           ("multi_staged_regs", _lib.MAXK_BWD_MULTI_STAGED, "gather"),
                           ("multi_edge_gather_lds", _lib.MAXK_BWD_MULTI_EDGE_GATHER, "lds"),
                           ("multi_edge_gather_regs", _lib.MAXK_BWD_MULTI_EDGE_GATHER, "gather"),
+                          ("multi_staged_banked", _lib.MAXK_BWD_MULTI_STAGED, "banked"),
                           ("local_rel8", _lib.MAXK_BWD_LOCAL, "auto")):
             if fm == "gather" and not multi_gather_ok(R, k, h):
+                continue
+            if fm == "banked" and not (R == 8 and k == 32):
                 continue
             cand_b[nm] = round(_min_ms(lambda: g.backward_multi(G, sel, vals, out=dx, algo=a,
                                                                 form=fm)), 4)
