@@ -1,0 +1,51 @@
+#!/usr/bin/env python3
+"""TILE backward time against the plan shape (groups x group size x source
+ranges) on one graph: checks how the time splits between the rows a workgroup
+sweeps and the records it processes.  Development tool.
+
+usage: tools/exp_tile_shape.py [graph] [reps] [G,GS,NS ...]"""
+import os
+import sys
+
+import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+import spgemm_new_amd as S  # noqa: E402
+from spgemm_new_amd import _lib, ops, tile  # noqa: E402
+from spgemm_new_amd.graphs import CONFIGS, synthetic_csr_gpu  # noqa: E402
+
+graph = sys.argv[1] if len(sys.argv) > 1 else "reddit"
+reps = int(sys.argv[2]) if len(sys.argv) > 2 else 10
+shapes = [tuple(int(x) for x in s.split(",")) for s in sys.argv[3:]] or [None]
+K = 32
+dev = torch.device("cuda:0")
+V, E = CONFIGS[graph]
+indptr, indices = synthetic_csr_gpu(V, E, device=dev)
+gen = torch.Generator(device=dev)
+gen.manual_seed(1)
+values = torch.rand(E, generator=gen, device=dev)
+X = torch.rand((V, 256), generator=gen, device=dev)
+G = torch.rand((V, 256), generator=gen, device=dev)
+data, sel = S.topk_cbsr(X, K)
+g = S.MaxKGraph(indptr, indices, values)
+dx = torch.empty((V, K), device=dev)
+ref = None
+for shape in shapes:
+    plan = tile.build(g.indptr, g.indices, g.values, V, V, k=K, shape=shape)
+    if plan is None:
+        print(shape, "no plan", flush=True)
+        continue
+    plan["values_key"], plan["values_ref"] = ops._tensor_key(g.values), g.values
+    NS = plan["splits"]
+    plan["part"] = torch.empty(max(1, (NS - 1) * V * K), device=dev)
+    g._tile[K] = plan
+    g.backward(G, sel, out=dx, algo=_lib.MAXK_BWD_TILE)
+    torch.cuda.synchronize()
+    if ref is None:
+        ref = dx.clone()
+    diff = (dx - ref).abs().max().item()
+    t = ops._min_ms(lambda: g.backward(G, sel, out=dx, algo=_lib.MAXK_BWD_TILE), reps=reps)
+    nch = plan["num_chunks"].float()
+    print(f"{graph} shape {plan['num_groups']} x {plan['group_size']} x {NS} "
+          f"(WGs {plan['num_groups'] * NS}): tile {t:.3f} ms, chunks/WG max {int(nch.max())} "
+          f"mean {nch.mean().item():.0f}, |diff| {diff:.2e}", flush=True)
