@@ -427,21 +427,25 @@ int maxk_sspmm_backward_multi_gather(int algo, const int32_t *sched, int64_t num
 /* ---------------------------------------------------------------------------
  * Backward SSpMM, TILE algorithm (dim_k = 32 or 64, dim_origin = 256): every
  * gradient row is read once per CU into an LDS ring instead of being
- * gathered per edge; destinations' dXs live in registers.  One workgroup per
- * (destination group of <= 2048 (k = 64: 1024) columns, source-row range): grid =
- * num_groups * splits, workgroup b = group b / splits, range b % splits.
- * Inputs from the plan (maxk_tile_plan_build below; format in csrc/maxk_spgemm.hip
- * above bwd_tile_kernel), one stream per (workgroup, wave) w = b * 16 + wave:
- * headers int32[.., 4] from header_start[w] (16-B aligned), records
- * int32[.., 2] from record_start[w] (16-B aligned, padded by 4 KB);
- * num_chunks int32[num_groups * splits]; zero_row: 1 KB of zeros (16-B
- * aligned).  part: fp32[(splits - 1) * num_cols * dim_k] scratch (NULL when
- * splits == 1).  Writes every element of dxs; same result as the other
- * algorithms up to fp32 summation order (deterministic).
+ * gathered per edge; destinations' dXs live in registers.  Destinations are cut
+ * into num_groups groups of group_size <= 2048 (k = 64: 1024) columns; the
+ * (group, source row) space is cut into num_workgroups equal ranges, one per
+ * workgroup (grid = num_workgroups), a range crossing a group boundary being
+ * two or more PIECES run one after the other (csrc/tile_format.h; piece ids
+ * 0 .. num_groups + num_workgroups - 2).  Inputs from the plan
+ * (maxk_tile_plan_build below; format in csrc/maxk_spgemm.hip above
+ * bwd_tile_kernel), one stream per (piece, wave) w = piece * 16 + wave: headers
+ * int32[.., 4] from header_start[w] (16-B aligned), records int32[.., 2|4] from
+ * record_start[w] (16-B aligned, padded by 4 KB); num_chunks int32[pieces];
+ * zero_row: 1 KB of zeros (16-B aligned).  part: fp32[planes * num_cols *
+ * dim_k] scratch, planes = maxk_tile_part_planes (NULL when 0): a group's
+ * later pieces' partial sums, added into dxs in piece order.  Writes every
+ * element of dxs; same result as the other algorithms up to fp32 summation
+ * order (deterministic).
  * ------------------------------------------------------------------------- */
 int maxk_sspmm_backward_tile(const void *headers, const int64_t *header_start,
                              const void *records, const int64_t *record_start,
-                             const int32_t *num_chunks, int num_groups, int splits,
+                             const int32_t *num_chunks, int num_groups, int num_workgroups,
                              int group_size, const float *grad, const float *zero_row,
                              const uint8_t *cbsr_sel, int num_rows, int num_cols, int dim_origin,
                              int dim_k, float *dxs, float *part, void *stream);
@@ -449,31 +453,36 @@ int maxk_sspmm_backward_tile(const void *headers, const int64_t *header_start,
 /* TILE plan, built on the device (spgemm_new_amd/csrc/maxk_plan.hip; no
  * reference counterpart: the reference backward reuses the forward's .warp4
  * chunks, kernels/spmm_maxk_backward.cu:117-139).  CSR with indptr[0] == 0.
- *  maxk_tile_plan_shape: (num_groups, group_size, splits) for num_cus CUs --
- *    groups of <= 2048 (k = 32) / 1024 (k = 64) destinations and source
- *    ranges so that about one workgroup runs per CU.
+ *  maxk_tile_plan_shape: (num_groups, group_size, num_workgroups) for num_cus
+ *    CUs -- groups of <= 2048 (k = 32) / 1024 (k = 64) destinations and S <= 8
+ *    equal source ranges per group (num_workgroups = num_groups * S, one piece
+ *    each) so that about one workgroup runs per CU.  Any other num_workgroups
+ *    is valid (ranges straddling groups), measured slower on Reddit.
  *  maxk_tile_plan_build: call once with headers == NULL (count call): writes
  *    sizes (host int64[3]) = {header entries, records, largest
  *    padded per-segment record count}; the plan is usable only if sizes[2] <=
  *    65535.  Then call with headers int32x4[sizes[0]], header_start
- *    int64[G*S*16], records int32 x maxk_tile_record_words() each [sizes[1]],
- *    record_start int64[G*S*16],
- *    num_chunks int32[G*S] and optionally edge_record int32[E] (the record of
+ *    int64[NP*16], records int32 x maxk_tile_record_words() each [sizes[1]],
+ *    record_start int64[NP*16], num_chunks int32[NP] (NP = num_groups +
+ *    num_workgroups - 1 pieces) and optionally edge_record int32[E] (the record of
  *    each CSR edge, for maxk_tile_plan_set_values).  Both calls synchronise
  *    the stream once.  Deterministic: records keep CSR order per segment.
  *  maxk_tile_plan_set_values: records' values := values (after the graph's
  *    edge values changed; the plan's structure does not depend on them). */
 int maxk_tile_plan_shape(int num_cols, int num_cus, int dim_k, int *num_groups, int *group_size,
-                         int *splits);
+                         int *num_workgroups);
 /* The plan format the library was built with (host out): LDS ring buffers and rows per
  * buffer (chunks hold rows - 1 source rows; the header stream leads by buffers - 1). */
 int maxk_tile_format(int *num_buffers, int *buffer_rows);
 /* int32 words per TILE record in this build (2 or 4; tile_format.h). */
 int maxk_tile_record_words(void);
-size_t maxk_tile_plan_workspace_bytes(int64_t num_edges, int num_workgroups);
+size_t maxk_tile_plan_workspace_bytes(int64_t num_edges, int num_groups, int num_workgroups);
+/* Partial planes the backward needs (fp32[planes * num_cols * dim_k] `part`):
+ * the most pieces any destination group spans, minus one. */
+int maxk_tile_part_planes(int num_rows, int num_groups, int num_workgroups);
 int maxk_tile_plan_build(const int32_t *indptr, const int32_t *indices, const float *values,
                          int num_rows, int num_cols, int64_t num_edges, int dim_k, int num_groups,
-                         int group_size, int splits, void *headers, int64_t header_capacity,
+                         int group_size, int num_workgroups, void *headers, int64_t header_capacity,
                          int64_t *header_start, void *records, int64_t record_capacity,
                          int64_t *record_start, int32_t *num_chunks, int32_t *edge_record,
                          int64_t *sizes, void *workspace, size_t workspace_bytes, void *stream);

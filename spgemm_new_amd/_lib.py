@@ -88,7 +88,8 @@ SIGNATURES = {
     "maxk_spgemm_forward_sum_parts": (_I, [_P, _L, _P, _P, _P, _P, _P, _I, _I, _I, _I, _P, _I, _P, _P, _S, _P]),
     "maxk_tile_plan_shape": (_I, [_I, _I, _I, ctypes.POINTER(_I), ctypes.POINTER(_I),
                                   ctypes.POINTER(_I)]),
-    "maxk_tile_plan_workspace_bytes": (_S, [_L, _I]),
+    "maxk_tile_plan_workspace_bytes": (_S, [_L, _I, _I]),
+    "maxk_tile_part_planes": (_I, [_I, _I, _I]),
     "maxk_tile_plan_build": (_I, [_P, _P, _P, _I, _I, _L, _I, _I, _I, _I, _P, _L, _P, _P, _L, _P,
                                   _P, _P, ctypes.POINTER(ctypes.c_int64), _P, _S, _P]),
     "maxk_tile_plan_set_values": (_I, [_P, _P, _L, _P, _P]),

@@ -361,28 +361,30 @@ void test_graph(const std::string &dir, const std::string &graph, int idx, int c
                 HIPCHECK(hipFree(p));
         }
         if ((k == 32 || k == 64) && E > 0) {
-            int G = 0, GS = 0, NS = 0;
-            MAXKCHECK(maxk_tile_plan_shape(V, prop.multiProcessorCount, k, &G, &GS, &NS));
-            const size_t b = maxk_tile_plan_workspace_bytes(E, G * NS);
+            int G = 0, GS = 0, P = 0;
+            MAXKCHECK(maxk_tile_plan_shape(V, prop.multiProcessorCount, k, &G, &GS, &P));
+            const size_t b = maxk_tile_plan_workspace_bytes(E, G, P);
+            const int NP = G + P - 1;   // plan pieces
             void *ws = dev_alloc<char>(b);
             int64_t sizes[3] = {0, 0, 0};
-            MAXKCHECK(maxk_tile_plan_build(indptr, indices, val, V, V, E, k, G, GS, NS, nullptr, 0,
+            MAXKCHECK(maxk_tile_plan_build(indptr, indices, val, V, V, E, k, G, GS, P, nullptr, 0,
                                            nullptr, nullptr, 0, nullptr, nullptr, nullptr, sizes, ws,
                                            b, st));
             if (sizes[2] <= 0xFFFF) {
-                const int nw = G * NS * 16;
+                const int nw = NP * 16;
                 void *hdrs = dev_alloc<int32_t>((size_t)sizes[0] * 4);
                 void *recs = dev_alloc<int32_t>((size_t)sizes[1] * maxk_tile_record_words());
                 int64_t *hstart = dev_alloc<int64_t>(nw), *rstart = dev_alloc<int64_t>(nw);
-                int32_t *nch = dev_alloc<int32_t>((size_t)G * NS);
-                MAXKCHECK(maxk_tile_plan_build(indptr, indices, val, V, V, E, k, G, GS, NS, hdrs,
+                int32_t *nch = dev_alloc<int32_t>((size_t)NP);
+                MAXKCHECK(maxk_tile_plan_build(indptr, indices, val, V, V, E, k, G, GS, P, hdrs,
                                                sizes[0], hstart, recs, sizes[1], rstart, nch, nullptr,
                                                sizes, ws, b, st));
                 std::vector<float> zeros(kDimOrigin, 0.f);
                 float *zero_row = to_device(zeros);
-                float *part = NS > 1 ? dev_alloc<float>((size_t)(NS - 1) * V * k) : nullptr;
+                const int planes = maxk_tile_part_planes(V, G, P);
+                float *part = planes > 0 ? dev_alloc<float>((size_t)planes * V * k) : nullptr;
                 const double t = time_ms([&] {
-                    MAXKCHECK(maxk_sspmm_backward_tile(hdrs, hstart, recs, rstart, nch, G, NS, GS,
+                    MAXKCHECK(maxk_sspmm_backward_tile(hdrs, hstart, recs, rstart, nch, G, P, GS,
                                                        dense, zero_row, sel, V, V, kDimOrigin, k,
                                                        dxs, part, st));
                 });

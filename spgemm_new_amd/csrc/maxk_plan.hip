@@ -240,10 +240,11 @@ size_t scan_temp_bytes(int64_t n)
 
 // ----------------------------------------------------------------- TILE
 // Plan of bwd_tile_kernel (format above it in maxk_spgemm.hip).  Edge e =
-// (row r, column d): destination group d / GS, source range split(r) (rows
-// cut at floor(s * V / NS)), workgroup wg = group * NS + range.  Within a
-// workgroup, the distinct source rows (ascending) are cut into 47-row chunks;
-// an edge's segment is (wg, wave, chunk, lane half) with wave = (d % GS) % 16.
+// (row r, column d): destination group g = d / GS, piece wg = tile_piece(g, r)
+// (tile_format.h: the (group, row) space cut into P equal workgroup ranges;
+// G + P - 1 piece ids, "wg" below).  Within a piece, the distinct source rows
+// (ascending) are cut into 47-row chunks; an edge's segment is (wg, wave,
+// chunk, lane half) with wave = (d % GS) % 16.
 // Segments are numbered in record-stream order, (wg, wave)-major:
 //   seg = ((chunk_base[wg] * 16 + wave * nch[wg] + chunk) * 2 + half),
 // and within a segment the records keep CSR edge order (two stable sorts).
@@ -252,22 +253,16 @@ constexpr int kTileRecPad = 512;   // records of over-read padding after the str
                                    // kernel's prefetch window is static_asserted against it)
 constexpr int kTileHdrPad = 8;     // header entries of padding
 
-__device__ __forceinline__ int tile_split(int r, int V, int NS)
-{
-    int s = 0;
-    for (int i = 1; i < NS; ++i) s += ((int64_t)i * V / NS) <= r;
-    return s;
-}
-
 __global__ void tile_edge_kernel(const int32_t *__restrict__ indptr, int num_rows,
                                  const int32_t *__restrict__ indices, int64_t num_edges, int GS,
-                                 int NS, int32_t *__restrict__ wg_key, int32_t *__restrict__ erow)
+                                 int G, int P, int32_t *__restrict__ wg_key,
+                                 int32_t *__restrict__ erow)
 {
     const int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (e >= num_edges) return;
     const int r = (int)(upper_bound(indptr, (int64_t)num_rows + 1, e) - 1);
     erow[e] = r;
-    wg_key[e] = (indices[e] / GS) * NS + tile_split(r, num_rows, NS);
+    wg_key[e] = tile_piece(indices[e] / GS, r, num_rows, G, P);
 }
 
 // flag[i] = 1 where the wg-sorted edge i starts a new (workgroup, row) pair
@@ -832,57 +827,81 @@ int maxk_tile_format(int *num_buffers, int *buffer_rows)
 int maxk_tile_record_words(void) { return kTileRecWords; }
 
 int maxk_tile_plan_shape(int num_cols, int num_cus, int dim_k, int *num_groups, int *group_size,
-                         int *splits)
+                         int *num_workgroups)
 {
     if (num_cols < 1 || num_cus < 1 || (dim_k != 32 && dim_k != 64) || !num_groups ||
-        !group_size || !splits)
+        !group_size || !num_workgroups)
         return MAXK_E_ARG;
+    // S equal source ranges per group (num_workgroups = G * S, one piece each):
+    // as many groups as fill about one workgroup per CU.  Workgroup ranges that
+    // straddle groups (num_workgroups = CUs with full groups) balance the rows
+    // swept but measured slower: the workgroups no longer sweep the same rows at
+    // the same time, which the L2 serves once
     int64_t groups = (num_cols + (int64_t)tile_max_group(dim_k) - 1) / tile_max_group(dim_k);
     int64_t ns = num_cus / groups;
     ns = ns < 1 ? 1 : ns > 8 ? 8 : ns;
     // as many groups as the CUs left over allow: smaller groups, same sweep
-    int64_t g2 = num_cus / ns < num_cols ? num_cus / ns : num_cols;
+    const int64_t g2 = num_cus / ns < num_cols ? num_cus / ns : num_cols;
     if (g2 > groups) groups = g2;
     const int64_t size = (num_cols + groups - 1) / groups;
-    *num_groups = (int)((num_cols + size - 1) / size);
+    groups = (num_cols + size - 1) / size;
+    *num_groups = (int)groups;
     *group_size = (int)size;
-    *splits = (int)ns;
+    *num_workgroups = (int)(groups * ns);
     return MAXK_OK;
 }
 
-size_t maxk_tile_plan_workspace_bytes(int64_t num_edges, int num_workgroups)
+int maxk_tile_part_planes(int num_rows, int num_groups, int num_workgroups)
 {
-    if (num_edges < 1 || num_workgroups < 1) return 0;
-    const int64_t bound = tile_seg_bound(num_edges, num_workgroups);
+    if (num_rows < 1 || num_groups < 1 || num_workgroups < 1) return MAXK_E_ARG;
+    int m = 0;
+    for (int g = 0; g < num_groups; ++g) {
+        const int n = tile_group_planes(g, num_rows, num_groups, num_workgroups);
+        m = n > m ? n : m;
+    }
+    return m;
+}
+
+size_t maxk_tile_plan_workspace_bytes(int64_t num_edges, int num_groups, int num_workgroups)
+{
+    if (num_edges < 1 || num_groups < 1 || num_workgroups < 1) return 0;
+    const int64_t np = (int64_t)num_groups + num_workgroups - 1;
+    if (np > INT32_MAX / 2) return 0;
+    const int num_pieces = (int)np;
+    const int64_t bound = tile_seg_bound(num_edges, num_pieces);
     const size_t ea = align_up((size_t)num_edges * 4, 256);
     size_t t = sort_temp_bytes(num_edges, bits_for(bound + 1));
     const size_t t2 = inclusive_scan_temp_bytes(num_edges);
     const size_t t3 = scan64_temp_bytes(bound + 1);
-    const size_t t4 = scan_temp_bytes((int64_t)num_workgroups + 1);
+    const size_t t4 = scan_temp_bytes((int64_t)num_pieces + 1);
     t = t > t2 ? t : t2;
     t = t > t3 ? t : t3;
     t = t > t4 ? t : t4;
-    return 9 * ea + 3 * align_up(((size_t)num_workgroups + 1) * 4, 256) +
+    return 9 * ea + 3 * align_up(((size_t)num_pieces + 1) * 4, 256) +
            align_up((size_t)(bound + 1) * 4, 256) + align_up((size_t)(bound + 1) * 8, 256) + 512 +
            align_up(t, 256) + 256;
 }
 
 int maxk_tile_plan_build(const int32_t *indptr, const int32_t *indices, const float *values,
                          int num_rows, int num_cols, int64_t num_edges, int dim_k, int num_groups,
-                         int group_size, int splits, void *headers, int64_t header_capacity,
-                         int64_t *header_start, void *records, int64_t record_capacity,
-                         int64_t *record_start, int32_t *num_chunks, int32_t *edge_record,
-                         int64_t *sizes, void *workspace, size_t workspace_bytes, void *stream)
+                         int group_size, int num_workgroups, void *headers,
+                         int64_t header_capacity, int64_t *header_start, void *records,
+                         int64_t record_capacity, int64_t *record_start, int32_t *num_chunks,
+                         int32_t *edge_record, int64_t *sizes, void *workspace,
+                         size_t workspace_bytes, void *stream)
 {
     if (!indptr || !indices || !values || !sizes) return MAXK_E_ARG;
     if ((dim_k != 32 && dim_k != 64) || num_rows < 1 || num_cols < 1 || num_edges < 1 ||
-        num_edges > INT32_MAX || num_groups < 1 || splits < 1 || splits > 64 || group_size < 1 ||
-        group_size > tile_max_group(dim_k) || (int64_t)num_groups * group_size < num_cols)
+        num_edges > INT32_MAX || num_groups < 1 || num_workgroups < 1 ||
+        num_workgroups > (1 << 20) || group_size < 1 || group_size > tile_max_group(dim_k) ||
+        (int64_t)num_groups * group_size < num_cols || (int64_t)num_groups + num_workgroups > (1 << 22))
         return MAXK_E_ARG;
-    const int NWG = num_groups * splits;
+    // piece ids (tile_format.h); "workgroup" below is a piece
+    const int NWG = num_groups + num_workgroups - 1;
     const int64_t bound = tile_seg_bound(num_edges, NWG);
     if (bound + 1 > INT32_MAX) return MAXK_E_ARG;
-    if (!workspace || workspace_bytes < maxk_tile_plan_workspace_bytes(num_edges, NWG))
+    if (!workspace ||
+        workspace_bytes < maxk_tile_plan_workspace_bytes(num_edges, num_groups, num_workgroups))
         return MAXK_E_WORKSPACE;
     const bool fill = headers != nullptr;
     if (fill && (!records || !header_start || !record_start || !num_chunks)) return MAXK_E_ARG;
@@ -915,7 +934,7 @@ int maxk_tile_plan_build(const int32_t *indptr, const int32_t *indices, const fl
     int rc;
 
     hipLaunchKernelGGL(tile_edge_kernel, dim3(eb), dim3(kThreads), 0, st, indptr, num_rows, indices,
-                       E, group_size, splits, key, erow);
+                       E, group_size, num_groups, num_workgroups, key, erow);
     if ((rc = launch_status())) return rc;
     tb = tmp_bytes;
     e = rocprim::radix_sort_pairs(tmp, tb, key, wgs, iota, perm, (size_t)E, 0u, bits_for(NWG), st);

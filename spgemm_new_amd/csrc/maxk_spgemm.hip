@@ -3399,241 +3399,309 @@ __device__ __forceinline__ void tile_prefetch(const uint32_t *p, uint32_t &d)
 // BDMA: the DMA pieces by range-checked buffer loads (tile_bdma3: offsets from
 // the header VGPRs, ~6 SALU per chunk) instead of one 64-bit address select per
 // piece (~9 SALU each); needs the gradient below 4 GiB - 1 KiB.
+struct TileArgs {
+    const tile_hdr_t *hdrs;
+    const int64_t *hdr_start;
+    const uint32_t *recs;
+    const int64_t *rec_start;
+    const int32_t *num_chunks;
+    const float *grad;
+    const float *zero_row;
+    const uint8_t *sel;
+    float *dxs;
+    float *part;
+    int num_cols, group_size, num_groups, num_wgs, num_rows;
+};
+using TileArgsK = __attribute__((address_space(4))) const TileArgs;
+
+// The kernel's arguments read where they are used, from the kernarg segment
+// (scalar loads), through a pointer the compiler cannot see through: values
+// used once per piece are not kept in SGPRs across the ring loop, which needs
+// all of them (kept live across the piece loop they spilled)
+__device__ __forceinline__ TileArgsK *tile_args()
+{
+    uint64_t p = reinterpret_cast<uint64_t>(__builtin_amdgcn_kernarg_segment_ptr());
+    asm volatile("" : "+s"(p));
+    return reinterpret_cast<TileArgsK *>(p);
+}
+
 template <int K, bool BDMA>
-__global__ __launch_bounds__(kTileWaves * kWave) void bwd_tile_kernel(
-    const tile_hdr_t *__restrict__ hdrs, const int64_t *__restrict__ hdr_start,
-    const uint32_t *__restrict__ recs, const int64_t *__restrict__ rec_start,
-    const int32_t *__restrict__ num_chunks, const float *__restrict__ grad,
-    const float *__restrict__ zero_row, const uint8_t *__restrict__ sel, int num_cols,
-    int group_size, int splits, float *__restrict__ dxs, float *__restrict__ part, int num_rows)
+__global__ __launch_bounds__(kTileWaves * kWave) void bwd_tile_kernel(const TileArgs)
 {
     __shared__ __attribute__((aligned(16))) float tb[kTileBufs * kTileBufRows * kMaxDim];
-    const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    const int lane = lane_id(), half = K == 32 ? lane >> 5 : 0, ent = lane & (K - 1);
-    const uint64_t lo = K == 32 ? 0x00000000ffffffffull : ~0ull;
-    const uint64_t hi = K == 32 ? 0xffffffff00000000ull : ~0ull;
-    auto dest_of = [&](int slot) { return (K == 32 ? 2 * slot + half : slot) * kTileWaves + wv; };
-    const int split = blockIdx.x % splits, grp = blockIdx.x / splits;
-    const int d0 = grp * group_size;
-    const int nd = min(group_size, num_cols - d0);
-    // selectors of the group's destinations, staged through LDS (tb is free
-    // until the first DMA); slot s = 4t + b of this wave holds destination
-    // (2s + half) * 16 + wv, byte b of selector word t
+    // this workgroup's range of the (group, source row) space: the pieces of
+    // groups g_first .. g_last (tile_format.h), one after the other.  The
+    // piece loop's state lives in LDS, not in registers: the ring loop below
+    // uses every SGPR and VGPR a wave has (state in registers spilled)
+    __shared__ int tstate[kTileWaves][4];  // next group, last group, workgroup
     {
-        uint8_t *sb = reinterpret_cast<uint8_t *>(tb);
-        constexpr int U = K / 16;  // 16-B units per selector row; 4096 units either way
-        for (int i = threadIdx.x; i < 64 * kTileWaves * 4; i += kTileWaves * kWave) {
-            const int j = i / U;
-            uint4 v = {0u, 0u, 0u, 0u};
-            if (j < nd) v = *reinterpret_cast<const uint4 *>(sel + (size_t)(d0 + j) * K + (i % U) * 16);
-            *reinterpret_cast<uint4 *>(sb + (size_t)i * 16) = v;
+        const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+        TileArgsK *A = tile_args();
+        const int wg = blockIdx.x, num_rows = A->num_rows;
+        const int64_t gv = (int64_t)A->num_groups * num_rows;
+        const int64_t x0 = tile_wg_start(wg, gv, A->num_wgs);
+        const int64_t x1 = tile_wg_start(wg + 1, gv, A->num_wgs);
+        if (x1 <= x0) return;
+        if (lane_id() == 0) {
+            tstate[wv][0] = (int)(x0 / num_rows);
+            tstate[wv][1] = (int)((x1 - 1) / num_rows);
+            tstate[wv][2] = wg;
+        }
+    }
+    for (;;) {
+        // lane constants recomputed per piece from an opaque copy: hoisted out of
+        // this loop, the values derived from them (selector and output addresses)
+        // stayed live across it and spilled
+        const int lane = lane_id();
+        int lane_o = lane;
+        asm volatile("" : "+v"(lane_o));
+        const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+        const int half = K == 32 ? lane_o >> 5 : 0, ent = lane_o & (K - 1);
+        const uint64_t lo = K == 32 ? 0x00000000ffffffffull : ~0ull;
+        const uint64_t hi = K == 32 ? 0xffffffff00000000ull : ~0ull;
+        auto dest_of = [&](int slot) { return (K == 32 ? 2 * slot + half : slot) * kTileWaves + wv; };
+        TileArgsK *A = tile_args();
+        const int grp = __builtin_amdgcn_readfirstlane(tstate[wv][0]);
+        const int wg = __builtin_amdgcn_readfirstlane(tstate[wv][2]);
+        if (lane == 0) tstate[wv][0] = grp + 1;
+        const int pid = grp + wg;
+        const int plane = wg - (int)((int64_t)grp * A->num_wgs / A->num_groups);
+        const int d0 = grp * A->group_size;
+        const int nd = min(A->group_size, A->num_cols - d0);
+        const uint8_t *__restrict__ sel = A->sel;
+        const float *__restrict__ grad = A->grad;
+        const float *__restrict__ zero_row = A->zero_row;
+        const int num_rows = A->num_rows;
+        // selectors of the group's destinations, staged through LDS (tb is free
+        // until the first DMA); slot s = 4t + b of this wave holds destination
+        // (2s + half) * 16 + wv, byte b of selector word t
+        {
+            uint8_t *sb = reinterpret_cast<uint8_t *>(tb);
+            constexpr int U = K / 16;  // 16-B units per selector row; 4096 units either way
+            for (int i = threadIdx.x; i < 64 * kTileWaves * 4; i += kTileWaves * kWave) {
+                const int j = i / U;
+                uint4 v = {0u, 0u, 0u, 0u};
+                if (j < nd) v = *reinterpret_cast<const uint4 *>(sel + (size_t)(d0 + j) * K + (i % U) * 16);
+                *reinterpret_cast<uint4 *>(sb + (size_t)i * 16) = v;
+            }
+            __syncthreads();
+        }
+        tile_sel_t selv;
+#pragma unroll
+        for (int t = 0; t < 16; ++t) {
+            const uint8_t *sb = reinterpret_cast<const uint8_t *>(tb);
+            uint32_t word = 0;
+#pragma unroll
+            for (int b = 0; b < 4; ++b)
+                word |= (uint32_t)sb[dest_of(4 * t + b) * K + ent] << (8 * b);
+            selv[t] = word;
+            asm volatile("" ::: "memory");  // four LDS reads in flight at a time
         }
         __syncthreads();
-    }
-    tile_sel_t selv;
+        tile_acc_t acc0 = 0.f, acc1 = 0.f;
+        const uint32_t tb_base = (uint32_t)reinterpret_cast<uintptr_t>(tb);
+        const int bw = pid * kTileWaves + wv;
+        const tile_hdr_t *hs = A->hdrs + A->hdr_start[bw];
+        const uint32_t *rb = A->recs + kTileRecWords * A->rec_start[bw];
+        uint32_t ro = 0;  // byte offset of the next record group in this wave's stream
+        const int nch = A->num_chunks[pid];
+        // raw buffer descriptor of the gradient: base, stride 0, num_records = its bytes
+        const uint64_t gbase = reinterpret_cast<uint64_t>(grad);
+        const tile_rsrc_t rsrc = {(int32_t)(uint32_t)gbase, (int32_t)(uint32_t)(gbase >> 32) & 0xffff,
+                                  BDMA ? (int32_t)((uint32_t)num_rows * 1024u) : 0, 0x00020000};
+        const uint32_t lane16 = (uint32_t)lane * 16u;
+        // pieces of rows wv*3 .. wv*3+2 of the chunk's buffer (48 rows = 16 waves x 3)
+        static_assert(!BDMA || kTileWaves * kTilePieces == kTileBufRows, "consecutive piece rows");
+        auto bdma = [&](int c, const tile_hdr_t &h) {
+            const uint32_t buf = tb_base + (uint32_t)(c % kTileBufs) * kTileBufRows * 1024u +
+                                 (uint32_t)wv * 3u * 1024u;
+            tile_bdma3(rsrc, ((uint32_t)h.y << 10) + lane16, ((uint32_t)h.z << 10) + lane16,
+                       ((uint32_t)h.w << 10) + lane16, __builtin_amdgcn_readfirstlane(buf));
+        };
+        auto dma = [&](int c, int r0, int r1, int r2) {
+            static_assert(kTilePieces == 3, "three DMA pieces per wave and chunk");
+            const uint32_t buf = tb_base + (uint32_t)(c % kTileBufs) * kTileBufRows * 1024u;
+            const int rows[3] = {r0, r1, r2};
 #pragma unroll
-    for (int t = 0; t < 16; ++t) {
-        const uint8_t *sb = reinterpret_cast<const uint8_t *>(tb);
-        uint32_t word = 0;
-#pragma unroll
-        for (int b = 0; b < 4; ++b)
-            word |= (uint32_t)sb[dest_of(4 * t + b) * K + ent] << (8 * b);
-        selv[t] = word;
-        asm volatile("" ::: "memory");  // four LDS reads in flight at a time
-    }
-    __syncthreads();
-    tile_acc_t acc0 = 0.f, acc1 = 0.f;
-    const uint32_t tb_base = (uint32_t)reinterpret_cast<uintptr_t>(tb);
-    const int bw = blockIdx.x * kTileWaves + wv;
-    const tile_hdr_t *hs = hdrs + hdr_start[bw];
-    const uint32_t *rb = recs + kTileRecWords * rec_start[bw];
-    uint32_t ro = 0;  // byte offset of the next record group in this wave's stream
-    const int nch = num_chunks[blockIdx.x];
-    // raw buffer descriptor of the gradient: base, stride 0, num_records = its bytes
-    const uint64_t gbase = reinterpret_cast<uint64_t>(grad);
-    const tile_rsrc_t rsrc = {(int32_t)(uint32_t)gbase, (int32_t)(uint32_t)(gbase >> 32) & 0xffff,
-                              BDMA ? (int32_t)((uint32_t)num_rows * 1024u) : 0, 0x00020000};
-    const uint32_t lane16 = (uint32_t)lane * 16u;
-    // pieces of rows wv*3 .. wv*3+2 of the chunk's buffer (48 rows = 16 waves x 3)
-    static_assert(!BDMA || kTileWaves * kTilePieces == kTileBufRows, "consecutive piece rows");
-    auto bdma = [&](int c, const tile_hdr_t &h) {
-        const uint32_t buf = tb_base + (uint32_t)(c % kTileBufs) * kTileBufRows * 1024u +
-                             (uint32_t)wv * 3u * 1024u;
-        tile_bdma3(rsrc, ((uint32_t)h.y << 10) + lane16, ((uint32_t)h.z << 10) + lane16,
-                   ((uint32_t)h.w << 10) + lane16, __builtin_amdgcn_readfirstlane(buf));
-    };
-    auto dma = [&](int c, int r0, int r1, int r2) {
-        static_assert(kTilePieces == 3, "three DMA pieces per wave and chunk");
-        const uint32_t buf = tb_base + (uint32_t)(c % kTileBufs) * kTileBufRows * 1024u;
-        const int rows[3] = {r0, r1, r2};
-#pragma unroll
-        for (int i = 0; i < 3; ++i) {
-            const int r = __builtin_amdgcn_readfirstlane(rows[i]);
-            const float *src = r >= 0 ? grad + (size_t)r * kMaxDim : zero_row;
-            // pieces past the buffer's rows (a ring of fewer than 48-row buffers)
-            // all write the zero row again: same bytes, same place
-            const int row = wv * 3 + i < kTileBufRows ? wv * 3 + i : kTileBufRows - 1;
-            tile_glds(src + lane * 4,
-                      __builtin_amdgcn_readfirstlane(buf + (uint32_t)row * 1024u));
-        }
-    };
-    // records about 1 KB ahead pulled into L2 for the s_loads (one load per chunk)
-    uint32_t pf = 0;
+            for (int i = 0; i < 3; ++i) {
+                const int r = __builtin_amdgcn_readfirstlane(rows[i]);
+                const float *src = r >= 0 ? grad + (size_t)r * kMaxDim : zero_row;
+                // pieces past the buffer's rows (a ring of fewer than 48-row buffers)
+                // all write the zero row again: same bytes, same place
+                const int row = wv * 3 + i < kTileBufRows ? wv * 3 + i : kTileBufRows - 1;
+                tile_glds(src + lane * 4,
+                          __builtin_amdgcn_readfirstlane(buf + (uint32_t)row * 1024u));
+            }
+        };
+        // records about 1 KB ahead pulled into L2 for the s_loads (one load per chunk)
+        uint32_t pf = 0;
 #ifndef TILE_PF_AHEAD
 #define TILE_PF_AHEAD 128  // dwords: the window starts 512 B past the chunk's records
 #endif
 #ifndef TILE_KPF
-// record groups 3 and 4 pulled into the scalar cache with the first two (0 or 2; 4
-// measured no better): Reddit k=32 2.81 -> 2.78 ms
+    // record groups 3 and 4 pulled into the scalar cache with the first two (0 or 2; 4
+    // measured no better): Reddit k=32 2.81 -> 2.78 ms
 #define TILE_KPF 2
 #endif
 #ifndef TILE_ABLATE
 #define TILE_ABLATE 0  // development timing ablations (results wrong): bits 1 / 2 / 4 / 8 below
 #endif
-    // the window must stay inside the record stream's padding: 512 records =
-    // 1024 dwords after the last wave's stream (kTileRecPad in maxk_plan.hip)
-    static_assert(TILE_PF_AHEAD + 4 * kWave <= kTileRecWords * 512,
-                  "TILE prefetch past the record padding");
+        // the window must stay inside the record stream's padding: 512 records =
+        // 1024 dwords after the last wave's stream (kTileRecPad in maxk_plan.hip)
+        static_assert(TILE_PF_AHEAD + 4 * kWave <= kTileRecWords * 512,
+                      "TILE prefetch past the record padding");
 #ifndef TILE_NO_PREFETCH
-    auto prefetch = [&]() { tile_prefetch(rb + (ro >> 2) + TILE_PF_AHEAD + lane * 4, pf); };
+        auto prefetch = [&]() { tile_prefetch(rb + (ro >> 2) + TILE_PF_AHEAD + lane * 4, pf); };
 #else
-    auto prefetch = [&]() {};
+        auto prefetch = [&]() {};
 #endif
-    // header e(i) = {n0 | n1 << 16 of chunk i - L, the wave's DMA rows of chunk i},
-    // L = kTileLead; queue: H(L); per "iteration" i = -L, ..., -1, 0, 1, ...:
-    // DMA(i + L), H(i + 2L + 1), prefetch -- so every step issues the same ops
-    tile_hdr_t e[kTileLead];   // plain loads, waited for by the compiler before any DMA
+        // header e(i) = {n0 | n1 << 16 of chunk i - L, the wave's DMA rows of chunk i},
+        // L = kTileLead; queue: H(L); per "iteration" i = -L, ..., -1, 0, 1, ...:
+        // DMA(i + L), H(i + 2L + 1), prefetch -- so every step issues the same ops
+        tile_hdr_t e[kTileLead];   // plain loads, waited for by the compiler before any DMA
 #pragma unroll
-    for (int i = 0; i < kTileLead; ++i) e[i] = hs[i];
-    tile_hdr_t hh[kTileBufs];
-    hh[0] = tile_load_hdr(hs + kTileLead);
+        for (int i = 0; i < kTileLead; ++i) e[i] = hs[i];
+        tile_hdr_t hh[kTileBufs];
+        hh[0] = tile_load_hdr(hs + kTileLead);
 #pragma unroll
-    for (int i = 0; i < kTileLead; ++i) {
-        if constexpr (BDMA)
-            bdma(i, e[i]);
-        else
-            dma(i, e[i].y, e[i].z, e[i].w);
-        hh[i + 1] = tile_load_hdr(hs + kTileLead + 1 + i);
-        prefetch();
-    }
-    auto step = [&](int c, tile_hdr_t &h) {
-        // the chunk's first record groups, in flight across the barrier (four-word
-        // records: pinned to s[64:79] / s[80:95], where the record asm reads them)
-        tile_g16_t pa, pb;
+        for (int i = 0; i < kTileLead; ++i) {
+            if constexpr (BDMA)
+                bdma(i, e[i]);
+            else
+                dma(i, e[i].y, e[i].z, e[i].w);
+            hh[i + 1] = tile_load_hdr(hs + kTileLead + 1 + i);
+            prefetch();
+        }
+        auto step = [&](int c, tile_hdr_t &h) {
+            // the chunk's first record groups, in flight across the barrier (four-word
+            // records: pinned to s[64:79] / s[80:95], where the record asm reads them)
+            tile_g16_t pa, pb;
 #if TILE_KPF
-        // groups 3..2+TILE_KPF pulled into the scalar cache with the first two, so
-        // that the loop's s_loads hit it (their lgkmcnt waits also wait for the
-        // LDS reads; a K$ hit keeps that short); dummies stay live to the wait
-        uint32_t kp[4];
-        const uint32_t *rp = rb + (ro >> 2);
-        if constexpr (kTileRecWords == 4)
-            asm volatile("s_load_dwordx16 s[64:79], %6, 0x0\n\t"
-                         "s_load_dwordx16 s[80:95], %6, 0x40\n\t"
-                         "s_load_dword %2, %6, 0x80\n\t"
-                         "s_load_dword %3, %6, 0xc0\n\t"
-                         ".if %7 > 2\n\t"
-                         "s_load_dword %4, %6, 0x100\n\t"
-                         "s_load_dword %5, %6, 0x140\n\t"
-                         ".endif"
-                         : "=&{s[64:79]}"(pa), "=&{s[80:95]}"(pb), "=&s"(kp[0]), "=&s"(kp[1]),
-                           "=&s"(kp[2]), "=&s"(kp[3])
-                         : "s"(rp), "n"(TILE_KPF) : "memory");
-        else
+            // groups 3..2+TILE_KPF pulled into the scalar cache with the first two, so
+            // that the loop's s_loads hit it (their lgkmcnt waits also wait for the
+            // LDS reads; a K$ hit keeps that short); dummies stay live to the wait
+            uint32_t kp[4];
+            const uint32_t *rp = rb + (ro >> 2);
+            if constexpr (kTileRecWords == 4)
+                asm volatile("s_load_dwordx16 s[64:79], %6, 0x0\n\t"
+                             "s_load_dwordx16 s[80:95], %6, 0x40\n\t"
+                             "s_load_dword %2, %6, 0x80\n\t"
+                             "s_load_dword %3, %6, 0xc0\n\t"
+                             ".if %7 > 2\n\t"
+                             "s_load_dword %4, %6, 0x100\n\t"
+                             "s_load_dword %5, %6, 0x140\n\t"
+                             ".endif"
+                             : "=&{s[64:79]}"(pa), "=&{s[80:95]}"(pb), "=&s"(kp[0]), "=&s"(kp[1]),
+                               "=&s"(kp[2]), "=&s"(kp[3])
+                             : "s"(rp), "n"(TILE_KPF) : "memory");
+            else
 #else
-        if constexpr (kTileRecWords == 4)
-            asm volatile("s_load_dwordx16 s[64:79], %2, %3\n\ts_load_dwordx16 s[80:95], %2, %4"
-                         : "=&{s[64:79]}"(pa), "=&{s[80:95]}"(pb)
-                         : "s"(rb), "s"(ro), "s"(ro + 64) : "memory");
-        else
+            if constexpr (kTileRecWords == 4)
+                asm volatile("s_load_dwordx16 s[64:79], %2, %3\n\ts_load_dwordx16 s[80:95], %2, %4"
+                             : "=&{s[64:79]}"(pa), "=&{s[80:95]}"(pb)
+                             : "s"(rb), "s"(ro), "s"(ro + 64) : "memory");
+            else
 #endif
-            asm volatile("s_load_dwordx16 %0, %2, %3\n\ts_load_dwordx16 %1, %2, %4"
-                         : "=&s"(pa), "=&s"(pb) : "s"(rb), "s"(ro), "s"(ro + 64) : "memory");
-        // this wave's DMA of chunk c and header of chunk c landed; after the
-        // barrier everyone's have, and chunk c-1's buffer is free
+                asm volatile("s_load_dwordx16 %0, %2, %3\n\ts_load_dwordx16 %1, %2, %4"
+                             : "=&s"(pa), "=&s"(pb) : "s"(rb), "s"(ro), "s"(ro + 64) : "memory");
+            // this wave's DMA of chunk c and header of chunk c landed; after the
+            // barrier everyone's have, and chunk c-1's buffer is free
 #if TILE_ABLATE & 1  // timing ablation (wrong results): no chunk barrier
-        asm volatile("s_waitcnt vmcnt(%2)" : "+v"(h), "+v"(pf) : "n"(kTileVmcnt) : "memory");
+            asm volatile("s_waitcnt vmcnt(%2)" : "+v"(h), "+v"(pf) : "n"(kTileVmcnt) : "memory");
 #else
-        asm volatile("s_waitcnt vmcnt(%2)\n\ts_barrier" : "+v"(h), "+v"(pf) : "n"(kTileVmcnt)
-                     : "memory");
+            asm volatile("s_waitcnt vmcnt(%2)\n\ts_barrier" : "+v"(h), "+v"(pf) : "n"(kTileVmcnt)
+                         : "memory");
 #endif
-        const uint32_t cnt = (uint32_t)__builtin_amdgcn_readfirstlane(h.x);
-        // (every step must issue exactly 3 DMA + 1 header load + 1 prefetch: the
-        // counted vmcnt above relies on it.  A step that issues fewer lets the wave
-        // read a header that has not landed -> garbage record counts -> s_loads past
-        // the record stream -> memory-access fault; measured with a "no DMA" ablation.)
-        if constexpr (BDMA)
-            bdma(c + kTileLead, h);
-        else
-            dma(c + kTileLead, __builtin_amdgcn_readfirstlane(h.y),
-                __builtin_amdgcn_readfirstlane(h.z), __builtin_amdgcn_readfirstlane(h.w));
-        h = tile_load_hdr(hs + c + 2 * kTileLead + 1);
-        prefetch();
-        const uint32_t g0n = (cnt & 0xffffu) >> 2, gn = g0n + (cnt >> 18);
-        uint32_t n = 0u - gn, m = 0u - g0n;
+            const uint32_t cnt = (uint32_t)__builtin_amdgcn_readfirstlane(h.x);
+            // (every step must issue exactly 3 DMA + 1 header load + 1 prefetch: the
+            // counted vmcnt above relies on it.  A step that issues fewer lets the wave
+            // read a header that has not landed -> garbage record counts -> s_loads past
+            // the record stream -> memory-access fault; measured with a "no DMA" ablation.)
+            if constexpr (BDMA)
+                bdma(c + kTileLead, h);
+            else
+                dma(c + kTileLead, __builtin_amdgcn_readfirstlane(h.y),
+                    __builtin_amdgcn_readfirstlane(h.z), __builtin_amdgcn_readfirstlane(h.w));
+            h = tile_load_hdr(hs + c + 2 * kTileLead + 1);
+            prefetch();
+            const uint32_t g0n = (cnt & 0xffffu) >> 2, gn = g0n + (cnt >> 18);
+            uint32_t n = 0u - gn, m = 0u - g0n;
 #if TILE_ABLATE & 2  // timing ablation: no record processing
-        n = 0u;
-        m = 0u;
+            n = 0u;
+            m = 0u;
 #endif
-        // the record groups must have landed before anything reads (or copies)
-        // their SGPRs -- also when this chunk has no records: a skipped wait let
-        // the next step's s_loads into the same SGPRs race with these (SMEM
-        // returns out of order), i.e. stale records, on graphs with empty
-        // wave-chunks (products k=32: runs differed in the last bits)
-        if constexpr (kTileRecWords == 4) {
+            // the record groups must have landed before anything reads (or copies)
+            // their SGPRs -- also when this chunk has no records: a skipped wait let
+            // the next step's s_loads into the same SGPRs race with these (SMEM
+            // returns out of order), i.e. stale records, on graphs with empty
+            // wave-chunks (products k=32: runs differed in the last bits)
+            if constexpr (kTileRecWords == 4) {
 #if TILE_KPF
-            asm volatile("s_waitcnt lgkmcnt(0)" : "+{s[64:79]}"(pa), "+{s[80:95]}"(pb),
-                         "+s"(kp[0]), "+s"(kp[1]), "+s"(kp[2]), "+s"(kp[3])::"memory");
+                asm volatile("s_waitcnt lgkmcnt(0)" : "+{s[64:79]}"(pa), "+{s[80:95]}"(pb),
+                             "+s"(kp[0]), "+s"(kp[1]), "+s"(kp[2]), "+s"(kp[3])::"memory");
 #else
-            asm volatile("s_waitcnt lgkmcnt(0)" : "+{s[64:79]}"(pa), "+{s[80:95]}"(pb)::"memory");
+                asm volatile("s_waitcnt lgkmcnt(0)" : "+{s[64:79]}"(pa), "+{s[80:95]}"(pb)::"memory");
 #endif
-            tile_groups2_r16(pa, pb, n, m, lo, hi, selv, acc0, acc1);
-            tile_group_loop_r16(rb, ro + 128, n, m, lo, hi, selv, acc0, acc1);
-            ro += 64 * gn;
-            return;
-        }
-        asm volatile("s_waitcnt lgkmcnt(0)" : "+s"(pa), "+s"(pb)::"memory");
-        uint32_t ga[16], gb[16];
+                tile_groups2_r16(pa, pb, n, m, lo, hi, selv, acc0, acc1);
+                tile_group_loop_r16(rb, ro + 128, n, m, lo, hi, selv, acc0, acc1);
+                ro += 64 * gn;
+                return;
+            }
+            asm volatile("s_waitcnt lgkmcnt(0)" : "+s"(pa), "+s"(pb)::"memory");
+            uint32_t ga[16], gb[16];
 #pragma unroll
-        for (int i = 0; i < 16; ++i) {
-            ga[i] = pa[i];
-            gb[i] = pb[i];
-        }
-        tile_groups2(ga, n, m, lo, hi, selv, acc0, acc1);
+            for (int i = 0; i < 16; ++i) {
+                ga[i] = pa[i];
+                gb[i] = pb[i];
+            }
+            tile_groups2(ga, n, m, lo, hi, selv, acc0, acc1);
 #if TILE_ABLATE & 8  // timing ablation: the first two record groups only
-        n = 0u;
+            n = 0u;
 #endif
-        tile_groups2(gb, n, m, lo, hi, selv, acc0, acc1);
+            tile_groups2(gb, n, m, lo, hi, selv, acc0, acc1);
 #if TILE_ABLATE & 4  // timing ablation: the four record groups loaded before the barrier only
-        n = 0u;
+            n = 0u;
 #endif
-        tile_group_loop(rb, ro + 128, n, m, lo, hi, selv, acc0, acc1);
-        ro += 32 * gn;
-    };
-    for (int c = 0; c < nch; c += kTileBufs) {
+            tile_group_loop(rb, ro + 128, n, m, lo, hi, selv, acc0, acc1);
+            ro += 32 * gn;
+        };
+        for (int c = 0; c < nch; c += kTileBufs) {
 #pragma unroll
-        for (int j = 0; j < kTileBufs; ++j)
-            if (c + j < nch) step(c + j, hh[j]);
-    }
-    asm volatile("s_waitcnt vmcnt(0)" : "+v"(pf)::"memory");
+            for (int j = 0; j < kTileBufs; ++j)
+                if (c + j < nch) step(c + j, hh[j]);
+        }
+        asm volatile("s_waitcnt vmcnt(0)" : "+v"(pf)::"memory");
 #pragma unroll
-    for (int j = 0; j < kTileBufs; ++j) asm volatile("" : "+v"(hh[j])::"memory");
-    float *out = split == 0 ? dxs : part + (size_t)(split - 1) * num_cols * K;
+        for (int j = 0; j < kTileBufs; ++j) asm volatile("" : "+v"(hh[j])::"memory");
+        TileArgsK *Z = tile_args();
+        float *out = plane == 0 ? Z->dxs : Z->part + (size_t)(plane - 1) * Z->num_cols * K;
 #pragma unroll
-    for (int s = 0; s < 64; ++s) {
-        const int j = dest_of(s);
-        if (j < nd) out[(size_t)(d0 + j) * K + ent] = s < 32 ? acc0[s] : acc1[s - 32];
+        for (int s = 0; s < 64; ++s) {
+            const int j = dest_of(s);
+            if (j < nd) out[(size_t)(d0 + j) * K + ent] = s < 32 ? acc0[s] : acc1[s - 32];
+        }
+        if (__builtin_amdgcn_readfirstlane(tstate[wv][0]) >
+            __builtin_amdgcn_readfirstlane(tstate[wv][1]))
+            break;
+        __syncthreads();   // every wave's ring reads of this piece are done
     }
 }
 
-// dxs += sum of the partial rows of source ranges 1 .. splits-1
+// dxs += the partial planes of each destination's group (tile_group_planes of
+// them, in plane order: deterministic)
 __global__ __launch_bounds__(kBlock) void tile_combine_kernel(float *__restrict__ dxs,
                                                               const float *__restrict__ part,
-                                                              int nparts, int64_t n4)
+                                                              int64_t n4, int k, int group_size,
+                                                              int num_rows, int num_groups,
+                                                              int num_wgs)
 {
     for (int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x; i < n4;
          i += (int64_t)gridDim.x * kBlock) {
+        const int g = (int)(i * 4 / k) / group_size;
+        const int np = tile_group_planes(g, num_rows, num_groups, num_wgs);
+        if (np == 0) continue;
         f4 a = reinterpret_cast<f4 *>(dxs)[i];
-        for (int p = 0; p < nparts; ++p) a += reinterpret_cast<const f4 *>(part)[(int64_t)p * n4 + i];
+        for (int p = 0; p < np; ++p) a += reinterpret_cast<const f4 *>(part)[(int64_t)p * n4 + i];
         reinterpret_cast<f4 *>(dxs)[i] = a;
     }
 }
@@ -4943,17 +5011,20 @@ int maxk_sspmm_backward_local_rel8(const int32_t *seg_edge_off, int num_segments
 
 int maxk_sspmm_backward_tile(const void *headers, const int64_t *header_start,
                              const void *records, const int64_t *record_start,
-                             const int32_t *num_chunks, int num_groups, int splits,
+                             const int32_t *num_chunks, int num_groups, int num_workgroups,
                              int group_size, const float *grad, const float *zero_row,
                              const uint8_t *cbsr_sel, int num_rows, int num_cols, int dim_origin,
                              int dim_k, float *dxs, float *part, void *stream)
 {
     if ((dim_k != 32 && dim_k != 64) || dim_origin != kMaxDim) return MAXK_E_DIM;
     if (!headers || !header_start || !records || !record_start || !num_chunks || !grad ||
-        !zero_row || !cbsr_sel || !dxs || num_groups < 1 || splits < 1 || group_size < 1 ||
+        !zero_row || !cbsr_sel || !dxs || num_groups < 1 || num_workgroups < 1 ||
+        num_workgroups > (1 << 20) || group_size < 1 ||
         group_size > (dim_k == 32 ? 128 : 64) * kTileWaves || num_rows < 1 || num_cols < 1 ||
-        (int64_t)num_groups * group_size < num_cols || (splits > 1 && !part))
+        (int64_t)num_groups * group_size < num_cols)
         return MAXK_E_ARG;
+    const int planes = maxk_tile_part_planes(num_rows, num_groups, num_workgroups);
+    if (planes > 0 && !part) return MAXK_E_ARG;
     if ((reinterpret_cast<uintptr_t>(headers) | reinterpret_cast<uintptr_t>(records) |
          reinterpret_cast<uintptr_t>(grad) | reinterpret_cast<uintptr_t>(zero_row) |
          reinterpret_cast<uintptr_t>(dxs) | reinterpret_cast<uintptr_t>(part) |
@@ -4969,16 +5040,18 @@ int maxk_sspmm_backward_tile(const void *headers, const int64_t *header_start,
     const bool bdma = !gdma && (int64_t)num_rows * 1024 <= (int64_t)0xFFFFFC00u - 1024;
     auto kern = dim_k == 32 ? (bdma ? bwd_tile_kernel<32, true> : bwd_tile_kernel<32, false>)
                             : (bdma ? bwd_tile_kernel<64, true> : bwd_tile_kernel<64, false>);
-    hipLaunchKernelGGL(kern, dim3((unsigned)(num_groups * splits)), dim3(kTileWaves * kWave), 0, st,
-                       reinterpret_cast<const tile_hdr_t *>(headers), header_start,
-                       reinterpret_cast<const uint32_t *>(records), record_start, num_chunks, grad,
-                       zero_row, cbsr_sel, num_cols, group_size, splits, dxs, part, num_rows);
+    const TileArgs args = {reinterpret_cast<const tile_hdr_t *>(headers), header_start,
+                           reinterpret_cast<const uint32_t *>(records), record_start, num_chunks,
+                           grad, zero_row, cbsr_sel, dxs, part, num_cols, group_size, num_groups,
+                           num_workgroups, num_rows};
+    hipLaunchKernelGGL(kern, dim3((unsigned)num_workgroups), dim3(kTileWaves * kWave), 0, st, args);
     int rc = launch_status();
-    if (rc || splits == 1) return rc;
+    if (rc || planes == 0) return rc;
     const int64_t n4 = (int64_t)num_cols * dim_k / 4;
     const int64_t blocks = ceil_div(n4, kBlock);
     hipLaunchKernelGGL(tile_combine_kernel, dim3((unsigned)(blocks < 4096 ? blocks : 4096)),
-                       dim3(kBlock), 0, st, dxs, part, splits - 1, n4);
+                       dim3(kBlock), 0, st, dxs, part, n4, dim_k, group_size, num_rows, num_groups,
+                       num_workgroups);
     return launch_status();
 }
 

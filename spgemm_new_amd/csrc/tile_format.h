@@ -41,4 +41,34 @@ static_assert(kTileWaves * kTilePieces >= kTileBufRows, "every buffer row has a 
 static_assert(kTileBufs >= 2 && kTileBufs * kTileBufRows <= 160, "ring fits the 160 KB of LDS");
 static_assert((kTileBufs - 1) * kTileBufRows + kTileRows < 256, "row field of a record is 8 bits");
 
+// Pieces (round 4): the (destination group g, source row r) space, x = g * V + r
+// over G groups and V source rows, is cut into P equal ranges, one per
+// workgroup b: [x_b, x_{b+1}) with x_b = ceil(b * G * V / P).  A workgroup
+// whose range crosses a group boundary finishes one group's rows and starts the
+// next group's.  The piece of (g, r) is p = g + b(x), b(x) = floor(x * P / (G * V)):
+// ids 0 .. G + P - 2 (an id whose workgroup holds none of its group's rows has
+// no edges).  Group g's pieces lie in workgroups b0(g) = floor(g * P / G) ..
+// b1(g) = b((g + 1) * V - 1); piece b0 writes dXs, piece b0 + i partial plane
+// i - 1 (summed into dXs afterwards, in plane order).  P = G * S cuts every
+// group into S equal source ranges (the round-3 "splits").
+__host__ __device__ inline int tile_wg_of(int64_t x, int64_t gv, int P)
+{
+    return (int)(x * P / gv);
+}
+__host__ __device__ inline int64_t tile_wg_start(int64_t b, int64_t gv, int P)
+{
+    return (b * gv + P - 1) / P;
+}
+__host__ __device__ inline int tile_piece(int g, int r, int V, int G, int P)
+{
+    const int64_t gv = (int64_t)G * V;
+    return g + tile_wg_of((int64_t)g * V + r, gv, P);
+}
+// extra partial planes of group g (its pieces - 1)
+__host__ __device__ inline int tile_group_planes(int g, int V, int G, int P)
+{
+    const int64_t gv = (int64_t)G * V;
+    return tile_wg_of((int64_t)(g + 1) * V - 1, gv, P) - (int)((int64_t)g * P / G);
+}
+
 #endif

@@ -487,8 +487,9 @@ class MaxKGraph:
                 cus = torch.cuda.get_device_properties(self.device).multi_processor_count
                 shape = None
                 if self.tile_splits is not None:
+                    # S equal source ranges per group: G * S workgroups
                     G, GS, _ = tile.choose_shape(self.num_cols, cus, dim_k)
-                    shape = (G, GS, max(1, int(self.tile_splits)))
+                    shape = (G, GS, G * max(1, int(self.tile_splits)))
                 plan = tile.build(self.indptr, self.indices[: self.num_edges],
                                   self.values[: self.num_edges], self.num_rows, self.num_cols,
                                   cus=cus, k=dim_k, shape=shape)
@@ -497,8 +498,7 @@ class MaxKGraph:
                 # address cannot be reused by another tensor with the same key)
                 plan["values_key"] = _tensor_key(self.values)
                 plan["values_ref"] = self.values
-                G, NS = plan["num_groups"], plan["splits"]
-                plan["part"] = torch.empty(max(1, (NS - 1) * self.num_cols * dim_k),
+                plan["part"] = torch.empty(max(1, plan["part_planes"] * self.num_cols * dim_k),
                                            dtype=torch.float32, device=self.device)
             self._tile[dim_k] = plan
         return self._tile[dim_k]
@@ -1314,13 +1314,13 @@ def sspmm_backward(g: MaxKGraph, grad, sel, out=None, values=None, algo: int = _
             raise RuntimeError("TILE backward unsupported for this shape (k = 32 or 64, h = 256)")
         g.tile_values(plan, values)   # the records' values (refreshed when they changed)
         g.last_bwd_algo = "tile"
-        NS = plan["splits"]
         _lib.check(L.maxk_sspmm_backward_tile(
             plan["headers"].data_ptr(), plan["header_start"].data_ptr(),
             plan["records"].data_ptr(), plan["record_start"].data_ptr(),
-            plan["num_chunks"].data_ptr(), plan["num_groups"], NS, plan["group_size"],
-            grad.data_ptr(), plan["zero_row"].data_ptr(), sel.data_ptr(), g.num_rows, g.num_cols,
-            dim_origin, k, out.data_ptr(), plan["part"].data_ptr() if NS > 1 else None,
+            plan["num_chunks"].data_ptr(), plan["num_groups"], plan["num_workgroups"],
+            plan["group_size"], grad.data_ptr(), plan["zero_row"].data_ptr(), sel.data_ptr(),
+            g.num_rows, g.num_cols, dim_origin, k, out.data_ptr(),
+            plan["part"].data_ptr() if plan["part_planes"] > 0 else None,
             _stream(out)), "maxk_sspmm_backward_tile")
         return out
     if algo == _lib.MAXK_BWD_LOCAL:

@@ -8,13 +8,17 @@ module builds, once per graph, the streams the kernel walks:
 * destinations are cut into ``num_groups`` groups of ``group_size`` <= 2048
   columns; in a group, destination j belongs to wave ``j % 16``, slot
   ``(j // 16) >> 1`` and lane half ``(j // 16) & 1``;
-* source rows are cut into ``splits`` equal ranges; workgroup
-  ``b = group * splits + range``;
-* a workgroup's distinct source rows (those with an edge into its group, in
+* the (group, source row) space x = g * V + r is cut into ``num_workgroups``
+  (P) equal ranges, one per workgroup; a range crossing a group boundary holds
+  one PIECE of each group it touches, run one after the other; the piece of
+  (g, r) is g + floor(x * P / (G * V)) (ids 0 .. G + P - 2, csrc/tile_format.h);
+  a group's first piece writes dXs, its later ones partial planes summed in
+  afterwards (P = G * S: S equal source ranges per group);
+* a piece's distinct source rows (those with an edge into its group, in
   ascending order) are cut into chunks of C = BR - 1 rows; chunk c sits in LDS
   buffer ``c % NB`` of a ring of NB buffers of BR rows, the last row of every
   buffer a zero row (NB, BR from ``ring_format()``; 3 x 48 by default);
-* per (workgroup, wave) a header stream of int32x4 entries: e(0) .. e(L-1) =
+* per (piece, wave) a header stream of int32x4 entries: e(0) .. e(L-1) =
   {0, rows of chunks 0 .. L-1}, then e(c + L) = {n0 | n1 << 16 of chunk c, rows
   of chunk c + L}, L = NB - 1, where "rows" are the source rows of the wave's
   three DMA pieces (rows 3w .. 3w+2 of the chunk; -1 = the zero row);
@@ -66,9 +70,9 @@ def max_group(k: int) -> int:
 
 
 def choose_shape(num_cols: int, cus: int = 256, k: int = 32) -> tuple[int, int, int]:
-    """(num_groups, group_size, splits): groups of <= max_group(k) destinations,
-    and source ranges so that num_groups * splits fills about one workgroup per
-    CU (maxk_tile_plan_shape)."""
+    """(num_groups, group_size, num_workgroups): groups of <= max_group(k)
+    destinations and S equal source ranges each (num_workgroups = groups * S),
+    about one workgroup per CU (maxk_tile_plan_shape)."""
     L = _lib.load()
     g, s, n = ctypes.c_int(0), ctypes.c_int(0), ctypes.c_int(0)
     _lib.check(L.maxk_tile_plan_shape(num_cols, cus, k, ctypes.byref(g), ctypes.byref(s),
@@ -88,17 +92,17 @@ def build(indptr: torch.Tensor, indices: torch.Tensor, values: torch.Tensor, num
     E = indices.numel()
     if E == 0 or num_rows < 1 or num_cols < 1 or k not in (32, 64):
         return None
-    G, GS, NS = shape or choose_shape(num_cols, cus, k)
+    G, GS, P = shape or choose_shape(num_cols, cus, k)
     if GS > max_group(k):
         return None
     L = _lib.load()
-    NWG = G * NS
-    ws = torch.empty(max(1, L.maxk_tile_plan_workspace_bytes(E, NWG)), dtype=torch.uint8,
+    NWG = G + P - 1          # pieces
+    ws = torch.empty(max(1, L.maxk_tile_plan_workspace_bytes(E, G, P)), dtype=torch.uint8,
                      device=dev)
     st = _lib.stream_ptr(dev)
     sizes = (ctypes.c_int64 * 3)()
     args = (indptr.data_ptr(), indices.data_ptr(), values.data_ptr(), num_rows, num_cols, E, k,
-            G, GS, NS)
+            G, GS, P)
     _lib.check(L.maxk_tile_plan_build(*args, None, 0, None, None, 0, None, None, None, sizes,
                                       ws.data_ptr(), ws.numel(), st), "maxk_tile_plan_build(count)")
     if sizes[2] > 0xFFFF:
@@ -117,9 +121,28 @@ def build(indptr: torch.Tensor, indices: torch.Tensor, values: torch.Tensor, num
     del ws
     return {"headers": hdrs, "header_start": hstart, "records": recs, "record_start": rstart,
             "num_chunks": nch, "edge_record": edge_record,
-            "num_groups": G, "group_size": GS, "splits": NS, "num_rows": num_rows,
-            "num_cols": num_cols, "k": k,
+            "num_groups": G, "group_size": GS, "num_workgroups": P, "num_rows": num_rows,
+            "num_cols": num_cols, "k": k, "part_planes": part_planes(num_rows, G, P),
             "zero_row": torch.zeros(256, dtype=torch.float32, device=dev)}
+
+
+def part_planes(num_rows: int, num_groups: int, num_workgroups: int) -> int:
+    """Partial planes the backward needs: the most pieces a group spans - 1."""
+    return max(0, max(_group_planes(g, num_rows, num_groups, num_workgroups)
+                      for g in range(num_groups)))
+
+
+def _group_planes(g: int, V: int, G: int, P: int) -> int:
+    return ((g + 1) * V - 1) * P // (G * V) - g * P // G
+
+
+def pieces_of(b: int, V: int, G: int, P: int):
+    """(piece id, group, plane) of workgroup b's pieces, in run order."""
+    gv = G * V
+    x0, x1 = -(-b * gv // P), -(-(b + 1) * gv // P)
+    if x1 <= x0:
+        return []
+    return [(g + b, g, b - g * P // G) for g in range(x0 // V, (x1 - 1) // V + 1)]
 
 
 def set_values(plan, values: torch.Tensor) -> None:
@@ -142,19 +165,19 @@ def emulate(plan, grad: torch.Tensor, sel: torch.Tensor) -> torch.Tensor:
     hs = plan["header_start"].cpu().tolist()
     rs = plan["record_start"].cpu().tolist()
     nch = plan["num_chunks"].cpu().tolist()
-    G, GS, NS, C = plan["num_groups"], plan["group_size"], plan["splits"], plan["num_cols"]
+    G, GS, P, C = plan["num_groups"], plan["group_size"], plan["num_workgroups"], plan["num_cols"]
+    V = plan["num_rows"]
     grad = grad.cpu().float()
     sel = sel.cpu().long()
     K = plan.get("k", 32)
-    out = torch.zeros(NS, C, K)
+    out = torch.zeros(part_planes(V, G, P) + 1, C, K)
     if K == 32:
         jj = (2 * torch.arange(64)[:, None] + torch.arange(64)[None, :] // 32) * WAVES  # [slot, lane]
     else:
         jj = torch.arange(64)[:, None].expand(64, 64) * WAVES
     ent = torch.arange(64)[None, :] % K
     lds = torch.zeros(NB * BR * 256)
-    for b in range(G * NS):
-        sp, g = b % NS, b // NS
+    for b, g, sp in (pc for w in range(P) for pc in pieces_of(w, V, G, P)):
         d0 = g * GS
         nd = min(GS, C - d0)
         acc = torch.zeros(WAVES, 64, 64)

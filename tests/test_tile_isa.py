@@ -9,6 +9,8 @@ disassembles the built library's gfx950 code object and checks every
 specialisation: each step barrier is preceded by vmcnt(kTileVmcnt), the code
 between consecutive step barriers issues exactly kTilePieces + 2 VMEM loads, no
 scratch is used, and the barrier count is the unrolled ring.
+Round 4: the kernel loops over the pieces of its workgroup range; the piece
+loop must not push the ring loop into spills (checked: no scratch).
 """
 import os
 import re
@@ -77,15 +79,21 @@ def test_tile_step_vmem_count(tmp_path):
     assert len(funcs) == 4, list(funcs)          # K in {32, 64} x {buffer, global} DMA
     for name, lines in funcs.items():
         assert not any(SCRATCH.search(ln) for ln in lines), f"{name}: scratch in the TILE kernel"
-        steps = []
+        steps, barriers = [], []
         for i, ln in enumerate(lines):
             if "s_barrier" in ln and i > 0:
-                m = re.search(r"s_waitcnt vmcnt\((\d+)\)", lines[i - 1])
+                barriers.append(i)
+                # the step barrier's own wait (the record asm: a bare counted vmcnt);
+                # the compiler's waits before __syncthreads name other counters too
+                m = re.search(r"s_waitcnt vmcnt\((\d+)\)\s*$", lines[i - 1])
                 if m:
                     assert int(m.group(1)) == VMCNT, (name, lines[i - 1])
                     steps.append(i)
         assert len(steps) == NBUF, (name, len(steps))   # the ring's steps, unrolled
-        for a, b_ in zip(steps, steps[1:] + [len(lines)]):
+        # a step's code runs to the next barrier (the last step's: to the piece's
+        # closing barrier, or the end)
+        ends = [next((j for j in barriers if j > a), len(lines)) for a in steps]
+        for a, b_ in zip(steps, ends):
             loads = [ln.strip() for ln in lines[a:b_] if LOAD.search(" " + ln + " ")]
             assert len(loads) == STEP_OPS, (name, loads)
             dma = [ln for ln in loads if " lds" in ln or "load_lds" in ln]

@@ -35,10 +35,12 @@ def _inputs(V, C, seed, k=32, h=256):
 
 @pytest.mark.parametrize("k", [32, 64])
 @pytest.mark.parametrize("V,C,deg,shape,hubs", [
-    (300, 300, 12, None, 0),           # one group, splits up to 8, several chunks
+    (300, 300, 12, None, 0),           # one group, 8 source ranges, several chunks
     (800, 800, 6, None, 12),           # hub rows: chunks cut short where records pile up
-    (500, 2600, 9, None, 0),           # two groups (> 2048 columns)
-    (700, 900, 20, (3, 300, 2), 0),    # forced: 3 groups of 300, 2 source ranges
+    (500, 2600, 9, None, 0),           # groups > 2048 columns
+    (700, 900, 20, (3, 300, 6), 0),    # forced: 3 groups of 300, 2 equal source ranges each
+    (700, 900, 20, (3, 300, 4), 0),    # forced: 4 workgroups over 3 groups (pieces straddle)
+    (900, 2500, 8, (3, 834, 7), 0),    # forced: 7 workgroups over 3 groups
     (200, 64, 4, (1, 64, 1), 0),       # few destinations, one range
 ])
 def test_plan_emulated_matches_oracle(oracle, V, C, deg, shape, hubs, k):
@@ -61,7 +63,7 @@ def test_plan_invariants():
     indptr, idx, vals = _graph(V, C, 15, seed=3)
     plan = tile_ref.build(torch.from_numpy(indptr), torch.from_numpy(idx), torch.from_numpy(vals),
                           V, C, cus=8)
-    G, GS, NS = plan["num_groups"], plan["group_size"], plan["splits"]
+    G, GS, P = plan["num_groups"], plan["group_size"], plan["num_workgroups"]
     assert G * GS >= C and GS <= tile.max_group(32)
     hdrs, recs = plan["headers"], plan["records"]
     hs, rs = plan["header_start"].tolist(), plan["record_start"].tolist()
@@ -69,7 +71,7 @@ def test_plan_invariants():
     NB, BR, _ = tile.ring_format()
     lead = NB - 1
     n_real = 0
-    for b in range(G * NS):
+    for b in range(G + P - 1):
         for wv in range(tile.WAVES):
             ro = rs[b * tile.WAVES + wv]
             for c in range(nch[b] + lead):
@@ -106,8 +108,9 @@ _KEYS = ("headers", "header_start", "records", "record_start", "num_chunks")
 @pytest.mark.parametrize("k", [32, 64])
 @pytest.mark.parametrize("V,C,deg,shape,hubs", [
     (300, 300, 12, None, 0), (800, 800, 6, None, 12), (500, 2600, 9, None, 0),
-    (700, 900, 20, (3, 300, 2), 0), (200, 64, 4, (1, 64, 1), 0), (3000, 3000, 40, None, 0),
-    (4000, 1500, 30, (2, 750, 5), 0), (1, 5, 3, None, 0),
+    (700, 900, 20, (3, 300, 6), 0), (700, 900, 20, (3, 300, 4), 0), (200, 64, 4, (1, 64, 1), 0),
+    (3000, 3000, 40, None, 0), (4000, 1500, 30, (2, 750, 10), 0),
+    (4000, 1500, 30, (2, 750, 9), 0), (1, 5, 3, None, 0),
 ])
 def test_device_plan_matches_reference_builder(dev, V, C, deg, shape, hubs, k):
     """maxk_tile_plan_build (device) == the torch reference builder, bit for
@@ -121,7 +124,7 @@ def test_device_plan_matches_reference_builder(dev, V, C, deg, shape, hubs, k):
     assert (got is None) == (ref is None)
     if got is None:
         return
-    for key in ("num_groups", "group_size", "splits"):
+    for key in ("num_groups", "group_size", "num_workgroups", "part_planes"):
         assert got[key] == ref[key], key
     for key in _KEYS:
         a, b = got[key].cpu(), ref[key].cpu().to(got[key].dtype)
@@ -320,10 +323,10 @@ def test_tile_backward_gpu_matches_oracle(dev, oracle, V, C, deg, k):
     assert torch.equal(got, again)
     loc = g.backward(G, sl, algo=_lib.MAXK_BWD_LOCAL)
     assert (got - loc).abs().max().item() <= 1e-4 * max(1.0, loc.abs().max().item())
-    if g.tile_plan(k)["splits"] == 1:
-        # one source range: TILE adds each destination's edges in source-row
-        # order, one FMA per edge, as LOCAL does -> bit-identical.  With
-        # splits > 1 the ranges' partial sums are added at the end instead.
+    if g.tile_plan(k)["part_planes"] == 0:
+        # one piece per group: TILE adds each destination's edges in source-row
+        # order, one FMA per edge, as LOCAL does -> bit-identical.  With more
+        # pieces their partial sums are added at the end instead.
         assert torch.equal(got, loc)
 
 

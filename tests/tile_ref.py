@@ -8,7 +8,7 @@ from __future__ import annotations
 
 import torch
 
-from spgemm_new_amd.tile import WAVES, ring_format
+from spgemm_new_amd.tile import WAVES, part_planes, ring_format
 
 
 def max_group(k: int) -> int:
@@ -16,15 +16,16 @@ def max_group(k: int) -> int:
 
 
 def choose_shape(num_cols: int, cus: int = 256, k: int = 32) -> tuple[int, int, int]:
-    """(num_groups, group_size, splits): groups of <= 2048 destinations, and
-    source ranges so that num_groups * splits fills about one workgroup per CU."""
+    """(num_groups, group_size, num_workgroups): groups of <= 2048 destinations
+    and S equal source ranges each (num_workgroups = groups * S) so that about
+    one workgroup runs per CU."""
     groups = -(-num_cols // max_group(k))
     splits = max(1, min(8, cus // groups))
     # as many groups as the CUs left over allow: smaller groups, same sweep
     groups = max(groups, min(cus // splits, num_cols))
     size = -(-num_cols // groups)
     groups = -(-num_cols // size)
-    return groups, size, splits
+    return groups, size, groups * splits
 
 
 def build(indptr: torch.Tensor, indices: torch.Tensor, values: torch.Tensor, num_rows: int,
@@ -45,10 +46,10 @@ def build(indptr: torch.Tensor, indices: torch.Tensor, values: torch.Tensor, num
         return None
     if k not in (32, 64):
         return None
-    G, GS, NS = shape or choose_shape(num_cols, cus, k)
+    G, GS, P = shape or choose_shape(num_cols, cus, k)
     if GS > max_group(k):
         return None
-    NWG = G * NS
+    NWG = G + P - 1          # pieces (spgemm_new_amd/tile.py)
     V = num_rows
     i64 = dict(dtype=torch.int64, device=dev)
     deg = (indptr[1:] - indptr[:-1]).long()
@@ -62,10 +63,8 @@ def build(indptr: torch.Tensor, indices: torch.Tensor, values: torch.Tensor, num
         slot, half = q >> 1, q & 1
     else:                                  # k = 64: one destination per slot register
         slot, half = q, torch.zeros_like(q)
-    bounds = (torch.arange(NS + 1, **i64) * V) // NS
-    split = torch.bucketize(rows, bounds[1:NS], right=True)
-    wg = grp * NS + split
-    del d, j, q, grp, split
+    wg = grp + (grp * V + rows) * P // (G * V)
+    del d, j, q, grp
     # distinct source rows per workgroup, and each edge's row index in that list
     key = wg * V + rows
     ukey, inv = torch.unique(key, sorted=True, return_inverse=True)
@@ -150,6 +149,6 @@ def build(indptr: torch.Tensor, indices: torch.Tensor, values: torch.Tensor, num
     hdrs[hp, 3] = r3[:, 2].to(torch.int32)
     return {"headers": hdrs, "header_start": hstart.contiguous(), "records": recs,
             "record_start": rstart.contiguous(), "num_chunks": nch.to(torch.int32).contiguous(),
-            "num_groups": G, "group_size": GS, "splits": NS, "num_rows": V, "num_cols": num_cols,
-            "k": k,
+            "num_groups": G, "group_size": GS, "num_workgroups": P, "num_rows": V,
+            "num_cols": num_cols, "k": k, "part_planes": part_planes(V, G, P),
             "zero_row": torch.zeros(256, dtype=torch.float32, device=dev)}

@@ -71,7 +71,7 @@ def main():
             t = timed(lambda: e.backward(g_l, sall, out=dx, algo=_lib.MAXK_BWD_TILE))
             p = e.tile_plan(k)
             tl = timed(lambda: e.backward(g_l, sall, out=dx, algo=_lib.MAXK_BWD_LOCAL))
-            print(f"world={world} tile shape {(p['num_groups'], p['group_size'], p['splits'])}: "
+            print(f"world={world} tile shape {(p['num_groups'], p['group_size'], p['num_workgroups'])}: "
                   f"bwd tile {t:.3f} ms (local {tl:.3f})", flush=True)
             del m, e
             torch.cuda.empty_cache()

@@ -149,7 +149,7 @@ def main():
                 e = getattr(m, nm, None)
                 if e is not None and hasattr(e, "_tile"):
                     tp = {kk: (None if v is None else (v["num_groups"], v["group_size"],
-                                                       v["splits"]))
+                                                       v["num_workgroups"]))
                           for kk, v in e._tile.items()}
                     print(f"   {nm}: rows {e.num_rows} cols {e.num_cols} edges {e.num_edges} "
                           f"tile plans {tp} bwd choice {e._bwd_choice} "
@@ -200,7 +200,7 @@ def breakdown_single(graph="reddit", k=32, world=8, rank=0):
     e = m.local
     print(f"{graph} k={k} world={world} rank={rank} single block: own={p.num_own} "
           f"halo={p.num_halo} edges={e.num_edges} bwd {e.last_bwd_algo} fwd blocks "
-          f"{e._fwd_blocks} tile {[(kk, None if v is None else (v['num_groups'], v['group_size'], v['splits'])) for kk, v in e._tile.items()]}")
+          f"{e._fwd_blocks} tile {[(kk, None if v is None else (v['num_groups'], v['group_size'], v['num_workgroups'])) for kk, v in e._tile.items()]}")
     for name, fn in rows.items():
         print(f"  {name:40s} {timed(fn, reps=20):.3f} ms", flush=True)
 

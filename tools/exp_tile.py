@@ -47,7 +47,7 @@ print(f"{graph}: plan {time.time() - t0:.2f} s", flush=True)
 if plan is None:
     print("no TILE plan (segment overflow)")
     sys.exit(0)
-print(f"  groups {plan['num_groups']} x {plan['group_size']}, splits {plan['splits']}, "
+print(f"  groups {plan['num_groups']} x {plan['group_size']}, workgroups {plan['num_workgroups']}, "
       f"chunks/WG max {int(plan['num_chunks'].max())} mean "
       f"{plan['num_chunks'].float().mean().item():.0f}, records {plan['records'].shape[0] / 1e6:.1f} M "
       f"({plan['records'].shape[0] / E:.2f} per edge)", flush=True)

@@ -27,7 +27,7 @@ data, sel = random_cbsr(V, k, 256, seed=3)
 sel = torch.from_numpy(sel).to(dev)
 G = torch.rand((V, 256), device=dev)
 plan = g.tile_plan(k)
-print("plan", plan["num_groups"], plan["group_size"], plan["splits"])
+print("plan", plan["num_groups"], plan["group_size"], plan["num_workgroups"])
 dt = g.backward(G, sel, algo=_lib.MAXK_BWD_TILE)
 ds = g.backward(G, sel, algo=_lib.MAXK_BWD_STAGED)
 torch.cuda.synchronize()

@@ -1,9 +1,10 @@
 #!/usr/bin/env python3
-"""TILE backward time against the plan shape (groups x group size x source
-ranges) on one graph: checks how the time splits between the rows a workgroup
-sweeps and the records it processes.  Development tool.
+"""TILE backward time against the plan shape (groups x group size x
+workgroups) on one graph: checks how the time splits between the rows a
+workgroup sweeps and the records it processes.  Development tool.
 
-usage: tools/exp_tile_shape.py [graph] [reps] [G,GS,NS ...]"""
+usage: tools/exp_tile_shape.py [graph] [reps] [G,GS,P ...]  (P = G * S: S equal
+source ranges per group; other P: pieces straddling groups)"""
 import os
 import sys
 
@@ -36,8 +37,8 @@ for shape in shapes:
         print(shape, "no plan", flush=True)
         continue
     plan["values_key"], plan["values_ref"] = ops._tensor_key(g.values), g.values
-    NS = plan["splits"]
-    plan["part"] = torch.empty(max(1, (NS - 1) * V * K), device=dev)
+    P = plan["num_workgroups"]
+    plan["part"] = torch.empty(max(1, plan["part_planes"] * V * K), device=dev)
     g._tile[K] = plan
     g.backward(G, sel, out=dx, algo=_lib.MAXK_BWD_TILE)
     torch.cuda.synchronize()
@@ -46,6 +47,8 @@ for shape in shapes:
     diff = (dx - ref).abs().max().item()
     t = ops._min_ms(lambda: g.backward(G, sel, out=dx, algo=_lib.MAXK_BWD_TILE), reps=reps)
     nch = plan["num_chunks"].float()
-    print(f"{graph} shape {plan['num_groups']} x {plan['group_size']} x {NS} "
-          f"(WGs {plan['num_groups'] * NS}): tile {t:.3f} ms, chunks/WG max {int(nch.max())} "
-          f"mean {nch.mean().item():.0f}, |diff| {diff:.2e}", flush=True)
+    per_wg = [sum(int(nch[pc[0]]) for pc in tile.pieces_of(w, V, plan["num_groups"], P))
+              for w in range(P)]
+    print(f"{graph} shape {plan['num_groups']} x {plan['group_size']} over {P} WGs "
+          f"(planes {plan['part_planes']}): tile {t:.3f} ms, chunks/WG max {max(per_wg)} "
+          f"mean {sum(per_wg) / len(per_wg):.0f}, |diff| {diff:.2e}", flush=True)
