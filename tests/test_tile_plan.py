@@ -101,6 +101,32 @@ def test_shape_library_matches_reference(C, cus, k):
     assert tile.choose_shape(C, cus, k) == tile_ref.choose_shape(C, cus, k)
 
 
+@pytest.mark.parametrize("V,G,P", [(1, 1, 1), (300, 1, 8), (300, 3, 4), (900, 3, 7), (232_965, 128, 256),
+                                   (232_965, 114, 256), (232_965, 128, 240), (2_449_029, 2392, 2392),
+                                   (10, 7, 64)])
+def test_part_planes_and_pieces(V, G, P):
+    """maxk_tile_part_planes (C ABI, host code) == the Python piece formula, and
+    the pieces of all workgroups tile the (group, row) space exactly once, each
+    group's pieces in consecutive workgroups with planes 0, 1, ..."""
+    from spgemm_new_amd import _lib
+    assert _lib.load().maxk_tile_part_planes(V, G, P) == tile.part_planes(V, G, P)
+    seen = {}
+    for b in range(P):
+        for pid, g, plane in tile.pieces_of(b, V, G, P):
+            assert pid == g + b and 0 <= g < G
+            seen.setdefault(g, []).append((b, plane))
+    assert sorted(seen) == list(range(G))
+    for g, lst in seen.items():
+        assert [pl for _, pl in lst] == list(range(len(lst)))
+        assert [b for b, _ in lst] == list(range(lst[0][0], lst[0][0] + len(lst)))
+        assert len(lst) - 1 <= tile.part_planes(V, G, P)
+    # rows: piece of (g, r) from the plan formula covers every row exactly once
+    if V * G <= 5000:
+        for g in range(G):
+            pids = {g + (g * V + r) * P // (G * V) for r in range(V)}
+            assert pids == {pid for b in range(P) for pid, gg, _ in tile.pieces_of(b, V, G, P) if gg == g}
+
+
 _KEYS = ("headers", "header_start", "records", "record_start", "num_chunks")
 
 
