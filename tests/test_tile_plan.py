@@ -411,6 +411,37 @@ def test_tile_one_range_is_sequential_fma(dev, k):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("k", [32, 64])
+@pytest.mark.parametrize("V,C,deg,P", [(3000, 3000, 40, 5), (3000, 5000, 30, 7), (2000, 4500, 25, 4),
+                                       (1500, 1500, 20, 63)])
+def test_tile_backward_straddling_pieces(dev, oracle, V, C, deg, P, k):
+    """Workgroup ranges that straddle destination groups (P not a multiple of
+    the group count): a workgroup runs two or more pieces, each group's later
+    pieces go to partial planes summed per group -- equal to the oracle, and
+    bitwise reproducible."""
+    import spgemm_new_amd as S
+    from spgemm_new_amd import _lib, ops
+    indptr, idx, vals = _graph(V, C, deg, seed=V + C + P)
+    grad, sel = _inputs(V, C, seed=V + P, k=k)
+    g = S.MaxKGraph(torch.from_numpy(indptr).to(dev), torch.from_numpy(idx).to(dev),
+                    torch.from_numpy(vals).to(dev), num_cols=C)
+    G = -(-C // tile.max_group(k))
+    G = max(G, 2)
+    plan = tile.build(g.indptr, g.indices, g.values, V, C, shape=(G, -(-C // G), P), k=k)
+    assert plan is not None and plan["num_workgroups"] == P
+    assert any(len(tile.pieces_of(b, V, G, P)) > 1 for b in range(P))
+    plan["values_key"], plan["values_ref"] = ops._tensor_key(g.values), g.values
+    plan["part"] = torch.empty(max(1, plan["part_planes"] * C * k), device=dev)
+    g._tile[k] = plan
+    Gt, sl = torch.from_numpy(grad).to(dev), torch.from_numpy(sel).to(dev)
+    got = g.backward(Gt, sl, algo=_lib.MAXK_BWD_TILE)
+    assert g.last_bwd_algo == "tile"
+    ref = oracle.np_backward(indptr, idx, vals, grad, sel)
+    assert oracle.parity_error(got.cpu().numpy(), ref) < TOL
+    assert torch.equal(got, g.backward(Gt, sl, algo=_lib.MAXK_BWD_TILE))
+
+
+@pytest.mark.gpu
 def test_tile_repeat_calls_with_empty_wave_chunks(dev, oracle):
     """A sparse graph (most wave-chunks hold no records): every step must wait for
     its record loads even when it has nothing to do, or the next step's loads race
