@@ -17,6 +17,9 @@ from spgemm_new_amd.graphs import CONFIGS, synthetic_csr_gpu  # noqa: E402
 
 graph = sys.argv[1] if len(sys.argv) > 1 else "reddit"
 reps = int(sys.argv[2]) if len(sys.argv) > 2 else 10
+world = 1
+if graph.count("/"):                      # e.g. reddit/8: rank 0's row block of world 8
+    graph, world = graph.split("/")[0], int(graph.split("/")[1])
 shapes = [tuple(int(x) for x in s.split(",")) for s in sys.argv[3:]] or [None]
 K = 32
 dev = torch.device("cuda:0")
@@ -26,19 +29,24 @@ gen = torch.Generator(device=dev)
 gen.manual_seed(1)
 values = torch.rand(E, generator=gen, device=dev)
 X = torch.rand((V, 256), generator=gen, device=dev)
-G = torch.rand((V, 256), generator=gen, device=dev)
 data, sel = S.topk_cbsr(X, K)
-g = S.MaxKGraph(indptr, indices, values)
-dx = torch.empty((V, K), device=dev)
+C = V                                     # destination columns (all nodes)
+if world > 1:
+    V = -(-V // world)
+    E = int(indptr[V].item())
+    indptr, indices, values = indptr[: V + 1].contiguous(), indices[:E].contiguous(), values[:E]
+G = torch.rand((V, 256), generator=gen, device=dev)
+g = S.MaxKGraph(indptr, indices, values, num_cols=C)
+dx = torch.empty((C, K), device=dev)
 ref = None
 for shape in shapes:
-    plan = tile.build(g.indptr, g.indices, g.values, V, V, k=K, shape=shape)
+    plan = tile.build(g.indptr, g.indices, g.values, V, C, k=K, shape=shape)
     if plan is None:
         print(shape, "no plan", flush=True)
         continue
     plan["values_key"], plan["values_ref"] = ops._tensor_key(g.values), g.values
     P = plan["num_workgroups"]
-    plan["part"] = torch.empty(max(1, plan["part_planes"] * V * K), device=dev)
+    plan["part"] = torch.empty(max(1, plan["part_planes"] * C * K), device=dev)
     g._tile[K] = plan
     g.backward(G, sel, out=dx, algo=_lib.MAXK_BWD_TILE)
     torch.cuda.synchronize()
