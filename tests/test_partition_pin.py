@@ -162,6 +162,7 @@ def _rel_err(a, b):
 
 
 @pytest.mark.gpu
+@pytest.mark.timeout(900)   # up to 8 spawned ranks time-share one card: minutes on a busy box
 @pytest.mark.parametrize("graph,world,R", [("products", 2, 1), ("products", 4, 1),
                                            ("products", 8, 1), ("proteins", 8, 8)])
 def test_partitioned_rows_match_single_gpu(graph, world, R, tmp_path, tmp_path_factory):
