@@ -70,6 +70,9 @@ def parse():
                         "(Flickr on the CPU, products k in {8,16,32,64}, proteins R=8)")
     p.add_argument("--configs-only", default=None,
                    help="comma list of sweep entries to run (flickr_cpu,products_k8,...,proteins_r8)")
+    p.add_argument("--config-steps", type=int, default=20,
+                   help="timed steps per config entry (at least 20 by default; fewer only for "
+                        "rehearsals of the plumbing)")
     return p.parse_args()
 
 
@@ -705,6 +708,174 @@ def config_sweep(args, dev, only=None):
     return out
 
 
+def _dist_step_ms(fn, steps, warmup, dist, dev):
+    """Whole-job ms per call of `fn` on every rank: `warmup` untimed calls, then
+    `steps` timed ones bracketed by synchronize + barrier on both sides, the MAX
+    over ranks of the elapsed time (the headline's protocol)."""
+    for _ in range(warmup):
+        fn()
+    torch.cuda.synchronize()
+    dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        fn()
+    torch.cuda.synchronize()
+    dist.barrier()
+    tt = torch.tensor([time.perf_counter() - t0], device=dev, dtype=torch.float64)
+    dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+    return float(tt) / steps * 1e3
+
+
+def _dist_call_stats(calls, steps, dist, dev):
+    """Per-call HIP-event times on each rank (_timed_calls, no extra warm-up),
+    then per call the MAX over ranks of the mean and of the median (ms)."""
+    ts = _timed_calls(calls, steps, 0)
+    t = torch.tensor([v for xs in ts for v in (sum(xs) / len(xs), _median(xs))], device=dev,
+                     dtype=torch.float64)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    t = t.tolist()
+    return [{"mean_max_over_ranks": round(t[2 * i], 4), "median_max_over_ranks": round(t[2 * i + 1], 4)}
+            for i in range(len(calls))]
+
+
+def _dist_sum(dist, dev, *xs):
+    t = torch.tensor(xs, device=dev, dtype=torch.float64)
+    dist.all_reduce(t)
+    return t.tolist()
+
+
+def partitioned_configs(args, dev, world, rank, dist, kw):
+    """BASELINE configs 4 and 5 in the same N > 1 launch as the headline (VERDICT
+    r4 item 1): the row-partitioned products h=256 k=32 step (config 4:
+    forward + backward with their halo exchanges) and the row-partitioned
+    proteins R=8 step (config 5: fused multi-relation forward + multi-relation
+    backward).  Each rank builds only its own row block of the N=1 graph (hashed
+    columns and values), times the step with the headline's protocol (barrier +
+    synchronize both sides, max over ranks), and checks the adjoint identity
+    sum_ranks <Y, G> = sum_ranks <X^_s, dXs> over the whole graph (fp64).  The
+    per-graph state is freed before the next graph, so a rank's peak memory is
+    one graph's."""
+    from spgemm_new_amd.distributed import PartitionedMaxK, row_partition
+    from spgemm_new_amd.graphs import (CONFIGS, synthetic_columns, synthetic_indptr,
+                                       synthetic_values)
+    from spgemm_new_amd.ops import topk_cbsr
+    steps, warmup = max(args.steps, args.config_steps), max(min(args.warmup, args.config_steps), 1)
+    only = set(args.configs_only.split(",")) if args.configs_only else None
+    h = 256
+    out = {"protocol": f"{warmup} warm-up + {steps} timed steps per graph, synchronize + barrier "
+                       "on both sides, max over ranks; per-call HIP events (max over ranks of the "
+                       "mean and median); same synthetic generator as N=1 (seed 123)"}
+
+    def block(graph):
+        V, E = CONFIGS[graph]
+        indptr = synthetic_indptr(V, E, seed=args.seed, device=dev)
+        b = row_partition(indptr, world)
+        rows = (b[rank], b[rank + 1])
+        e0, e1 = int(indptr[rows[0]]), int(indptr[rows[1]])
+        indices = synthetic_columns(indptr, seed=args.seed, rows=rows)
+        return V, E, indptr, indices, e0, e1
+
+    if only is None or "products_k32" in only:
+        t0 = time.time()
+        k = 32
+        V, E, indptr, indices, e0, e1 = block("products")
+        values = synthetic_values(args.seed, e0, e1, device=dev)
+        gen = torch.Generator(device=dev)
+        gen.manual_seed(args.seed + 1)
+        X = torch.rand((V, h), generator=gen, device=dev)
+        G = torch.rand((V, h), generator=gen, device=dev)
+        data, sel = topk_cbsr(X, k)
+        del X
+        model = PartitionedMaxK(indptr, indices, values, rank, world, dev, local_block=True,
+                                overlap={"auto": "auto", "on": True, "off": False}[args.overlap],
+                                **kw)
+        data_l, sel_l, G_l = model.local_rows(data), model.local_rows(sel), model.local_rows(G)
+        del data, sel, G
+        res = {}
+
+        def step():
+            res["y"] = model.forward(data_l, sel_l, h)
+            res["dx"] = model.backward(G_l, sel_l)
+        step()   # plans, workspaces, the local AUTO choices
+        ms = _dist_step_ms(step, steps, warmup, dist, dev)
+        fw, bw = _dist_call_stats([lambda: model.forward(data_l, sel_l, h),
+                                   lambda: model.backward(G_l, sel_l)], steps, dist, dev)
+        step()
+        lhs, rhs = _dist_sum(dist, dev, float((res["y"].double() * G_l.double()).sum()),
+                             float((data_l.double() * res["dx"].double()).sum()))
+        ex = model.exchange_ms(k)
+        names = sorted(kk for kk in ex if kk.endswith("_ms"))
+        t = torch.tensor([ex[kk] for kk in names], device=dev, dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        b_iter = 2 * (8 * E + 5 * k * E + 4 * h * V)
+        p = model.plan
+        out[f"products_k32_rowpart{world}"] = {
+            "baseline_config": 4, "graph": "products", "num_nodes": V, "num_edges": E,
+            "hidden": h, "k": k, "parallelism": f"rowpart{world}", "n_gpus": world,
+            "ms_per_step": round(ms, 4), "fwd_ms": fw, "bwd_ms": bw,
+            "value_GBs": round(b_iter / (ms / 1e3) / 1e9, 1),
+            "value_def": "2*(8E + 5kE + 4hV) of the whole graph / ms_per_step",
+            "overlap": model.overlap, "halo_mode": model.halo_mode if model.overlap else "records",
+            "own_nodes_rank0": p.num_own, "halo_nodes_rank0": p.num_halo,
+            "halo_bytes_rank0": model.halo_bytes(k),
+            "exchange_ms_max_over_ranks": {kk: round(float(v), 4) for kk, v in zip(names, t)},
+            "local_bwd_algo_rank0": model.local.last_bwd_algo if not model.overlap else
+            {"own": model.local_own.last_bwd_algo, "halo": model.local_halo.last_bwd_algo},
+            "check": {"adjoint_rel_err": abs(lhs - rhs) / max(abs(lhs), 1e-30),
+                      "what": "sum over ranks <Y_own, G_own> vs <X^_s own, dXs own> (fp64)"},
+            "wall_s": round(time.time() - t0, 1)}
+        log(f"[bench] rowpart{world} products k=32: {ms:.3f} ms/step in {time.time() - t0:.1f}s")
+        del model, data_l, sel_l, G_l, res, indptr, indices, values
+        torch.cuda.empty_cache()
+    if only is None or "proteins_r8" in only:
+        t0 = time.time()
+        k, R = 32, 8
+        V, E, indptr, indices, e0, e1 = block("proteins")
+        vals = torch.stack([synthetic_values(args.seed + 7 + q, e0, e1, device=dev)
+                            for q in range(R)], dim=1).contiguous()
+        gen = torch.Generator(device=dev)
+        gen.manual_seed(args.seed + 1)
+        X = torch.rand((V, h), generator=gen, device=dev)
+        data, sel = topk_cbsr(X, k)
+        del X
+        model = PartitionedMaxK(indptr, indices, vals, rank, world, dev, local_block=True, **kw)
+        r0, r1 = model.bounds[rank], model.bounds[rank + 1]
+        data_l, sel_l = model.local_rows(data), model.local_rows(sel)
+        del data, sel
+        G_l = torch.rand((R, r1 - r0, h), generator=gen, device=dev)
+        res = {}
+
+        def step():
+            res["y"] = model.forward_multi(data_l, sel_l, h)
+            res["dx"] = model.backward_multi(G_l, sel_l)
+        step()
+        ms = _dist_step_ms(step, steps, warmup, dist, dev)
+        fw, bw = _dist_call_stats([lambda: model.forward_multi(data_l, sel_l, h),
+                                   lambda: model.backward_multi(G_l, sel_l)], steps, dist, dev)
+        step()
+        lhs, rhs = _dist_sum(dist, dev, float((res["y"].double() * G_l.double()).sum()),
+                             float((data_l.double() * res["dx"].double()).sum()))
+        b_call = E * (4 + 4 * R + 5 * k) + R * 4 * h * V
+        p = model.plan
+        out[f"proteins_r8_rowpart{world}"] = {
+            "baseline_config": 5, "graph": "proteins", "num_nodes": V, "num_edges": E,
+            "hidden": h, "k": k, "relations": R, "parallelism": f"rowpart{world}",
+            "n_gpus": world, "ms_per_step": round(ms, 4), "fwd_ms": fw, "bwd_ms": bw,
+            "algorithmic_bytes_per_call": b_call,
+            "bytes_formula": "E*(4 + 4R + 5k) + R*4hV (SURVEY.md §8d, fused)",
+            "value_GBs": round(2 * b_call / (ms / 1e3) / 1e9, 1),
+            "own_nodes_rank0": p.num_own, "halo_nodes_rank0": p.num_halo,
+            "local_bwd_algo_rank0": model.local.last_bwd_algo,
+            "check": {"adjoint_rel_err": abs(lhs - rhs) / max(abs(lhs), 1e-30),
+                      "what": "sum over ranks and relations <Y_q, G_q> vs <X^_s, dXs> (fp64)"},
+            "wall_s": round(time.time() - t0, 1)}
+        log(f"[bench] rowpart{world} proteins R=8: {ms:.3f} ms/step in {time.time() - t0:.1f}s")
+        del model, data_l, sel_l, G_l, res, vals, indptr, indices
+        torch.cuda.empty_cache()
+    return out
+
+
 def _cpu_model():
     try:
         for line in open("/proc/cpuinfo"):
@@ -1056,6 +1227,12 @@ def main():
         result["exchange_bytes_rank0"] = {kk: v for kk, v in ex.items() if not kk.endswith("_ms")}
         result["local_bwd_algo_rank0"] = model.local.last_bwd_algo if not model.overlap else \
             {"own": model.local_own.last_bwd_algo, "halo": model.local_halo.last_bwd_algo}
+        if dist and not args.no_configs and args.graph == "reddit":
+            # configs 4 and 5 in the same launch (the driver's scaling runs are
+            # `bench.py --gpus N`): the Reddit state is freed first
+            del model, data_l, sel_l, G_l, X, G, data, sel, indices, values
+            torch.cuda.empty_cache()
+            result["configs"] = partitioned_configs(args, dev, world, rank, dist, kw)
     if not partitioned:
         # per-call timing with HIP events on the launch stream (the current stream)
         st = torch.cuda.current_stream()

@@ -56,6 +56,15 @@ extern "C" {
 /* Library build identification (string, host memory, static). */
 const char *maxk_version(void);
 
+/* ABI revision of this header.  Bumped whenever an existing entry point changes
+ * its arguments or their meaning (not for added entry points); a binding checks
+ * maxk_abi_version() == MAXK_ABI_VERSION at load time and refuses a library
+ * built from other sources instead of calling it with the wrong arguments.
+ *   5: maxk_tile_plan_shape takes num_rows; num_workgroups <= num_groups *
+ *      num_rows is required by maxk_tile_plan_build / maxk_sspmm_backward_tile. */
+#define MAXK_ABI_VERSION 5
+int maxk_abi_version(void);
+
 /* ---------------------------------------------------------------------------
  * Schedule.  Replaces the offline .warp4 file (generate_meta.py:26-48,
  * loaded by cuda_kernel_bindings.cpp:287-317 / spmm_maxk.cu:117).
@@ -456,8 +465,10 @@ int maxk_sspmm_backward_tile(const void *headers, const int64_t *header_start,
  *  maxk_tile_plan_shape: (num_groups, group_size, num_workgroups) for num_cus
  *    CUs -- groups of <= 2048 (k = 32) / 1024 (k = 64) destinations and S <= 8
  *    equal source ranges per group (num_workgroups = num_groups * S, one piece
- *    each) so that about one workgroup runs per CU.  Any other num_workgroups
- *    is valid (ranges straddling groups), measured slower on Reddit.
+ *    each, S <= num_rows) so that about one workgroup runs per CU.  Any other
+ *    num_workgroups <= num_groups * num_rows is valid (ranges straddling
+ *    groups), measured slower on Reddit; more would leave empty workgroup
+ *    ranges and is refused (MAXK_E_ARG) by the build and the backward.
  *  maxk_tile_plan_build: call once with headers == NULL (count call): writes
  *    sizes (host int64[3]) = {header entries, records, largest
  *    padded per-segment record count}; the plan is usable only if sizes[2] <=
@@ -469,8 +480,8 @@ int maxk_sspmm_backward_tile(const void *headers, const int64_t *header_start,
  *    the stream once.  Deterministic: records keep CSR order per segment.
  *  maxk_tile_plan_set_values: records' values := values (after the graph's
  *    edge values changed; the plan's structure does not depend on them). */
-int maxk_tile_plan_shape(int num_cols, int num_cus, int dim_k, int *num_groups, int *group_size,
-                         int *num_workgroups);
+int maxk_tile_plan_shape(int num_rows, int num_cols, int num_cus, int dim_k, int *num_groups,
+                         int *group_size, int *num_workgroups);
 /* The plan format the library was built with (host out): LDS ring buffers and rows per
  * buffer (chunks hold rows - 1 source rows; the header stream leads by buffers - 1). */
 int maxk_tile_format(int *num_buffers, int *buffer_rows);

@@ -46,6 +46,9 @@ MAXK_FWD_CACHED_GATHER = 2
 DEFAULT_PANEL_COST = 2048
 DEFAULT_ROW_COST = 16
 
+# include/maxk_spgemm.h MAXK_ABI_VERSION: the library must report the same
+ABI_VERSION = 5
+
 _ERRORS = {MAXK_E_ARG: "invalid argument", MAXK_E_DIM: "invalid dimension (dim_origin must be "
            "<= 256 and 1 <= dim_k <= dim_origin)", MAXK_E_WORKSPACE: "workspace too small"}
 
@@ -56,6 +59,7 @@ _L = ctypes.c_int64
 _S = ctypes.c_size_t
 SIGNATURES = {
     "maxk_version": (ctypes.c_char_p, []),
+    "maxk_abi_version": (_I, []),
     "maxk_schedule_num_panels": (_I, [_L, _L, _I, _I, ctypes.POINTER(ctypes.c_int64)]),
     "maxk_schedule_build": (_I, [_P, _I, _I, _I, _P, _L, _P]),
     "maxk_warp4_build": (_I, [_P, _I, _I, _P, _P, _L, ctypes.POINTER(ctypes.c_int64), _P]),
@@ -86,7 +90,7 @@ SIGNATURES = {
     "maxk_permute_f32": (_I, [_P, _P, _L, _P, _P]),
     "maxk_rows_sum": (_I, [_P, _I, _L, _P, _P]),
     "maxk_spgemm_forward_sum_parts": (_I, [_P, _L, _P, _P, _P, _P, _P, _I, _I, _I, _I, _P, _I, _P, _P, _S, _P]),
-    "maxk_tile_plan_shape": (_I, [_I, _I, _I, ctypes.POINTER(_I), ctypes.POINTER(_I),
+    "maxk_tile_plan_shape": (_I, [_I, _I, _I, _I, ctypes.POINTER(_I), ctypes.POINTER(_I),
                                   ctypes.POINTER(_I)]),
     "maxk_tile_plan_workspace_bytes": (_S, [_L, _I, _I]),
     "maxk_tile_part_planes": (_I, [_I, _I, _I]),
@@ -137,15 +141,15 @@ class MaxKError(RuntimeError):
     pass
 
 
-def _missing(name):
-    def call(*_a, **_k):
-        raise MaxKError(f"{name} is not in {LIB_PATH} (built from older sources); rebuild it with "
-                        "`python -c 'import __graft_entry__ as g; g.build()'`")
-    return call
+def _stale(why):
+    return MaxKError(f"{LIB_PATH} was built from other sources than these bindings ({why}); "
+                     "rebuild it with `python -c 'import __graft_entry__ as g; g.build()'`")
 
 
 def load():
-    """Load the HIP library (raises if it has not been built)."""
+    """Load the HIP library (raises if it has not been built, or if it was built
+    from sources whose ABI differs from these bindings: an entry point whose
+    arguments changed would otherwise bind without error and be called wrongly)."""
     global _lib
     if _lib is None:
         if not os.path.exists(LIB_PATH):
@@ -153,14 +157,18 @@ def load():
                 f"MI355X HIP library not found at {LIB_PATH}; build it with "
                 "`python -c 'import __graft_entry__ as g; g.build()'` (no CPU fallback exists)")
         L = ctypes.CDLL(LIB_PATH)
+        try:
+            abi = L.maxk_abi_version
+        except AttributeError:
+            raise _stale("no maxk_abi_version: older than ABI 5") from None
+        abi.restype, abi.argtypes = _I, []
+        if abi() != ABI_VERSION:
+            raise _stale(f"library ABI {abi()}, bindings ABI {ABI_VERSION}")
         for name, (res, args) in SIGNATURES.items():
             try:
                 f = getattr(L, name)
             except AttributeError:
-                # a library older than these bindings: the entry raises when called
-                # (loudly, naming it), the rest stays usable
-                setattr(L, name, _missing(name))
-                continue
+                raise _stale(f"{name} missing") from None
             f.restype = res
             f.argtypes = args
         _lib = L

@@ -362,7 +362,7 @@ void test_graph(const std::string &dir, const std::string &graph, int idx, int c
         }
         if ((k == 32 || k == 64) && E > 0) {
             int G = 0, GS = 0, P = 0;
-            MAXKCHECK(maxk_tile_plan_shape(V, prop.multiProcessorCount, k, &G, &GS, &P));
+            MAXKCHECK(maxk_tile_plan_shape(V, V, prop.multiProcessorCount, k, &G, &GS, &P));
             const size_t b = maxk_tile_plan_workspace_bytes(E, G, P);
             const int NP = G + P - 1;   // plan pieces
             void *ws = dev_alloc<char>(b);

@@ -826,11 +826,11 @@ int maxk_tile_format(int *num_buffers, int *buffer_rows)
 
 int maxk_tile_record_words(void) { return kTileRecWords; }
 
-int maxk_tile_plan_shape(int num_cols, int num_cus, int dim_k, int *num_groups, int *group_size,
-                         int *num_workgroups)
+int maxk_tile_plan_shape(int num_rows, int num_cols, int num_cus, int dim_k, int *num_groups,
+                         int *group_size, int *num_workgroups)
 {
-    if (num_cols < 1 || num_cus < 1 || (dim_k != 32 && dim_k != 64) || !num_groups ||
-        !group_size || !num_workgroups)
+    if (num_rows < 1 || num_cols < 1 || num_cus < 1 || (dim_k != 32 && dim_k != 64) ||
+        !num_groups || !group_size || !num_workgroups)
         return MAXK_E_ARG;
     // S equal source ranges per group (num_workgroups = G * S, one piece each):
     // as many groups as fill about one workgroup per CU.  Workgroup ranges that
@@ -840,6 +840,9 @@ int maxk_tile_plan_shape(int num_cols, int num_cus, int dim_k, int *num_groups, 
     int64_t groups = (num_cols + (int64_t)tile_max_group(dim_k) - 1) / tile_max_group(dim_k);
     int64_t ns = num_cus / groups;
     ns = ns < 1 ? 1 : ns > 8 ? 8 : ns;
+    // at most one source range per source row: with P > G * V some workgroup
+    // ranges would be empty, and their partial planes never written
+    if (ns > num_rows) ns = num_rows;
     // as many groups as the CUs left over allow: smaller groups, same sweep
     const int64_t g2 = num_cus / ns < num_cols ? num_cus / ns : num_cols;
     if (g2 > groups) groups = g2;
@@ -894,7 +897,8 @@ int maxk_tile_plan_build(const int32_t *indptr, const int32_t *indices, const fl
     if ((dim_k != 32 && dim_k != 64) || num_rows < 1 || num_cols < 1 || num_edges < 1 ||
         num_edges > INT32_MAX || num_groups < 1 || num_workgroups < 1 ||
         num_workgroups > (1 << 20) || group_size < 1 || group_size > tile_max_group(dim_k) ||
-        (int64_t)num_groups * group_size < num_cols || (int64_t)num_groups + num_workgroups > (1 << 22))
+        (int64_t)num_groups * group_size < num_cols || (int64_t)num_groups + num_workgroups > (1 << 22) ||
+        (int64_t)num_workgroups > (int64_t)num_groups * num_rows)
         return MAXK_E_ARG;
     // piece ids (tile_format.h); "workgroup" below is a piece
     const int NWG = num_groups + num_workgroups - 1;

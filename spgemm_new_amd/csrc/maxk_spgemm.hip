@@ -4295,6 +4295,8 @@ extern "C" {
 
 const char *maxk_version(void) { return MAXK_VERSION_STRING; }
 
+int maxk_abi_version(void) { return MAXK_ABI_VERSION; }
+
 int maxk_schedule_num_panels(int64_t num_rows, int64_t num_edges, int panel_cost, int row_cost,
                              int64_t *num_panels)
 {
@@ -5021,7 +5023,10 @@ int maxk_sspmm_backward_tile(const void *headers, const int64_t *header_start,
         !zero_row || !cbsr_sel || !dxs || num_groups < 1 || num_workgroups < 1 ||
         num_workgroups > (1 << 20) || group_size < 1 ||
         group_size > (dim_k == 32 ? 128 : 64) * kTileWaves || num_rows < 1 || num_cols < 1 ||
-        (int64_t)num_groups * group_size < num_cols)
+        (int64_t)num_groups * group_size < num_cols ||
+        // an empty workgroup range would leave a partial plane unwritten that
+        // tile_combine_kernel still adds
+        (int64_t)num_workgroups > (int64_t)num_groups * num_rows)
         return MAXK_E_ARG;
     const int planes = maxk_tile_part_planes(num_rows, num_groups, num_workgroups);
     if (planes > 0 && !part) return MAXK_E_ARG;

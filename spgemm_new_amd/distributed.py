@@ -24,6 +24,8 @@ can be tested on CPU with gloo; the default engine is the HIP MaxKGraph.
 """
 from __future__ import annotations
 
+import warnings
+
 import torch
 import torch.distributed as dist
 
@@ -313,6 +315,12 @@ class PartitionedMaxK:
         V = self.bounds[-1]
         frac, unsplit = self._max_over_ranks(p.num_halo / max(1, V), 0.0 if self.overlap else 1.0)
         if unsplit > 0:
+            if mode == "allgather":
+                # a pinned mode is not downgraded silently: the caller
+                # would measure the all-to-all-v path believing it all-gathers
+                warnings.warn("halo_mode='allgather' needs the own | halo split on every rank "
+                              "(overlap on, a halo on each rank); using 'records'",
+                              RuntimeWarning, stacklevel=3)
             return "records"
         if mode == "allgather":
             return mode

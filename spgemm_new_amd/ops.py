@@ -488,8 +488,8 @@ class MaxKGraph:
                 shape = None
                 if self.tile_splits is not None:
                     # S equal source ranges per group: G * S workgroups
-                    G, GS, _ = tile.choose_shape(self.num_cols, cus, dim_k)
-                    shape = (G, GS, G * max(1, int(self.tile_splits)))
+                    G, GS, _ = tile.choose_shape(self.num_rows, self.num_cols, cus, dim_k)
+                    shape = (G, GS, G * max(1, min(int(self.tile_splits), self.num_rows)))
                 plan = tile.build(self.indptr, self.indices[: self.num_edges],
                                   self.values[: self.num_edges], self.num_rows, self.num_cols,
                                   cus=cus, k=dim_k, shape=shape)

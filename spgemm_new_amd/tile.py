@@ -69,13 +69,14 @@ def max_group(k: int) -> int:
     return (128 if k == 32 else 64) * WAVES
 
 
-def choose_shape(num_cols: int, cus: int = 256, k: int = 32) -> tuple[int, int, int]:
+def choose_shape(num_rows: int, num_cols: int, cus: int = 256,
+                 k: int = 32) -> tuple[int, int, int]:
     """(num_groups, group_size, num_workgroups): groups of <= max_group(k)
-    destinations and S equal source ranges each (num_workgroups = groups * S),
-    about one workgroup per CU (maxk_tile_plan_shape)."""
+    destinations and S <= num_rows equal source ranges each (num_workgroups =
+    groups * S), about one workgroup per CU (maxk_tile_plan_shape)."""
     L = _lib.load()
     g, s, n = ctypes.c_int(0), ctypes.c_int(0), ctypes.c_int(0)
-    _lib.check(L.maxk_tile_plan_shape(num_cols, cus, k, ctypes.byref(g), ctypes.byref(s),
+    _lib.check(L.maxk_tile_plan_shape(num_rows, num_cols, cus, k, ctypes.byref(g), ctypes.byref(s),
                                       ctypes.byref(n)), "maxk_tile_plan_shape")
     return g.value, s.value, n.value
 
@@ -92,9 +93,12 @@ def build(indptr: torch.Tensor, indices: torch.Tensor, values: torch.Tensor, num
     E = indices.numel()
     if E == 0 or num_rows < 1 or num_cols < 1 or k not in (32, 64):
         return None
-    G, GS, P = shape or choose_shape(num_cols, cus, k)
+    G, GS, P = shape or choose_shape(num_rows, num_cols, cus, k)
     if GS > max_group(k):
         return None
+    if P > G * num_rows:
+        # empty workgroup ranges: their partial planes would never be written
+        raise ValueError(f"TILE shape {G} groups x {num_rows} rows cannot feed {P} workgroups")
     L = _lib.load()
     NWG = G + P - 1          # pieces
     ws = torch.empty(max(1, L.maxk_tile_plan_workspace_bytes(E, G, P)), dtype=torch.uint8,
@@ -170,7 +174,9 @@ def emulate(plan, grad: torch.Tensor, sel: torch.Tensor) -> torch.Tensor:
     grad = grad.cpu().float()
     sel = sel.cpu().long()
     K = plan.get("k", 32)
-    out = torch.zeros(part_planes(V, G, P) + 1, C, K)
+    # unwritten plane entries stay NaN and poison the result, as stale memory
+    # would on the GPU (the kernel's `part` is not zeroed)
+    out = torch.full((part_planes(V, G, P) + 1, C, K), float("nan"))
     if K == 32:
         jj = (2 * torch.arange(64)[:, None] + torch.arange(64)[None, :] // 32) * WAVES  # [slot, lane]
     else:
@@ -221,4 +227,10 @@ def emulate(plan, grad: torch.Tensor, sel: torch.Tensor) -> torch.Tensor:
             j = jj + wv
             m = j < nd
             out[sp, d0 + j[m], ent.expand(64, 64)[m]] = acc[wv][m]
-    return out.sum(0)
+    # tile_combine_kernel: dxs += group g's _group_planes(g) partial planes, in order
+    res = out[0].clone()
+    for g in range(G):
+        d0, d1 = g * GS, min(C, (g + 1) * GS)
+        for p in range(_group_planes(g, V, G, P)):
+            res[d0:d1] += out[1 + p, d0:d1]
+    return res

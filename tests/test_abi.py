@@ -75,6 +75,20 @@ def test_missing_library_fails_loudly(tmp_path, monkeypatch):
         _lib.load()
 
 
+def test_library_of_other_abi_is_refused(monkeypatch):
+    """A library built from sources with another ABI revision (an entry point
+    whose arguments changed) is refused at load, not bound with wrong argtypes
+    (ADVICE r4)."""
+    L = _lib.load()
+    assert L.maxk_abi_version() == _lib.ABI_VERSION
+    hdr = open(HEADER).read()
+    assert re.search(r"#define MAXK_ABI_VERSION %d\b" % _lib.ABI_VERSION, hdr)
+    monkeypatch.setattr(_lib, "_lib", None)
+    monkeypatch.setattr(_lib, "ABI_VERSION", _lib.ABI_VERSION + 1)
+    with pytest.raises(_lib.MaxKError, match="other sources"):
+        _lib.load()
+
+
 def test_oracle_not_imported_by_product_package():
     import spgemm_new_amd
     pkg = os.path.dirname(spgemm_new_amd.__file__)

@@ -98,6 +98,33 @@ def test_bench_launches_its_own_ranks():
 
 
 @pytest.mark.gpu
+def test_bench_n2_reports_multi_gpu_configs():
+    """one `bench.py --gpus N` launch (what the driver's scaling
+    runs call) also measures BASELINE config 4 (products k=32) and config 5
+    (proteins R=8) row-partitioned, in the `configs` of rank 0's line.  2 ranks on
+    the one GPU, gloo standing in for RCCL (host-staged exchanges: plumbing only)."""
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK",
+                                                            "MASTER_PORT")}
+    env["BENCH_BACKEND"] = "gloo"
+    cmd = [sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--steps", "2",
+           "--warmup", "1", "--config-steps", "2"]
+    out = subprocess.run(cmd, cwd=ROOT, capture_output=True, text=True, timeout=900, env=env)
+    assert out.returncode == 0, out.stderr[-3000:]
+    d = json.loads(out.stdout.strip().splitlines()[-1])
+    assert d["n_gpus"] == 2 and d["config"]["parallelism"] == "rowpart2"
+    c = d["configs"]
+    p, q = c["products_k32_rowpart2"], c["proteins_r8_rowpart2"]
+    for e in (p, q):
+        assert e["n_gpus"] == 2 and e["parallelism"] == "rowpart2" and e["ms_per_step"] > 0
+        assert e["fwd_ms"]["median_max_over_ranks"] > 0 and e["bwd_ms"]["median_max_over_ranks"] > 0
+        assert e["check"]["adjoint_rel_err"] < 1e-6
+    assert p["baseline_config"] == 4 and p["num_nodes"] == 2449029
+    assert p["halo_mode"] in ("records", "allgather") and p["halo_bytes_rank0"]["reverse_bwd"] > 0
+    assert p["exchange_ms_max_over_ranks"]["bwd_a2a_ms"] > 0
+    assert q["baseline_config"] == 5 and q["relations"] == 8 and q["num_nodes"] == 132534
+
+
+@pytest.mark.gpu
 def test_bench_more_gpus_than_visible_fails():
     """--gpus 9 on a one-GPU box (RCCL: one GPU per rank) exits non-zero, prints no line."""
     env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK",

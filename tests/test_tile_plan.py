@@ -3,6 +3,8 @@ tests/tile_ref.py, replayed by spgemm_new_amd.tile.emulate against the float64
 oracle), the device plan builder (GPU: maxk_tile_plan_build bit-identical to
 the reference builder) and the kernel (GPU, against the oracle and the other
 backward algorithms)."""
+import ctypes
+
 import numpy as np
 import pytest
 import torch
@@ -15,7 +17,7 @@ TOL = 1e-4  # fp32 summation order vs the float64 oracle (north_star tolerance)
 
 def _graph(V, C, avg_deg, seed, hub_rows=0):
     rng = np.random.default_rng(seed)
-    deg = rng.poisson(avg_deg, V).astype(np.int64)
+    deg = np.minimum(rng.poisson(avg_deg, V), C).astype(np.int64)
     if hub_rows:
         deg[:hub_rows] = min(C, avg_deg * 20)
     indptr = np.zeros(V + 1, np.int64)
@@ -42,6 +44,8 @@ def _inputs(V, C, seed, k=32, h=256):
     (700, 900, 20, (3, 300, 4), 0),    # forced: 4 workgroups over 3 groups (pieces straddle)
     (900, 2500, 8, (3, 834, 7), 0),    # forced: 7 workgroups over 3 groups
     (200, 64, 4, (1, 64, 1), 0),       # few destinations, one range
+    (5, 5, 2, None, 0),                # fewer source rows than ranges the CUs allow
+    (3, 700, 40, None, 0),             # 3 source rows, many destinations
 ])
 def test_plan_emulated_matches_oracle(oracle, V, C, deg, shape, hubs, k):
     """Both record formats (tile_format.h TILE_REC_WORDS 2 and 4) replayed on
@@ -94,11 +98,72 @@ def test_plan_invariants():
 
 
 @pytest.mark.parametrize("k", [32, 64])
-@pytest.mark.parametrize("C", [1, 63, 1000, 2048, 2049, 4096, 100_000, 232_965, 2_449_029])
+@pytest.mark.parametrize("C", [1, 5, 63, 1000, 2048, 2049, 4096, 100_000, 232_965, 2_449_029])
+@pytest.mark.parametrize("V", [1, 3, 5, 7, 40, 232_965])
 @pytest.mark.parametrize("cus", [8, 256])
-def test_shape_library_matches_reference(C, cus, k):
-    """maxk_tile_plan_shape (C ABI, host code: no GPU needed) == the reference rule."""
-    assert tile.choose_shape(C, cus, k) == tile_ref.choose_shape(C, cus, k)
+def test_shape_library_matches_reference(V, C, cus, k):
+    """maxk_tile_plan_shape (C ABI, host code: no GPU needed) == the reference
+    rule, and never asks for more workgroups than (group, source row) pairs:
+    an empty workgroup range would leave a partial plane unwritten."""
+    got = tile.choose_shape(V, C, cus, k)
+    assert got == tile_ref.choose_shape(V, C, cus, k)
+    G, GS, P = got
+    assert P <= G * V and G * GS >= C
+
+
+def test_oversubscribed_shape_refused_without_gpu():
+    """num_workgroups > num_groups * num_rows is refused before any launch by the
+    plan builder and the backward, and by tile.build."""
+    from spgemm_new_amd import _lib
+    L = _lib.load()
+    a = 1 << 12   # aligned dummy pointers: validation fails before they are used
+    rc = L.maxk_sspmm_backward_tile(a, a, a, a, a, 5, 40, 1, a, a, a, 5, 5, 256, 32, a, a, None)
+    assert rc == _lib.MAXK_E_ARG
+    rc = L.maxk_sspmm_backward_tile(a, a, a, a, a, 5, 25, 1, a, a, a, 5, 5, 1, 32, a, a, None)
+    assert rc == _lib.MAXK_E_DIM          # the same call with P = G * V passes the shape check
+    sizes = (ctypes.c_int64 * 3)()
+    rc = L.maxk_tile_plan_build(a, a, a, 5, 5, 10, 32, 5, 1, 40, None, 0, None, None, 0, None, None,
+                                None, sizes, a, 1 << 30, None)
+    assert rc == _lib.MAXK_E_ARG
+    idx = torch.zeros(3, dtype=torch.int32)
+    with pytest.raises(ValueError):
+        tile.build(torch.tensor([0, 3], dtype=torch.int32), idx, torch.ones(3), 1, 5,
+                   shape=(5, 1, 6))
+
+
+def test_emulator_leaves_unwritten_planes_nan():
+    """The CPU replay starts its planes as NaN (the kernel's `part` is torch.empty),
+    so a plan whose pieces missed a plane would fail test_plan_emulated_matches_oracle."""
+    indptr, idx, vals = _graph(40, 300, 6, seed=3)
+    plan = tile_ref.build(torch.from_numpy(indptr), torch.from_numpy(idx), torch.from_numpy(vals),
+                          40, 300, shape=(2, 150, 8), k=32, record_words=4)
+    grad, sel = _inputs(40, 300, seed=3)
+    assert torch.isfinite(tile.emulate(plan, torch.from_numpy(grad), torch.from_numpy(sel))).all()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("k", [32, 64])
+@pytest.mark.parametrize("V,C,splits", [(5, 5, None), (3, 700, None), (7, 7, 64), (2, 3000, 8)])
+def test_tile_few_source_rows_nan_part(dev, oracle, V, C, splits, k):
+    """Graphs with fewer source rows than the ranges the CUs would allow (and
+    tile_splits > V): the shape must not create empty workgroup ranges, whose
+    partial planes tile_combine_kernel would add unwritten.  `part` is filled
+    with NaN first, so any plane the kernel skips shows up."""
+    import spgemm_new_amd as S
+    from spgemm_new_amd import _lib
+    indptr, idx, vals = _graph(V, C, min(C // 2, 30), seed=V * 7 + C)
+    grad, sel = _inputs(V, C, seed=V + C, k=k)
+    g = S.MaxKGraph(torch.from_numpy(indptr).to(dev), torch.from_numpy(idx).to(dev),
+                    torch.from_numpy(vals).to(dev), num_cols=C, tile_splits=splits)
+    plan = g.tile_plan(k)
+    assert plan is not None
+    assert plan["num_workgroups"] <= plan["num_groups"] * V
+    plan["part"].fill_(float("nan"))
+    got = g.backward(torch.from_numpy(grad).to(dev), torch.from_numpy(sel).to(dev),
+                     algo=_lib.MAXK_BWD_TILE)
+    assert g.last_bwd_algo == "tile"
+    ref = oracle.np_backward(indptr, idx, vals, grad, sel)
+    assert oracle.parity_error(got.cpu().numpy(), ref) < TOL
 
 
 @pytest.mark.parametrize("V,G,P", [(1, 1, 1), (300, 1, 8), (300, 3, 4), (900, 3, 7), (232_965, 128, 256),

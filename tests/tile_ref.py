@@ -15,12 +15,13 @@ def max_group(k: int) -> int:
     return (128 if k == 32 else 64) * WAVES
 
 
-def choose_shape(num_cols: int, cus: int = 256, k: int = 32) -> tuple[int, int, int]:
+def choose_shape(num_rows: int, num_cols: int, cus: int = 256,
+                 k: int = 32) -> tuple[int, int, int]:
     """(num_groups, group_size, num_workgroups): groups of <= 2048 destinations
-    and S equal source ranges each (num_workgroups = groups * S) so that about
-    one workgroup runs per CU."""
+    and S <= num_rows equal source ranges each (num_workgroups = groups * S) so
+    that about one workgroup runs per CU."""
     groups = -(-num_cols // max_group(k))
-    splits = max(1, min(8, cus // groups))
+    splits = max(1, min(8, cus // groups, num_rows))
     # as many groups as the CUs left over allow: smaller groups, same sweep
     groups = max(groups, min(cus // splits, num_cols))
     size = -(-num_cols // groups)
@@ -46,7 +47,7 @@ def build(indptr: torch.Tensor, indices: torch.Tensor, values: torch.Tensor, num
         return None
     if k not in (32, 64):
         return None
-    G, GS, P = shape or choose_shape(num_cols, cus, k)
+    G, GS, P = shape or choose_shape(num_rows, num_cols, cus, k)
     if GS > max_group(k):
         return None
     NWG = G + P - 1          # pieces (spgemm_new_amd/tile.py)
