@@ -41,8 +41,7 @@ def parse():
     p.add_argument("--h", type=int, default=256)
     p.add_argument("--seed", type=int, default=123)
     p.add_argument("--bwd-algo", default="auto",
-                   choices=["auto", "atomic", "staged", "local", "tile", "staged_edge", "edge_gather",
-                            "binned", "binned_edge"])
+                   choices=["auto", "atomic", "staged", "local", "tile", "staged_edge", "edge_gather"])
     p.add_argument("--panel-cost", type=int, default=None)
     p.add_argument("--row-cost", type=int, default=None)
     p.add_argument("--no-cpu-baseline", action="store_true")
@@ -656,27 +655,15 @@ def config_sweep(args, dev, only=None):
             del rq, vq
         bwd_vendor = float(((dx - ref).abs() / ref.abs().clamp_min(1)).max())
         del xm, ref
-        # every candidate form, timed the same way (min of 3 after one call): the
-        # forward's two kernels and the backward's fused forms + the composed one
-        from spgemm_new_amd.ops import _min_ms, multi_gather_ok
-        cand_f = {"lds": round(_min_ms(lambda: g.forward_multi(data, sel, vals, h, out=y,
-                                                               form="lds")), 4)}
-        if multi_gather_ok(R, k, h):
-            cand_f["gather"] = round(_min_ms(lambda: g.forward_multi(data, sel, vals, h, out=y,
-                                                                     form="gather")), 4)
+        # every backward candidate, timed the same way (min of 3 after one call): the
+        # fused forms and the composed one (the register and bank-ordered phase-1
+        # forms, measured slower, are in the ablation build: tools/variants_lib)
+        from spgemm_new_amd.ops import _min_ms
         cand_b = {}
-        for nm, a, fm in (("multi_staged_lds", _lib.MAXK_BWD_MULTI_STAGED, "lds"),
-                          ("multi_staged_regs", _lib.MAXK_BWD_MULTI_STAGED, "gather"),
-                          ("multi_edge_gather_lds", _lib.MAXK_BWD_MULTI_EDGE_GATHER, "lds"),
-                          ("multi_edge_gather_regs", _lib.MAXK_BWD_MULTI_EDGE_GATHER, "gather"),
-                          ("multi_staged_banked", _lib.MAXK_BWD_MULTI_STAGED, "banked"),
-                          ("local_rel8", _lib.MAXK_BWD_LOCAL, "auto")):
-            if fm == "gather" and not multi_gather_ok(R, k, h):
-                continue
-            if fm == "banked" and not (R == 8 and k == 32):
-                continue
-            cand_b[nm] = round(_min_ms(lambda: g.backward_multi(G, sel, vals, out=dx, algo=a,
-                                                                form=fm)), 4)
+        for nm, a in (("multi_staged", _lib.MAXK_BWD_MULTI_STAGED),
+                      ("multi_edge_gather", _lib.MAXK_BWD_MULTI_EDGE_GATHER),
+                      ("local_rel8", _lib.MAXK_BWD_LOCAL)):
+            cand_b[nm] = round(_min_ms(lambda: g.backward_multi(G, sel, vals, out=dx, algo=a)), 4)
         cand_b["composed"] = round(_min_ms(lambda: g._backward_composed(G, sel, vals, dx,
                                                                         _lib.MAXK_BWD_AUTO)), 4)
         g.forward_multi(data, sel, vals, h, out=y)
@@ -691,8 +678,8 @@ def config_sweep(args, dev, only=None):
             "fwd_frac": round(b / (fs["mean"] / 1e3) / 1e9 / HBM_PEAK_GBS, 4),
             "bwd_frac": round(b / (bs["mean"] / 1e3) / 1e9 / HBM_PEAK_GBS, 4),
             "bwd_algo": algo_b,
-            "fwd_form": "gather" if multi_gather_ok(R, k, h) and S.ops.MULTI_GATHER else "lds",
-            "fwd_candidates_ms": cand_f, "bwd_candidates_ms": cand_b,
+            "fwd_form": "lds (relation-vector, interleaved lanes, bank-ordered CBSR)",
+            "bwd_candidates_ms": cand_b,
             "check": {"fwd_rel0_vs_single_max_rel_diff": fwd_err,
                       "fwd_vs_rocsparse_max_rel_diff": fwd_vendor,
                       "bwd_vs_rocsparse_max_rel_diff": bwd_vendor,
@@ -1092,8 +1079,7 @@ def main():
     algo = {"auto": _lib.MAXK_BWD_AUTO, "atomic": _lib.MAXK_BWD_ATOMIC,
             "staged": _lib.MAXK_BWD_STAGED, "local": _lib.MAXK_BWD_LOCAL,
             "tile": _lib.MAXK_BWD_TILE, "staged_edge": _lib.MAXK_BWD_STAGED_EDGE,
-            "edge_gather": _lib.MAXK_BWD_EDGE_GATHER, "binned": _lib.MAXK_BWD_BINNED,
-            "binned_edge": _lib.MAXK_BWD_BINNED_EDGE}[args.bwd_algo]
+            "edge_gather": _lib.MAXK_BWD_EDGE_GATHER}[args.bwd_algo]
     kw = {}
     if args.panel_cost:
         kw["panel_cost"] = args.panel_cost

@@ -30,14 +30,10 @@ MAXK_BWD_LOCAL = 3
 MAXK_BWD_TILE = 4
 MAXK_BWD_STAGED_EDGE = 5
 MAXK_BWD_EDGE_GATHER = 6
-MAXK_BWD_BINNED = 7
-MAXK_BWD_BINNED_EDGE = 8
 # backward_multi only (Python level; the C entry is maxk_sspmm_backward_multi with
 # MAXK_BWD_STAGED / MAXK_BWD_EDGE_GATHER): relations summed per edge in phase 1
 MAXK_BWD_MULTI_STAGED = 16
 MAXK_BWD_MULTI_EDGE_GATHER = 17
-MAXK_BIN_DESTS = 255
-MAXK_BIN_WINDOW = 64
 MAXK_TOPK_ORDER_COLUMN = 0
 MAXK_TOPK_ORDER_VALUE = 1
 MAXK_TOPK_ORDER_LANE = 2
@@ -47,7 +43,7 @@ DEFAULT_PANEL_COST = 2048
 DEFAULT_ROW_COST = 16
 
 # include/maxk_spgemm.h MAXK_ABI_VERSION: the library must report the same
-ABI_VERSION = 5
+ABI_VERSION = 6
 
 _ERRORS = {MAXK_E_ARG: "invalid argument", MAXK_E_DIM: "invalid dimension (dim_origin must be "
            "<= 256 and 1 <= dim_k <= dim_origin)", MAXK_E_WORKSPACE: "workspace too small"}
@@ -76,11 +72,6 @@ SIGNATURES = {
                                             _P]),
     "maxk_sspmm_backward_multi": (_I, [_I, _P, _L, _P, _P, _P, _I, _P, _P, _I, _I, _L, _I, _I, _P,
                                        _P, _P, _L, _P, _P, _S, _P]),
-    "maxk_sspmm_backward_multi_gather": (_I, [_I, _P, _L, _P, _P, _P, _I, _P, _P, _I, _I, _L, _I,
-                                              _I, _P, _P, _P, _L, _P, _P, _S, _P]),
-    "maxk_sspmm_backward_multi_banked": (_I, [_I, _P, _L, _P, _P, _P, _I, _P, _P, _I, _I, _L, _I,
-                                              _I, _P, _P, _P, _L, _P, _P, _S, _P]),
-    "maxk_cbsr_bank_order_ex": (_I, [_P, _P, _I, _I, _I, _P, _P, _P, _P]),
     "maxk_sspmm_backward_tile": (_I, [_P, _P, _P, _P, _P, _I, _I, _I, _P, _P, _P, _I, _I, _I, _I,
                                       _P, _P, _P]),
     "maxk_tile_format": (_I, [ctypes.POINTER(_I), ctypes.POINTER(_I)]),
@@ -113,9 +104,6 @@ SIGNATURES = {
     "maxk_spmm_gnna_sag": (_I, [_P, _L, _P, _P, _P, _I, _P, _P]),
     "maxk_forward_multi_workspace_bytes": (_S, [_L, _I, _I]),
     "maxk_spgemm_forward_multi": (_I, [_P, _L, _P, _P, _P, _I, _P, _P, _I, _I, _I, _P, _P, _S, _P]),
-    "maxk_cbsr_colmask": (_I, [_P, _P, _I, _I, _P, _P, _P]),
-    "maxk_spgemm_forward_multi_gather": (_I, [_P, _L, _P, _P, _P, _I, _P, _P, _I, _I, _I, _P, _P,
-                                              _S, _P]),
     "maxk_records_sel_gather": (_I, [_P, _I, _P, _L, _P, _P]),
     "maxk_cbsr_gather_records": (_I, [_P, _P, _P, _L, _I, _P, _P]),
     "maxk_spgemm_forward_records": (_I, [_P, _L, _P, _P, _P, _P, _I, _I, _I, _I, _P, _P, _S, _P]),
@@ -124,12 +112,6 @@ SIGNATURES = {
     "maxk_topk_cbsr": (_I, [_P, _I, _I, _L, _I, _I, _P, _P, _P, _P]),
     "maxk_cbsr_scatter": (_I, [_P, _P, _I, _I, _I, _P, _P]),
     "maxk_cbsr_mask": (_I, [_P, _P, _I, _I, _I, _P, _P]),
-    "maxk_bin_plan_workspace_bytes": (_S, [_L, _I]),
-    "maxk_bin_plan_build": (_I, [_P, _L, _P, _L, _I, _P, _P, _P, _L, ctypes.POINTER(ctypes.c_int64),
-                                 _P, _S, _P]),
-    "maxk_backward_binned_workspace_bytes": (_S, [_L, _I]),
-    "maxk_sspmm_backward_binned": (_I, [_P, _L, _P, _P, _P, _P, _P, _I, _I, _I, _L, _I, _I, _P, _P,
-                                        _P, _P, _I, _L, _P, _S, _P]),
     "maxk_spmm_forward_warp4": (_I, [_P, _P, _P, _P, _P, _P, _I, _I, _I, _I, _I, _P]),
     "maxk_spmm_backward_warp4": (_I, [_P, _P, _P, _P, _P, _P, _I, _I, _I, _I, _I, _P]),
 }

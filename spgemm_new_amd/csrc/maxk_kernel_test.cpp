@@ -15,7 +15,7 @@
 //                   this is the library's HIP dense SpMM on the same input)
 //   maxk            forward SpGEMM (merge-path schedule, no pre-zeroing)
 //   maxk_backward   backward SSpMM, the fastest of the algorithms below
-//   maxk_backward_{atomic,staged,staged_edge,local,tile,binned}   (staged_edge: the
+//   maxk_backward_{atomic,staged,staged_edge,local,tile}   (staged_edge: the
 //                   edge selectors written by maxk_spgemm_forward_esel; tile: k in {32, 64}; its plan
 //                   from maxk_tile_plan_build, as MaxKGraph.tile_plan builds it)
 // Each time is the mean of 4 runs after 4 warm-ups, each run followed by a
@@ -396,30 +396,6 @@ void test_graph(const std::string &dir, const std::string &graph, int idx, int c
                     if (q) HIPCHECK(hipFree(q));
             }
             HIPCHECK(hipFree(ws));
-        }
-        if ((k == 8 || k == 16 || k == 32) && E > 0) {
-            // BINNED: destination bins summed in LDS; plan tied to the panel schedule
-            const size_t b = maxk_bin_plan_workspace_bytes(E, V);
-            void *ws = dev_alloc<char>(b);
-            int64_t slots = 0;
-            MAXKCHECK(maxk_bin_plan_build(sched, P, indices, E, V, nullptr, nullptr, nullptr, 0, &slots,
-                                          ws, b, st));
-            const int nb = (V + MAXK_BIN_DESTS - 1) / MAXK_BIN_DESTS;
-            int32_t *bpos = dev_alloc<int32_t>(E), *bptr = dev_alloc<int32_t>((size_t)nb + 1);
-            uint8_t *bdst = dev_alloc<uint8_t>((size_t)slots);
-            MAXKCHECK(maxk_bin_plan_build(sched, P, indices, E, V, bpos, bptr, bdst, slots, &slots, ws,
-                                          b, st));
-            const size_t pb = maxk_backward_binned_workspace_bytes(slots, k);
-            void *prod = dev_alloc<char>(pb);
-            const double t = time_ms([&] {
-                MAXKCHECK(maxk_sspmm_backward_binned(sched, P, indptr, indices, val, dense, sel, 0, V,
-                                                     V, E, kDimOrigin, k, dxs, bpos, bptr, bdst, nb,
-                                                     slots, prod, pb, st));
-            });
-            std::printf("%s maxk_backward_binned %g\n", out.c_str(), t);
-            compare("binned");
-            best = std::min(best, t);
-            for (void *q : {(void *)bpos, (void *)bptr, (void *)bdst, prod, ws}) HIPCHECK(hipFree(q));
         }
         std::printf("%s maxk_backward %g\n", out.c_str(), best);
         std::fflush(stdout);

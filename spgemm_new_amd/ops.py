@@ -71,10 +71,6 @@ MIN_PANELS = int(os.environ.get("MAXK_MIN_PANELS", 16384))
 TILE_AUTO = os.environ.get("MAXK_TILE", "1") != "0"
 # STAGED_EDGE backward (edge selectors written by the forward) among the AUTO candidates
 ESEL_AUTO = os.environ.get("MAXK_ESEL", "1") != "0"
-# BINNED backward (destination bins summed in LDS, k in {8, 16, 32}) among the AUTO
-# candidates; its plan is dropped when window padding would exceed this many slots per edge
-BIN_AUTO = os.environ.get("MAXK_BIN", "1") != "0"
-BIN_MAX_SLOTS_PER_EDGE = 1.5
 # AUTO backward: "measure" (time the candidates once per graph and shape; the fastest
 # is kept) or "fixed" (a rule of the shape alone, no timing: the same algorithm -- and
 # so the same fp32 summation order -- on every run and machine)
@@ -96,16 +92,8 @@ FWD_BLOCKED_MIN_DEGREE = 128
 FWD_BLOCKED_CANDIDATES = (3, 4, 6, 8)  # Reddit: 4 best at k = 32 and 64
 # fused multi-relation forward: reorder CBSR entries against LDS store conflicts
 MULTI_BANK_ORDER = os.environ.get("MAXK_MULTI_BANK_ORDER", "1") != "0"
-# fused R = 8 forward at h = 256, k <= 32: the register-accumulator (gather) kernel
-# instead of the LDS relation-vector one (same bits; MAXK_MULTI_GATHER=0 disables)
-MULTI_GATHER = os.environ.get("MAXK_MULTI_GATHER", "0") != "0"
-# multi-relation STAGED backward at R = 8, k = 32: phase 1 on bank-ordered
-# selectors (maxk_sspmm_backward_multi_banked; same bits; measured slower, DESIGN §4: 1 enables)
-MULTI_BANKED = os.environ.get("MAXK_MULTI_BANKED", "0") != "0"
-
-
-def multi_gather_ok(R: int, k: int, dim_origin: int) -> bool:
-    return R == 8 and dim_origin == 256 and k in (4, 8, 16, 32)
+# (the register-accumulator and bank-ordered multi-relation forms and the BINNED
+# backward, all measured slower, live in the ablation build: tools/variants_lib)
 
 
 def _build_schedule(indptr: torch.Tensor, num_rows: int, num_edges: int, panel_cost: int,
@@ -148,18 +136,12 @@ def _validate_csr(indptr: torch.Tensor, indices: torch.Tensor, num_cols: int) ->
         raise RuntimeError(f"indices out of range: every column must be in [0, {num_cols})")
 
 
-_ESEL_ALGOS = (_lib.MAXK_BWD_STAGED_EDGE, _lib.MAXK_BWD_EDGE_GATHER, _lib.MAXK_BWD_BINNED_EDGE)
-_BIN_ALGOS = (_lib.MAXK_BWD_BINNED, _lib.MAXK_BWD_BINNED_EDGE)
+_ESEL_ALGOS = (_lib.MAXK_BWD_STAGED_EDGE, _lib.MAXK_BWD_EDGE_GATHER)
 
 
 _ALGO_NAMES = {_lib.MAXK_BWD_ATOMIC: "atomic", _lib.MAXK_BWD_STAGED: "staged",
                _lib.MAXK_BWD_LOCAL: "local", _lib.MAXK_BWD_TILE: "tile",
-               _lib.MAXK_BWD_STAGED_EDGE: "staged_edge", _lib.MAXK_BWD_EDGE_GATHER: "edge_gather",
-               _lib.MAXK_BWD_BINNED: "binned", _lib.MAXK_BWD_BINNED_EDGE: "binned_edge"}
-
-
-def bin_shape_ok(dim_k: int) -> bool:
-    return dim_k in (8, 16, 32)
+               _lib.MAXK_BWD_STAGED_EDGE: "staged_edge", _lib.MAXK_BWD_EDGE_GATHER: "edge_gather"}
 
 
 def _edge_gather_ok(k: int) -> bool:
@@ -263,7 +245,6 @@ class MaxKGraph:
         self._esel_on = set()     # (k, h): forwards write edge selectors (AUTO chose STAGED_EDGE)
         self._esel = []           # [(sel key, sel, uint8 buffer[E * k], pinned)], most recent last
         self.last_bwd_algo = None
-        self._bin = None          # BINNED backward plan (False: padding too high)
         self._blocked = {}        # column-blocked forward plans, per block count
         self._fwd_blocks = {}     # (k, h) -> block count chosen (0: plain forward)
 
@@ -353,43 +334,6 @@ class MaxKGraph:
                        "maxk_csc_perm_build")
             self._csc_perm = perm
         return self._csc_perm
-
-    def bin_plan(self):
-        """Plan of the BINNED backward (maxk_sspmm_backward_binned), built once on
-        the device (maxk_bin_plan_build; one host read of the slot count), or None
-        when the graph has no edges or its destination windows would need more
-        than BIN_MAX_SLOTS_PER_EDGE slots per edge, plus the partly filled windows
-        that end each bin (hub destinations: a window holds each destination once).  Tied to bwd_sched (phase 1's panels)."""
-        if self._bin is None:
-            self._bin = False
-            E, C = self.num_edges, self.num_cols
-            if E > 0:
-                import ctypes
-                L = _lib.load()
-                ws = torch.empty(max(1, L.maxk_bin_plan_workspace_bytes(E, C)), dtype=torch.uint8,
-                                 device=self.device)
-                st = _stream(ws)
-                n = ctypes.c_int64(0)
-                args = (self.bwd_sched.data_ptr(), self.bwd_num_panels, self.indices.data_ptr(),
-                        E, C)
-                _lib.check(L.maxk_bin_plan_build(*args, None, None, None, 0, ctypes.byref(n),
-                                                 ws.data_ptr(), ws.numel(), st),
-                           "maxk_bin_plan_build(count)")
-                slots = int(n.value)
-                nb = -(-C // _lib.MAXK_BIN_DESTS)
-                # beyond the <= 8 partly filled windows every bin may end with
-                if slots <= BIN_MAX_SLOTS_PER_EDGE * E + nb * 8 * _lib.MAXK_BIN_WINDOW:
-                    pos = torch.empty(E, dtype=torch.int32, device=self.device)
-                    ptr = torch.empty(nb + 1, dtype=torch.int32, device=self.device)
-                    dst = torch.empty(slots, dtype=torch.uint8, device=self.device)
-                    _lib.check(L.maxk_bin_plan_build(*args, pos.data_ptr(), ptr.data_ptr(),
-                                                     dst.data_ptr(), slots, ctypes.byref(n),
-                                                     ws.data_ptr(), ws.numel(), st),
-                               "maxk_bin_plan_build")
-                    self._bin = {"bin_pos": pos, "bin_ptr": ptr, "bin_dst": dst,
-                                 "num_bins": nb, "num_slots": slots}
-                del ws
-        return self._bin or None
 
     def local_plan(self, dim_k: int):
         """Plan of the LOCAL backward (maxk_sspmm_backward_local), or None when
@@ -644,12 +588,6 @@ class MaxKGraph:
             cands.append(_lib.MAXK_BWD_LOCAL)
         if tile_ok and self.tile_plan(k) is not None:
             cands.append(_lib.MAXK_BWD_TILE)
-        # (k <= 16 only: at k = 32 the records are whole lines and STAGED's layout
-        # serves as well, and the plan's per-bin packing is slow on graphs with few
-        # bins -- Reddit: 914 bins of 125 K edges, 0.45 s)
-        bin_ok = BIN_AUTO and k in (8, 16) and self.bin_plan() is not None
-        if bin_ok:
-            cands.append(_lib.MAXK_BWD_BINNED)
         pair = None
         if ESEL_AUTO and grad.shape[1] <= 256:
             # STAGED_EDGE moves work into the forward (it writes the edge
@@ -660,8 +598,6 @@ class MaxKGraph:
             cands.append(_lib.MAXK_BWD_STAGED_EDGE)
             if _edge_gather_ok(k):
                 cands.append(_lib.MAXK_BWD_EDGE_GATHER)
-            if bin_ok:
-                cands.append(_lib.MAXK_BWD_BINNED_EDGE)
             dummy = self._workspace(("esel_data", k), self.num_cols * k * 4)
             dummy = dummy[: self.num_cols * k * 4].view(torch.float32).view(self.num_cols, k)
             yd = torch.empty((self.num_rows, grad.shape[1]), dtype=torch.float32,
@@ -721,18 +657,16 @@ class MaxKGraph:
 
     def forward_multi(self, cbsr_data: torch.Tensor, cbsr_sel: torch.Tensor,
                       values: torch.Tensor, dim_origin: int = 256,
-                      out: torch.Tensor | None = None, form: str = "auto") -> torch.Tensor:
+                      out: torch.Tensor | None = None) -> torch.Tensor:
         """Fused multi-relation forward (BASELINE config 5, ogbn-proteins):
         Y[q] = A_q . scatter(CBSR) with A_q's values = values[:, q]
         (fp32[E, R], R <= 16).  Returns fp32[R, V, dim_origin]; equals R
-        forward() calls with values[:, q].contiguous().  form: "gather" (the
-        register-accumulator kernel: R = 8, h = 256, k <= 32), "lds" (the
-        relation-vector LDS kernel) or "auto" (gather where it applies)."""
-        return spgemm_forward_multi(self, cbsr_data, cbsr_sel, values, dim_origin, out, form)
+        forward() calls with values[:, q].contiguous() (the relation-vector LDS
+        kernel, maxk_spgemm_forward_multi)."""
+        return spgemm_forward_multi(self, cbsr_data, cbsr_sel, values, dim_origin, out)
 
     def backward_multi(self, grad: torch.Tensor, cbsr_sel: torch.Tensor, values: torch.Tensor,
-                       out: torch.Tensor | None = None, algo: int = _lib.MAXK_BWD_AUTO,
-                       form: str = "auto"):
+                       out: torch.Tensor | None = None, algo: int = _lib.MAXK_BWD_AUTO):
         """Backward of forward_multi: dXs = sum_q (A_q^T G_q) sampled at sel,
         with grad fp32[R, V, h] and values fp32[E, R].  Returns fp32[V, k].
         Algorithms: MAXK_BWD_MULTI_STAGED / MULTI_EDGE_GATHER -- one staged pass
@@ -742,9 +676,7 @@ class MaxKGraph:
         by relation; any single-relation algorithm -- composed from R
         single-relation calls (per-relation value columns cached), summed on the
         device.  AUTO times the fused candidates once per (k, h, R) (MAXK_AUTO=
-        fixed: MULTI_STAGED when it applies, then LOCAL rel8, else composed).  form:
-        phase 1 of the MULTI_* algorithms in register ("gather") or LDS ("lds")
-        form, "auto" = MAXK_MULTI_GATHER's choice; the same bits either way."""
+        fixed: MULTI_STAGED when it applies, then LOCAL rel8, else composed)."""
         check_tensor(grad, "grad_output", torch.float32, dim=3)
         check_tensor(values, "values", torch.float32, dim=2)
         R = values.shape[1]
@@ -822,52 +754,27 @@ class MaxKGraph:
                 raise RuntimeError("multi-relation STAGED backward needs R in {4, 8, 16}, k in "
                                    "{8, 16, 32, 64}, h % 4 == 0 and 16-B aligned grad/values")
             return self._backward_multi_staged(grad, cbsr_sel, values, out,
-                                               algo == _lib.MAXK_BWD_MULTI_EDGE_GATHER, form)
+                                               algo == _lib.MAXK_BWD_MULTI_EDGE_GATHER)
         if algo == _lib.MAXK_BWD_LOCAL and R % 8 == 0 and k == 32 and self.num_edges > 0 \
                 and self.local_plan(k) is not None:
             return self._backward_rel8(grad, cbsr_sel, values, out)
         return self._backward_composed(grad, cbsr_sel, values, out, algo)
 
-    def _backward_multi_staged(self, grad, sel, values, out, edge_order: bool, form: str = "auto"):
+    def _backward_multi_staged(self, grad, sel, values, out, edge_order: bool):
         """One pass for all R relations (maxk_sspmm_backward_multi): phase 1 writes
-        per edge sum_q val[e,q] * G_q[row, sel[c, :]], phase 2 the CSC segmented sum
-        (edge_order: rows in edge order, gathered through the CSC permutation).
-        form: "gather" (phase 1 in registers, maxk_sspmm_backward_multi_gather: R = 8,
-        h = 256, k <= 32), "banked" (R = 8, k = 32: one edge per wave-instruction on
-        bank-ordered selectors, maxk_sspmm_backward_multi_banked), "lds", or "auto"
-        (gather where it applies and MAXK_MULTI_GATHER is on, else banked where it
-        applies and MAXK_MULTI_BANKED is on) -- the same bits in every form."""
+        per edge sum_q val[e,q] * G_q[row, sel[c, :]] (LDS form), phase 2 the CSC
+        segmented sum (edge_order: rows in edge order, gathered through the CSC
+        permutation)."""
         L = _lib.load()
         k, h, R = sel.shape[1], grad.shape[2], values.shape[1]
-        regs = R == 8 and h == 256 and k in (8, 16, 32) and (
-            form == "gather" or (form == "auto" and MULTI_GATHER))
-        if form == "gather" and not regs:
-            raise RuntimeError("the gather form needs R = 8, h = 256 and k in {8, 16, 32}")
-        banked = not regs and R == 8 and k == 32 and (
-            form == "banked" or (form == "auto" and MULTI_BANKED))
-        if form == "banked" and not banked:
-            raise RuntimeError("the banked form needs R = 8 and k = 32")
-        if form not in ("auto", "gather", "banked", "lds"):
-            raise RuntimeError(f"unknown backward_multi form {form!r}")
         cabi = _lib.MAXK_BWD_EDGE_GATHER if edge_order else _lib.MAXK_BWD_STAGED
         csc_pos, csc_indptr, csc_sched, CP = self.csc()
         if edge_order:
             csc_pos = self.csc_perm()
         ws = self._workspace(("bwd", k), L.maxk_backward_workspace_bytes(cabi, self.num_edges, k, CP))
-        fn = L.maxk_sspmm_backward_multi_gather if regs else L.maxk_sspmm_backward_multi
-        sel_arg = sel
-        if banked:
-            # this call's selectors bank-ordered, each | its original entry << 8
-            # (one small pass over sel: 3 B per entry)
-            sp = self._workspace(("bwd_banked", k), self.num_cols * k * 2)
-            sp = sp[: self.num_cols * k * 2].view(torch.int16)
-            _lib.check(L.maxk_cbsr_bank_order_ex(None, sel.data_ptr(), self.num_cols, k, R, None,
-                                                 None, sp.data_ptr(), _stream(out)),
-                       "maxk_cbsr_bank_order_ex")
-            fn, sel_arg = L.maxk_sspmm_backward_multi_banked, sp
-        _lib.check(fn(
+        _lib.check(L.maxk_sspmm_backward_multi(
             cabi, self.bwd_sched.data_ptr(), self.bwd_num_panels, self.indptr.data_ptr(),
-            self.indices.data_ptr(), values.data_ptr(), R, grad.data_ptr(), sel_arg.data_ptr(),
+            self.indices.data_ptr(), values.data_ptr(), R, grad.data_ptr(), sel.data_ptr(),
             self.num_rows, self.num_cols, self.num_edges, h, k, out.data_ptr(), csc_pos.data_ptr(),
             csc_sched.data_ptr(), CP, csc_indptr.data_ptr(), ws.data_ptr(), ws.numel(),
             _stream(out)), "maxk_sspmm_backward_multi")
@@ -1221,8 +1128,7 @@ def spgemm_forward_records(g: MaxKGraph, records: torch.Tensor, k: int, dim_orig
     return out
 
 
-def spgemm_forward_multi(g: MaxKGraph, data, sel, values, dim_origin: int = 256, out=None,
-                         form: str = "auto"):
+def spgemm_forward_multi(g: MaxKGraph, data, sel, values, dim_origin: int = 256, out=None):
     _check_cbsr(g, data, sel)
     k = data.shape[1]
     check_tensor(values, "values", torch.float32, dim=2)
@@ -1243,27 +1149,6 @@ def spgemm_forward_multi(g: MaxKGraph, data, sel, values, dim_origin: int = 256,
         _on_device(g, output=out)
     vals = values if g.num_edges > 0 else torch.zeros((1, R), device=g.device)
     L = _lib.load()
-    if form not in ("auto", "gather", "lds"):
-        raise RuntimeError("form must be 'auto', 'gather' or 'lds'")
-    gather = multi_gather_ok(R, k, dim_origin) and (form == "gather" or
-                                                    (form == "auto" and MULTI_GATHER))
-    if form == "gather" and not gather:
-        raise RuntimeError("the gather form needs R = 8, dim_origin = 256 and k in {4, 8, 16, 32}")
-    if gather:
-        # column-sorted CBSR + per-word column bitmasks (maxk_cbsr_colmask), then the
-        # register-accumulator kernel
-        sd = g._workspace(("colmask_data", k), g.num_cols * k * 4)
-        mr = g._workspace(("colmask_rec",), g.num_cols * 64)
-        _lib.check(L.maxk_cbsr_colmask(data.data_ptr(), sel.data_ptr(), g.num_cols, k, sd.data_ptr(),
-                                       mr.data_ptr(), _stream(out)), "maxk_cbsr_colmask")
-        nbytes = L.maxk_forward_multi_workspace_bytes(g.num_panels, dim_origin, R)
-        ws = g._workspace(("fwd_multi", dim_origin, R), nbytes)
-        _lib.check(L.maxk_spgemm_forward_multi_gather(
-            g.sched.data_ptr(), g.num_panels, g.indptr.data_ptr(), g.indices.data_ptr(),
-            vals.data_ptr(), R, sd.data_ptr(), mr.data_ptr(), g.num_rows, dim_origin, k,
-            out.data_ptr(), ws.data_ptr(), ws.numel(), _stream(out)),
-            "maxk_spgemm_forward_multi_gather")
-        return out
     if MULTI_BANK_ORDER and R % 4 == 0 and k % 8 == 0 and k <= 64:
         # bank-aware entry order for the relation-vector kernel's LDS stores
         # (same CBSR set, bit-identical result)
@@ -1335,23 +1220,6 @@ def sspmm_backward(g: MaxKGraph, grad, sel, out=None, values=None, algo: int = _
             plan["edge_rc"].data_ptr(), ev.data_ptr(), grad.data_ptr(),
             sel.data_ptr(), g.num_rows, dim_origin, k, out.data_ptr(), _stream(out)),
             "maxk_sspmm_backward_local")
-        return out
-    if algo in _BIN_ALGOS:
-        plan = g.bin_plan() if bin_shape_ok(k) else None
-        if plan is None:
-            raise RuntimeError("BINNED backward unsupported for this graph / shape (k in {8, 16, 32})")
-        edge = algo == _lib.MAXK_BWD_BINNED_EDGE
-        sel_arg = g.make_edge_selectors(sel) if edge else sel
-        ws = g._workspace(("bwd_bin", k),
-                          L.maxk_backward_binned_workspace_bytes(plan["num_slots"], k))
-        g.last_bwd_algo = "binned_edge" if edge else "binned"
-        _lib.check(L.maxk_sspmm_backward_binned(
-            g.bwd_sched.data_ptr(), g.bwd_num_panels, g.indptr.data_ptr(), g.indices.data_ptr(),
-            values.data_ptr(), grad.data_ptr(), sel_arg.data_ptr(), int(edge), g.num_rows,
-            g.num_cols, g.num_edges, dim_origin, k, out.data_ptr(), plan["bin_pos"].data_ptr(),
-            plan["bin_ptr"].data_ptr(), plan["bin_dst"].data_ptr(), plan["num_bins"],
-            plan["num_slots"], ws.data_ptr(), ws.numel(), _stream(out)),
-            "maxk_sspmm_backward_binned")
         return out
     csc_pos = csc_indptr = csc_sched = None
     CP = 0

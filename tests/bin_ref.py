@@ -1,8 +1,8 @@
 """Reference restatement of the BINNED backward's plan and of its two phases
-(test infrastructure; the product builds the plan on the device,
-maxk_bin_plan_build in spgemm_new_amd/csrc/maxk_plan.hip).
+(test infrastructure; the ablation library builds the plan on the device,
+maxk_bin_plan_build in tools/variants_lib/maxk_variants_plan.hip).
 
-Plan (include/maxk_spgemm.h, BINNED): destination bin b = columns
+Plan (tools/variants_lib/maxk_variants.h, BINNED): destination bin b = columns
 [b*255, b*255 + 255); a bin's in-edges ordered by (XCD of the edge's phase-1
 panel = (panel // 4) % 8, edge id), then packed first-fit into windows of 64
 slots with distinct destinations, at most 8 windows open (the oldest closed,

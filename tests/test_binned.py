@@ -1,5 +1,6 @@
 """BINNED backward (propagation blocking: products into destination bins, bins
-summed in LDS; include/maxk_spgemm.h).
+summed in LDS).  Measured slower than STAGED / EDGE_GATHER at every k (DESIGN.md
+§5), so it lives in the ablation build (tools/variants_lib, maxk_variants.h).
 
 CPU: the plan restatement (tests/bin_ref.py) keeps its invariants -- every
 edge in exactly one slot of its destination's bin, windows of 64 with distinct
@@ -8,12 +9,18 @@ emulation equals the oracle's backward (spmm_maxk_backward.cu:15-115 semantics).
 GPU: the device plan is bit-identical to the restatement, the kernels
 bit-identical to the emulation (same fp32 products, same slot-order sums), and
 within 1e-4 of the oracle, node and edge selectors, k in {8, 16, 32}."""
+import os
+import sys
+
 import numpy as np
 import pytest
 import torch
 
 from spgemm_new_amd.graphs import random_cbsr, small_csr
 from tests import bin_ref
+
+sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))),
+                                "tools", "variants_lib"))
 
 TOL = 1e-4
 
@@ -105,8 +112,9 @@ def _graph(dev, kind, num_cols=None):
 @pytest.mark.gpu
 @pytest.mark.parametrize("kind", ["small", "hub", "rect"])
 def test_device_plan_equals_reference(dev, kind):
+    import variants as V
     g, indptr, indices, values = _graph(dev, kind)
-    plan = g.bin_plan()
+    plan = V.bin_plan(g)
     assert plan is not None
     starts = g.bwd_sched.view(-1, 2)[:, 1].cpu().numpy()
     pos, ptr, dst, slots = bin_ref.build(starts, indices, g.num_cols)
@@ -121,61 +129,55 @@ def test_device_plan_equals_reference(dev, kind):
 @pytest.mark.parametrize("kind", ["small", "hub", "rect"])
 @pytest.mark.parametrize("h", [256, 100])
 def test_binned_backward(dev, oracle, k, kind, h):
-    from spgemm_new_amd import _lib
+    import variants as V
     g, indptr, indices, values = _graph(dev, kind)
     C = g.num_cols
     _, sel = random_cbsr(C, k, h, seed=50 + k)
     grad = np.random.default_rng(k).random((g.num_rows, h), dtype=np.float32)
-    plan = g.bin_plan()
+    plan = V.bin_plan(g)
     starts = g.bwd_sched.view(-1, 2)[:, 1].cpu().numpy()
     ref_plan = bin_ref.build(starts, indices, C)
     emu = bin_ref.backward(indptr, indices, values, grad, sel, C, ref_plan)
     ref = oracle.np_backward(indptr, indices, values, grad, sel) if kind != "rect" else \
         oracle.c_backward_csr(indptr, indices, values, grad, sel)
     G, Sel = T(grad, dev), T(sel, dev)
-    for algo in (_lib.MAXK_BWD_BINNED, _lib.MAXK_BWD_BINNED_EDGE):
+    for edge in (False, True):
         out = torch.full((C, k), float("nan"), device=dev)
-        g.backward(G, Sel, out=out, algo=algo)
+        V.backward_binned(g, G, Sel, plan, edge=edge, out=out)
         got = out.cpu().numpy()
-        assert np.array_equal(got, emu), (algo, np.abs(got - emu).max())
+        assert np.array_equal(got, emu), (edge, np.abs(got - emu).max())
         assert oracle.parity_error(got, ref) <= TOL
-        again = g.backward(G, Sel, algo=algo)
+        again = V.backward_binned(g, G, Sel, plan, edge=edge)
         assert torch.equal(again, out)                 # deterministic
     assert plan["num_slots"] >= g.num_edges
 
 
 @pytest.mark.gpu
-def test_binned_values_per_call_and_autograd_auto(dev, oracle):
-    """Per-call edge values; and AUTO may pick BINNED (its result stays within
-    tolerance whichever algorithm wins)."""
-    from spgemm_new_amd import _lib
+def test_binned_values_per_call(dev, oracle):
+    """Per-call edge values."""
+    import variants as V
     g, indptr, indices, values = _graph(dev, "small")
     k, h = 8, 256
     _, sel = random_cbsr(g.num_cols, k, h, seed=3)
     grad = np.random.default_rng(5).random((g.num_rows, h), dtype=np.float32)
     w = np.random.default_rng(6).random(len(indices), dtype=np.float32)
-    out = g.backward(T(grad, dev), T(sel, dev), values=T(w, dev), algo=_lib.MAXK_BWD_BINNED)
+    out = V.backward_binned(g, T(grad, dev), T(sel, dev), V.bin_plan(g), values=T(w, dev))
     assert oracle.parity_error(out.cpu().numpy(),
                                oracle.np_backward(indptr, indices, w, grad, sel)) <= TOL
-    out = g.backward(T(grad, dev), T(sel, dev))
-    assert oracle.parity_error(out.cpu().numpy(),
-                               oracle.np_backward(indptr, indices, values, grad, sel)) <= TOL
 
 
 @pytest.mark.gpu
 def test_binned_plan_refused_for_heavy_padding(dev):
     """A destination with a huge in-degree needs a window per in-edge: the plan
-    is dropped (too many padding slots) and BINNED raises; AUTO skips it."""
+    is dropped (too many padding slots) and BINNED raises."""
     import spgemm_new_amd as S
-    from spgemm_new_amd import _lib
+    import variants as V
     v = 4000
     indptr = np.arange(v + 1, dtype=np.int32)            # every row -> column 0
     indices = np.zeros(v, np.int32)
     g = S.MaxKGraph(T(indptr, dev), T(indices, dev))
-    assert g.bin_plan() is None
+    assert V.bin_plan(g) is None
     _, sel = random_cbsr(v, 8, 256, seed=1)
     G = torch.rand((v, 256), device=dev)
     with pytest.raises(RuntimeError):
-        g.backward(G, T(sel, dev), algo=_lib.MAXK_BWD_BINNED)
-    g.backward(G, T(sel, dev))    # AUTO: another algorithm
-    assert g.last_bwd_algo not in ("binned", "binned_edge")
+        V.backward_binned(g, G, T(sel, dev), None)

@@ -43,18 +43,15 @@ def test_harness_runs_and_validates(tmp_path):
                      "maxk_backward_local"]
             if k in (32, 64):
                 algos.append("maxk_backward_tile")   # the TILE plan through the C ABI
-            if k in (16, 32):
-                algos.append("maxk_backward_binned")   # the BINNED plan through the C ABI
             fwds = ["maxk"] + (["maxk_blocked4"] if k >= 32 else [])   # column-blocked forward
             for kern in fwds + ["maxk_backward"] + algos:
                 assert times[(g, k, kern)] > 0, (g, k, kern)
             assert times[(g, k, "maxk_backward")] == min(times[(g, k, a)] for a in algos)
     checks = [ln for ln in lines if "validation" in ln]
-    # per graph: k=16 fwd + staged + staged_edge + local + binned; k=32 and k=64 also tile
-    # and the blocked forward; binned at k = 16 and 32
-    assert len(checks) == 2 * (5 + 7 + 6), checks
+    # per graph: k=16 fwd + staged + staged_edge + local; k=32 and k=64 also tile
+    # and the blocked forward
+    assert len(checks) == 2 * (4 + 6 + 6), checks
     assert all("validation pass!" in ln for ln in checks), checks
     assert sum("backward tile vs atomic" in ln for ln in checks) == 4
-    assert sum("backward binned vs atomic" in ln for ln in checks) == 4
     assert sum("forward blocked4 vs plain" in ln for ln in checks) == 4
     assert np.isfinite(list(times.values())).all()

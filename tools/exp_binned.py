@@ -14,6 +14,9 @@ from spgemm_new_amd import _lib  # noqa: E402
 from spgemm_new_amd.graphs import CONFIGS, synthetic_columns, synthetic_indptr, synthetic_values  # noqa: E402
 from spgemm_new_amd.ops import _ESEL_ALGOS, topk_cbsr  # noqa: E402
 
+sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), "variants_lib"))
+import variants as VL  # noqa: E402  (BINNED lives in the ablation build)
+
 
 def ms_of(fn, n=10):
     fn()
@@ -39,7 +42,7 @@ def main():
     values = synthetic_values(123, 0, E, device=dev)
     g = S.MaxKGraph(indptr, indices, values)
     t1 = time.time()
-    plan = g.bin_plan()
+    plan = VL.bin_plan(g)
     torch.cuda.synchronize()
     print(f"graph {time.time() - t0:.1f}s, bin plan {time.time() - t1:.2f}s: slots "
           f"{plan['num_slots']} ({plan['num_slots'] / E:.4f} per edge), bins {plan['num_bins']}",
@@ -50,8 +53,8 @@ def main():
     G = torch.rand((V, 256), generator=gen, device=dev)
     y = torch.empty((V, 256), device=dev)
     names = {_lib.MAXK_BWD_STAGED: "staged", _lib.MAXK_BWD_STAGED_EDGE: "staged_edge",
-             _lib.MAXK_BWD_EDGE_GATHER: "edge_gather", _lib.MAXK_BWD_BINNED: "binned",
-             _lib.MAXK_BWD_BINNED_EDGE: "binned_edge"}
+             _lib.MAXK_BWD_EDGE_GATHER: "edge_gather", VL.MAXK_BWD_BINNED: "binned",
+             VL.MAXK_BWD_BINNED_EDGE: "binned_edge"}
     for k in ks:
         data, sel = topk_cbsr(X, k)
         dx = torch.empty((V, k), device=dev)
@@ -61,9 +64,13 @@ def main():
                 continue
             if only and name not in only.split(","):
                 continue
-            esel = a in _ESEL_ALGOS
+            esel = a in _ESEL_ALGOS or a == VL.MAXK_BWD_BINNED_EDGE
             f = ms_of(lambda: g.forward(data, sel, 256, out=y, edge_sel=esel))
-            b = ms_of(lambda: g.backward(G, sel, out=dx, algo=a))
+            if a in (VL.MAXK_BWD_BINNED, VL.MAXK_BWD_BINNED_EDGE):
+                b = ms_of(lambda: VL.backward_binned(g, G, sel, plan,
+                                                     edge=a == VL.MAXK_BWD_BINNED_EDGE, out=dx))
+            else:
+                b = ms_of(lambda: g.backward(G, sel, out=dx, algo=a))
             err = float(((dx - ref).abs() / ref.abs().clamp_min(1)).max())
             print(f"k={k} {name:12s} fwd {f:.3f} bwd {b:.3f} sum {f + b:.3f} ms  rel {err:.2e}",
                   flush=True)

@@ -17,6 +17,9 @@ from spgemm_new_amd import _lib  # noqa: E402
 from spgemm_new_amd.graphs import CONFIGS, synthetic_columns, synthetic_indptr, synthetic_values  # noqa: E402
 from spgemm_new_amd.ops import _min_ms  # noqa: E402
 
+sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), "variants_lib"))
+import variants as VL  # noqa: E402  (the ablation build: register / bank-ordered forms)
+
 
 def main():
     ap = argparse.ArgumentParser()
@@ -38,20 +41,15 @@ def main():
     data, sel = S.topk_cbsr(X, k)
     y = torch.empty((R, V, h), device=dev)
     dx = torch.empty((V, k), device=dev)
+    ms, me = _lib.MAXK_BWD_MULTI_STAGED, _lib.MAXK_BWD_MULTI_EDGE_GATHER
     calls = {
-        "fwd lds": lambda: g.forward_multi(data, sel, vals, h, out=y, form="lds"),
-        "fwd gather": lambda: g.forward_multi(data, sel, vals, h, out=y, form="gather"),
-        "bwd lds": lambda: g.backward_multi(G, sel, vals, out=dx, algo=_lib.MAXK_BWD_MULTI_STAGED,
-                                            form="lds"),
-        "bwd regs": lambda: g.backward_multi(G, sel, vals, out=dx,
-                                             algo=_lib.MAXK_BWD_MULTI_STAGED, form="gather"),
-        "bwd banked": lambda: g.backward_multi(G, sel, vals, out=dx,
-                                               algo=_lib.MAXK_BWD_MULTI_STAGED, form="banked"),
-        "bwd eg lds": lambda: g.backward_multi(G, sel, vals, out=dx,
-                                               algo=_lib.MAXK_BWD_MULTI_EDGE_GATHER, form="lds"),
-        "bwd eg banked": lambda: g.backward_multi(G, sel, vals, out=dx,
-                                                  algo=_lib.MAXK_BWD_MULTI_EDGE_GATHER,
-                                                  form="banked"),
+        "fwd lds": lambda: g.forward_multi(data, sel, vals, h, out=y),
+        "fwd gather": lambda: VL.forward_multi_gather(g, data, sel, vals, h, out=y),
+        "bwd lds": lambda: g.backward_multi(G, sel, vals, out=dx, algo=ms),
+        "bwd regs": lambda: VL.backward_multi_form(g, G, sel, vals, "gather", False, out=dx),
+        "bwd banked": lambda: VL.backward_multi_form(g, G, sel, vals, "banked", False, out=dx),
+        "bwd eg lds": lambda: g.backward_multi(G, sel, vals, out=dx, algo=me),
+        "bwd eg banked": lambda: VL.backward_multi_form(g, G, sel, vals, "banked", True, out=dx),
     }
     only = [x.strip() for x in a.only.split(",") if x.strip()]
     for name, fn in calls.items():
