@@ -169,14 +169,24 @@ __global__ __launch_bounds__(256) void exclusive_scan_1block(int32_t *c, int n, 
 // at <= 8 KB per wave for every k >= 8.
 // ---------------------------------------------------------------------------
 #ifndef FWD_VEC16
-#define FWD_VEC16 2   // CBSR entries per lane at k = 16 (development knob)
+// CBSR entries per lane at k = 16: 1 (16 lanes per edge, 4 row copies) measured
+// 3.16 ms against 4.14 ms for 2 on products (round 5, tools/exp_fwd_small_k.py)
+#define FWD_VEC16 1
 #endif
 #ifndef FWD_VEC8
 #define FWD_VEC8 1    // ... at k = 8
 #endif
+#ifndef FWD_VEC32
+#define FWD_VEC32 4   // ... at k = 32 (development knob)
+#endif
+#ifndef FWD_VEC64
+#define FWD_VEC64 4   // ... at k = 64 (development knob)
+#endif
 template <int K>
 struct FwdLayout {
-    static constexpr int VEC = K >= 32 ? 4 : (K >= 16 ? FWD_VEC16 : (K >= 8 ? FWD_VEC8 : 1));
+    static constexpr int VEC = K > 64 ? 4 : K == 64 ? FWD_VEC64
+                             : K >= 32 ? FWD_VEC32
+                             : (K >= 16 ? FWD_VEC16 : (K >= 8 ? FWD_VEC8 : 1));
     static constexpr int LPE = K / VEC;
     static constexpr int EPS = kWave / LPE;
 };
@@ -257,6 +267,9 @@ __device__ __forceinline__ void fwd_edges_vec(int e0, int e1, const int32_t *__r
 #ifndef FWD_U
 #define FWD_U 8
 #endif
+#ifndef FWD_ABLATE
+#define FWD_ABLATE 0  // development timing ablations (results wrong): bits 1 / 2 / 4 below
+#endif
     constexpr int U = STEPS < FWD_U ? STEPS : FWD_U;  // gathers in flight per lane
     using D = typename VecT<VEC>::D;
     using SB = typename VecT<VEC>::S;
@@ -264,6 +277,9 @@ __device__ __forceinline__ void fwd_edges_vec(int e0, int e1, const int32_t *__r
     const int sub = lane % LPE;
     const int slot = lane / LPE;
     float *my_acc = acc + slot * kMaxDim;
+#if FWD_ABLATE & 1
+    float ablate_sink = 0.f;
+#endif
     for (int base = e0; base < e1; base += kWave) {
         const int n = (e1 - base) < kWave ? (e1 - base) : kWave;
         int my_c = 0;
@@ -283,6 +299,12 @@ __device__ __forceinline__ void fwd_edges_vec(int e0, int e1, const int32_t *__r
                 const int t = (s0 + u) * EPS + slot;
                 const int c = __shfl(my_c, t < kWave ? t : 0);
                 v[u] = __shfl(my_v, t < kWave ? t : 0);
+#if FWD_ABLATE & 4  // no gathers: lane-made data and distinct selectors
+                if (true) {
+                    d[u] = D{} + v[u];
+                    sb[u] = (SB)(0x03020100u * 0 + (uint32_t)(sub * VEC) * 0x01010101u + 0x03020100u);
+                } else
+#endif
                 if (t < n) {
                     if constexpr (RS == 0) {
                         const size_t off = (size_t)c * K + sub * VEC;
@@ -310,7 +332,15 @@ __device__ __forceinline__ void fwd_edges_vec(int e0, int e1, const int32_t *__r
 #pragma unroll
             for (int u = 0; u < U; ++u) {
                 const int t = (s0 + u) * EPS + slot;
+#if FWD_ABLATE & 1  // no LDS read-modify-write: the products summed in a register
+                if (t < n) {
+                    if constexpr (VEC == 4) ablate_sink += v[u] * (d[u].x + d[u].y + d[u].z + d[u].w) + (float)sb[u];
+                    else if constexpr (VEC == 2) ablate_sink += v[u] * (d[u].x + d[u].y) + (float)sb[u];
+                    else ablate_sink += v[u] * d[u] + (float)sb[u];
+                }
+#else
                 if (t < n) rmw_acc<VEC>(my_acc, sb[u], v[u], d[u]);
+#endif
                 if constexpr (ESEL) {
                     // one dword store per 4 selector bytes: neighbouring lanes of the
                     // edge hand theirs over (byte / short stores ran at ~1 TB/s)
@@ -341,7 +371,11 @@ __device__ __forceinline__ void fwd_edges_vec(int e0, int e1, const int32_t *__r
             }
         }
     }
+#if FWD_ABLATE & 1
+    my_acc[lane] += ablate_sink;   // keeps the sums live (one LDS op per call)
+#endif
 }
+
 
 // Any k: one CBSR entry per lane, EPS = 64 / min(k, 64) row copies.
 __device__ __forceinline__ void fwd_edges_scalar(int e0, int e1, int k,
@@ -417,6 +451,9 @@ __device__ __forceinline__ void flush_row(float *acc, int copies, float *__restr
         for (int c4 = lane; c4 < (dim >> 2); c4 += kWave) {
             f4 a = reinterpret_cast<f4 *>(acc)[c4];
             reinterpret_cast<f4 *>(acc)[c4] = f4{0.f, 0.f, 0.f, 0.f};
+#if FWD_ABLATE & 2  // timing ablation: copy 0 only (the other copies neither summed nor zeroed)
+            copies = 1;
+#endif
             for (int cp = 1; cp < copies; ++cp) {
                 f4 *q = reinterpret_cast<f4 *>(acc + cp * kMaxDim) + c4;
                 a += *q;

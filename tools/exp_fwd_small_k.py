@@ -25,7 +25,8 @@ def med(fn, n=20):
 
 
 dev = torch.device("cuda", 0)
-V, E = CONFIGS["products"]
+GRAPH = os.environ.get("GRAPH", "products")
+V, E = CONFIGS[GRAPH]
 indptr = synthetic_indptr(V, E, seed=123, device=dev)
 g = S.MaxKGraph(indptr, synthetic_columns(indptr, seed=123), synthetic_values(123, 0, E, device=dev))
 gen = torch.Generator(device=dev)
@@ -36,4 +37,4 @@ ref = {}
 for k in [int(a) for a in sys.argv[1:]] or [8, 16]:
     data, sel = topk_cbsr(X, k)
     ms = med(lambda: g.forward(data, sel, 256, out=y))
-    print(f"k={k} fwd {ms:.3f} ms  checksum {float(y.double().sum()):.6e}", flush=True)
+    print(f"{GRAPH} k={k} fwd {ms:.3f} ms  checksum {float(y.double().sum()):.6e}", flush=True)
