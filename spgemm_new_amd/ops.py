@@ -529,7 +529,8 @@ class MaxKGraph:
         picks on the BASELINE shapes, so the algorithm -- and every
         bit of the result -- repeats on every box: TILE on long-row graphs (mean
         degree >= 128: Reddit, proteins) and at k = 64; else LOCAL when the gradient
-        fits a few source bands (small graphs); else, on large short-row graphs
+        fits a few source bands (small graphs); else TILE when the destinations fit
+        one group per CU (small rank blocks); else, on large short-row graphs
         (products), EDGE_GATHER at k = 8, STAGED_EDGE at k = 32 (both with the
         forward writing the edge selectors) and STAGED otherwise."""
         long_rows = self.num_edges >= FWD_BLOCKED_MIN_DEGREE * max(self.num_rows, 1)
@@ -538,6 +539,15 @@ class MaxKGraph:
             return _lib.MAXK_BWD_TILE
         if self.num_rows * h * 4 <= 8 * LOCAL_BAND_BYTES and self.local_plan(k) is not None:
             return _lib.MAXK_BWD_LOCAL
+        if own and TILE_AUTO and tile_shape_ok(k, h) and self.device.type == "cuda":
+            # destinations that fit one TILE group per CU (a rank's own-column block at
+            # products N=8: 306 K columns, TILE 0.455 vs STAGED 0.566 ms fwd+bwd measured,
+            # profiles/r5_rank_products_n8_candidates.txt); BASELINE's N=1 shapes are
+            # unchanged (Reddit / proteins are long-row, products has 2.45 M columns)
+            from . import tile
+            cus = torch.cuda.get_device_properties(self.device).multi_processor_count
+            if self.num_cols <= tile.max_group(k) * cus and self.tile_plan(k) is not None:
+                return _lib.MAXK_BWD_TILE
         if ESEL_AUTO and h <= 256 and k == 8:
             return _lib.MAXK_BWD_EDGE_GATHER
         if ESEL_AUTO and h <= 256 and k == 32:
