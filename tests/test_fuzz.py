@@ -119,3 +119,54 @@ def test_fuzz_parity(dev, oracle, seed):
         g.backward_multi(T(g8, dev), sel, T(vals8, dev), out=dx8, algo=_lib.MAXK_BWD_LOCAL)
         ref8 = sum(oracle.np_backward(indptr, indices, vals8[:, q], g8[q], sel_np) for q in range(8))
         assert oracle.parity_error(dx8.cpu().numpy(), ref8) <= TOL, f"{ctx} rel8"
+
+
+@pytest.mark.parametrize("seed", range(128, 224))
+def test_fuzz_parity_fast_paths(dev, oracle, seed):
+    """The same random problems through the forms the sweep above leaves to
+    AUTO: the forward that also writes the edge selectors and the two
+    backwards that read them (STAGED_EDGE, EDGE_GATHER), the column-blocked
+    forward (random block count), and TILE (k = 32 / 64, h = 256) with a
+    random number of source ranges per destination group."""
+    from spgemm_new_amd import ops
+    rng, V, C, indptr, indices, values, k, h, pc, rc = draw(seed)
+    if rng.random() < 0.5 and k not in (32, 64):
+        k = int(rng.choice([32, 64]))          # TILE / blocked shapes more often
+        h = 256 if rng.random() < 0.7 else max(h, k)
+    h = max(h, k)
+    x = rng.standard_normal((C, h)).astype(np.float32)
+    grad = rng.standard_normal((V, h)).astype(np.float32)
+    splits = int(rng.integers(1, 5))
+    g = S.MaxKGraph(T(indptr, dev), T(indices, dev), T(values, dev), num_cols=C,
+                    panel_cost=pc, row_cost=rc, tile_splits=splits)
+    ctx = f"V={V} C={C} E={len(indices)} k={k} h={h} panel_cost={pc} row_cost={rc} splits={splits}"
+    data, sel = S.topk_cbsr(T(x, dev), k)
+    sel_np, data_np = sel.cpu().numpy(), data.cpu().numpy()
+    ref = oracle.np_forward(indptr, indices, values, data_np, sel_np, h)
+    ref_b = oracle.np_backward(indptr, indices, values, grad, sel_np)
+    G = T(grad, dev)
+
+    # forward writing the edge selectors, then the backwards that read them
+    out = torch.full((V, h), float("nan"), device=dev)
+    y = ops.spgemm_forward(g, data, sel, h, out=out, edge_sel=True)
+    assert oracle.parity_error(y.cpu().numpy(), ref) <= TOL, f"{ctx} esel forward"
+    algos = [_lib.MAXK_BWD_STAGED_EDGE]
+    if ops._edge_gather_ok(k):
+        algos.append(_lib.MAXK_BWD_EDGE_GATHER)
+    for a in algos:
+        dx = torch.full((C, k), float("nan"), device=dev)
+        g.backward(G, sel, out=dx, algo=a)
+        assert oracle.parity_error(dx.cpu().numpy(), ref_b) <= TOL, f"{ctx} algo={a}"
+
+    # column-blocked forward (the restacked CSR, partial outputs, fused last block)
+    if len(indices) > 0:
+        nb = int(rng.integers(1, 9))
+        out = torch.full((V, h), float("nan"), device=dev)
+        ops._forward_blocked(g, nb, data, sel, h, out, g.values)
+        assert oracle.parity_error(out.cpu().numpy(), ref) <= TOL, f"{ctx} blocked nb={nb}"
+
+    # TILE (its plan may decline a shape: the other algorithms serve it)
+    if k in (32, 64) and h == 256 and len(indices) > 0 and g.tile_plan(k) is not None:
+        dx = torch.full((C, k), float("nan"), device=dev)
+        g.backward(G, sel, out=dx, algo=_lib.MAXK_BWD_TILE)
+        assert oracle.parity_error(dx.cpu().numpy(), ref_b) <= TOL, f"{ctx} TILE"
