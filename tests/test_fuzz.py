@@ -127,7 +127,8 @@ def test_fuzz_parity_fast_paths(dev, oracle, seed):
     AUTO: the forward that also writes the edge selectors and the two
     backwards that read them (STAGED_EDGE, EDGE_GATHER), the column-blocked
     forward (random block count), and TILE (k = 32 / 64, h = 256) with a
-    random number of source ranges per destination group."""
+    random number of source ranges per destination group; and the fused
+    multi-relation forward with both fused multi-relation backwards (R = 4, 8, 16)."""
     from spgemm_new_amd import ops
     rng, V, C, indptr, indices, values, k, h, pc, rc = draw(seed)
     if rng.random() < 0.5 and k not in (32, 64):
@@ -170,3 +171,19 @@ def test_fuzz_parity_fast_paths(dev, oracle, seed):
         dx = torch.full((C, k), float("nan"), device=dev)
         g.backward(G, sel, out=dx, algo=_lib.MAXK_BWD_TILE)
         assert oracle.parity_error(dx.cpu().numpy(), ref_b) <= TOL, f"{ctx} TILE"
+
+    # fused multi-relation forward and both fused multi-relation backwards
+    if k in (8, 16, 32, 64) and len(indices) > 0 and h % 4 == 0:
+        R = int(rng.choice([4, 8, 16]))
+        vals = rng.standard_normal((len(indices), R)).astype(np.float32)
+        gm = rng.standard_normal((R, V, h)).astype(np.float32)
+        ym = g.forward_multi(data, sel, T(vals, dev), h).cpu().numpy()
+        ref_m = np.zeros((C, k))
+        for q in range(R):
+            refq = oracle.np_forward(indptr, indices, vals[:, q], data_np, sel_np, h)
+            assert oracle.parity_error(ym[q], refq) <= TOL, f"{ctx} R={R} q={q}"
+            ref_m += oracle.np_backward(indptr, indices, vals[:, q], gm[q], sel_np)
+        for a in (_lib.MAXK_BWD_MULTI_STAGED, _lib.MAXK_BWD_MULTI_EDGE_GATHER):
+            dxm = torch.full((C, k), float("nan"), device=dev)
+            g.backward_multi(T(gm, dev), sel, T(vals, dev), out=dxm, algo=a)
+            assert oracle.parity_error(dxm.cpu().numpy(), ref_m) <= TOL, f"{ctx} R={R} algo={a}"
