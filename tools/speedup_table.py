@@ -61,8 +61,9 @@ def main():
             del a
         for k in args.ks:
             data, sel = S.topk_cbsr(X, k)
-            fwd_ms = ev_ms(lambda: g.forward(data, sel, args.h))
-            g.backward(G, sel)   # AUTO: measure once, then cached
+            g.backward(G, sel)   # AUTO's choice first (measured once, or by rule, then cached):
+            # when it reads edge selectors the forward writes them, as in a training step
+            fwd_ms = ev_ms(lambda: g.forward(data, sel, args.h, edge_sel="auto"))
             bwd_ms = ev_ms(lambda: g.backward(G, sel))
             r = {"graph": name, "V": V, "E": E, "h": args.h, "k": k, "fwd_ms": round(fwd_ms, 3),
                  "bwd_ms": round(bwd_ms, 3), "bwd_algo": g.last_bwd_algo,
