@@ -71,6 +71,11 @@ MIN_PANELS = int(os.environ.get("MAXK_MIN_PANELS", 16384))
 TILE_AUTO = os.environ.get("MAXK_TILE", "1") != "0"
 # STAGED_EDGE backward (edge selectors written by the forward) among the AUTO candidates
 ESEL_AUTO = os.environ.get("MAXK_ESEL", "1") != "0"
+# MAXK_AUTO=fixed takes STAGED_EDGE at k = 32 only when the selector table (num_cols * k
+# bytes) is at least this large: smaller tables keep STAGED's per-edge selector reads in
+# the caches (products rank blocks at N = 2 / 4, 39 / 20 MB: STAGED 3.74 / 1.33 ms vs
+# STAGED_EDGE 3.88 / 1.48 fwd + bwd; products N = 1, 78 MB: STAGED_EDGE)
+ESEL_MIN_SEL_BYTES = int(os.environ.get("MAXK_ESEL_MIN_SEL_BYTES", 64 << 20))
 # AUTO backward: "measure" (time the candidates once per graph and shape; the fastest
 # is kept) or "fixed" (a rule of the shape alone, no timing: the same algorithm -- and
 # so the same fp32 summation order -- on every run and machine)
@@ -531,8 +536,9 @@ class MaxKGraph:
         degree >= 128: Reddit, proteins) and at k = 64; else LOCAL when the gradient
         fits a few source bands (small graphs); else TILE when the destinations fit
         one group per CU (small rank blocks); else, on large short-row graphs
-        (products), EDGE_GATHER at k = 8, STAGED_EDGE at k = 32 (both with the
-        forward writing the edge selectors) and STAGED otherwise."""
+        (products), EDGE_GATHER at k = 8, STAGED_EDGE at k = 32 when the selector
+        table reaches ESEL_MIN_SEL_BYTES (both with the forward writing the edge
+        selectors) and STAGED otherwise."""
         long_rows = self.num_edges >= FWD_BLOCKED_MIN_DEGREE * max(self.num_rows, 1)
         if (own and TILE_AUTO and tile_shape_ok(k, h) and (long_rows or k == 64)
                 and self.tile_plan(k) is not None):
@@ -550,7 +556,7 @@ class MaxKGraph:
                 return _lib.MAXK_BWD_TILE
         if ESEL_AUTO and h <= 256 and k == 8:
             return _lib.MAXK_BWD_EDGE_GATHER
-        if ESEL_AUTO and h <= 256 and k == 32:
+        if ESEL_AUTO and h <= 256 and k == 32 and self.num_cols * k >= ESEL_MIN_SEL_BYTES:
             return _lib.MAXK_BWD_STAGED_EDGE
         return _lib.MAXK_BWD_STAGED
 

@@ -118,6 +118,9 @@ def main():
             lb = Loopback(indptr, indices, bounds, p, data, sel)
             D.a2a = lb
             D.ag = GatherLoopback(bounds, data, sel)
+            # no process group here: the collective decisions (halo mode, overlap) take
+            # this rank's own values, as if every rank had the same
+            D.PartitionedMaxK._max_over_ranks = lambda self, *xs: xs[0] if len(xs) == 1 else list(xs)
             m = D.PartitionedMaxK(indptr, indices, values, p, world, dev, records=not a.rows,
                                   halo_mode=a.halo_mode if world > 1 else "records",
                                   overlap=not a.no_overlap)
