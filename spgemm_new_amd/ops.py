@@ -705,6 +705,10 @@ class MaxKGraph:
         k = cbsr_sel.shape[1]
         if out is None:
             out = torch.empty((self.num_cols, k), dtype=torch.float32, device=self.device)
+        if self.num_cols == 0:
+            return out
+        if self.num_rows == 0:
+            return out.zero_()   # an empty block: dXs = 0
         staged_ok = (R in (4, 8, 16) and k in (8, 16, 32, 64) and grad.shape[2] % 4 == 0
                      and self.num_edges > 0 and values.data_ptr() % 16 == 0
                      and grad.data_ptr() % 16 == 0)
@@ -941,6 +945,8 @@ def spgemm_forward(g: MaxKGraph, data, sel, dim_origin: int = 256, out=None, val
         if tuple(out.shape) != (g.num_rows, dim_origin):
             raise RuntimeError("output has the wrong shape")
         _on_device(g, output=out)
+    if g.num_rows == 0:
+        return out   # an empty block (a rank of the row partition that owns no row)
     L = _lib.load()
     nbytes = L.maxk_forward_workspace_bytes(g.num_panels, dim_origin)
     ws = g._workspace(("fwd", dim_origin), nbytes)
@@ -1133,6 +1139,8 @@ def spgemm_forward_records(g: MaxKGraph, records: torch.Tensor, k: int, dim_orig
         if tuple(out.shape) != (g.num_rows, dim_origin):
             raise RuntimeError("output has the wrong shape")
         _on_device(g, output=out)
+    if g.num_rows == 0:
+        return out
     L = _lib.load()
     nbytes = L.maxk_forward_workspace_bytes(g.num_panels, dim_origin)
     ws = g._workspace(("fwd", dim_origin), nbytes)
@@ -1163,6 +1171,8 @@ def spgemm_forward_multi(g: MaxKGraph, data, sel, values, dim_origin: int = 256,
         if tuple(out.shape) != (R, g.num_rows, dim_origin):
             raise RuntimeError("output must be [R, V, dim_origin]")
         _on_device(g, output=out)
+    if g.num_rows == 0:
+        return out
     vals = values if g.num_edges > 0 else torch.zeros((1, R), device=g.device)
     L = _lib.load()
     if MULTI_BANK_ORDER and R % 4 == 0 and k % 8 == 0 and k <= 64:
@@ -1200,6 +1210,10 @@ def sspmm_backward(g: MaxKGraph, grad, sel, out=None, values=None, algo: int = _
         if tuple(out.shape) != (g.num_cols, k):
             raise RuntimeError("grad_input has the wrong shape")
         _on_device(g, grad_input=out)
+    if g.num_cols == 0:
+        return out
+    if g.num_rows == 0:
+        return out.zero_()   # no gradient rows, no edges: dXs = 0
     if algo == _lib.MAXK_BWD_AUTO:
         algo = g.autotune_backward(grad, sel, out, values)
         if algo in _ESEL_ALGOS and g.edge_selectors(sel) is None:

@@ -758,3 +758,62 @@ def test_partitioned_hip_engine_sweep(cfg):
     if cfg["halo"] == "allgather" and cfg["overlap"]:
         assert mode == "allgather"
     assert ey <= 1e-4 and ed <= 1e-4, (ey, ed, mode, overlap)
+
+
+def _tiny_worker(rank, world, port, q, V, overlap):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from spgemm_new_amd.distributed import PartitionedMaxK
+        dev = torch.device("cuda:0")
+        rng = np.random.default_rng(5)
+        deg = rng.integers(0, V + 1, V)
+        deg[0] = V                                   # one full row
+        indptr = np.zeros(V + 1, np.int64)
+        indptr[1:] = np.cumsum(deg)
+        indices = np.concatenate([np.sort(rng.choice(V, d, replace=False)) for d in deg]
+                                 ).astype(np.int32)
+        values = rng.random(len(indices)).astype(np.float32)
+        k, h = 8, 64
+        data, sel = random_cbsr(V, k, h, seed=2)
+        grad = rng.random((V, h)).astype(np.float32)
+        m = PartitionedMaxK(torch.from_numpy(indptr.astype(np.int32)).to(dev),
+                            torch.from_numpy(indices).to(dev), torch.from_numpy(values).to(dev),
+                            rank, world, dev, overlap=overlap)
+        td = lambda a: m.local_rows(torch.from_numpy(a).to(dev))  # noqa: E731
+        sel_l = td(sel)
+        y = m.forward(td(data), sel_l, h)
+        dx = m.backward(td(grad), sel_l)
+        torch.cuda.synchronize()
+        ys, dxs = [None] * world, [None] * world
+        dist.all_gather_object(ys, y.cpu().numpy())
+        dist.all_gather_object(dxs, dx.cpu().numpy())
+        if rank == 0:
+            from oracle import oracle as O
+            ip = indptr.astype(np.int32)
+            ey = O.parity_error(np.concatenate(ys), O.np_forward(ip, indices, values, data, sel, h))
+            ed = O.parity_error(np.concatenate(dxs), O.np_backward(ip, indices, values, grad, sel))
+            q.put((ey, ed, m.bounds))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("V,world,overlap", [(3, 4, True), (3, 4, False), (1, 2, True)])
+def test_partitioned_hip_engine_empty_ranks(V, world, overlap):
+    """More ranks than rows: some ranks own no row (an empty block on the HIP
+    engine, still taking part in every collective)."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_tiny_worker, args=(r, world, port, q, V, overlap))
+             for r in range(world)]
+    for p in procs:
+        p.start()
+    for p in procs:
+        p.join(timeout=300)
+    assert all(p.exitcode == 0 for p in procs), [p.exitcode for p in procs]
+    ey, ed, bounds = q.get(timeout=5)
+    assert bounds[-1] == V and any(bounds[i] == bounds[i + 1] for i in range(world))
+    assert ey <= 1e-4 and ed <= 1e-4, (ey, ed)
