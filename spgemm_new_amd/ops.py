@@ -947,6 +947,8 @@ def spgemm_forward(g: MaxKGraph, data, sel, dim_origin: int = 256, out=None, val
         _on_device(g, output=out)
     if g.num_rows == 0:
         return out   # an empty block (a rank of the row partition that owns no row)
+    if g.num_cols == 0:
+        return out if accumulate else out.zero_()   # no source nodes: Y = 0
     L = _lib.load()
     nbytes = L.maxk_forward_workspace_bytes(g.num_panels, dim_origin)
     ws = g._workspace(("fwd", dim_origin), nbytes)
@@ -1012,6 +1014,8 @@ def _forward_blocked(g: MaxKGraph, nb: int, data, sel, dim_origin: int, out, val
     partial outputs (cacheable gathers), then the last block, whose row flush
     adds the partials in block order (bitwise the sum maxk_rows_sum gives over
     all nb parts, one partial write + read and one pass fewer)."""
+    if g.num_edges == 0 or g.num_rows == 0:
+        return out.zero_()
     L = _lib.load()
     plan = g.blocked_plan(nb)
     vals = g._blocked_values(plan, values)
@@ -1141,6 +1145,8 @@ def spgemm_forward_records(g: MaxKGraph, records: torch.Tensor, k: int, dim_orig
         _on_device(g, output=out)
     if g.num_rows == 0:
         return out
+    if g.num_cols == 0:
+        return out if accumulate else out.zero_()
     L = _lib.load()
     nbytes = L.maxk_forward_workspace_bytes(g.num_panels, dim_origin)
     ws = g._workspace(("fwd", dim_origin), nbytes)
@@ -1173,6 +1179,8 @@ def spgemm_forward_multi(g: MaxKGraph, data, sel, values, dim_origin: int = 256,
         _on_device(g, output=out)
     if g.num_rows == 0:
         return out
+    if g.num_cols == 0:
+        return out.zero_()
     vals = values if g.num_edges > 0 else torch.zeros((1, R), device=g.device)
     L = _lib.load()
     if MULTI_BANK_ORDER and R % 4 == 0 and k % 8 == 0 and k <= 64:

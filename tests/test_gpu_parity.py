@@ -1081,3 +1081,55 @@ def test_gnna_sag_baseline(dev, dim):
     assert np.abs(got_w - ref_w).max() / max(1.0, np.abs(ref_w).max()) <= 1e-5
     parts = g._sag_parts.cpu().numpy().reshape(-1, 4)
     assert (parts[:, 2] <= max(1, e // v)).all() and parts[:, 2].sum() == e
+
+
+@pytest.mark.parametrize("V,C,deg", [(0, 5, 0), (5, 0, 0), (5, 5, 0), (1, 1, 1), (3, 700, 2)])
+@pytest.mark.parametrize("k", [8, 16, 32, 64])
+def test_degenerate_shapes(dev, oracle, V, C, deg, k):
+    """Empty graphs, rows without edges, zero source columns and one-edge graphs
+    through every forward form (two-array / packed, edge-selector, records,
+    fused multi-relation) and every backward algorithm that serves the shape:
+    right shapes, Y = 0 and dXs = 0 where nothing reaches them, the oracle's
+    values elsewhere (a row block of the partition may be any of these)."""
+    rng = np.random.default_rng(V * 1000 + C + k)
+    degs = np.minimum(np.full(V, deg, np.int64), C)
+    indptr = np.zeros(V + 1, np.int32)
+    indptr[1:] = np.cumsum(degs)
+    idx = (np.concatenate([np.sort(rng.choice(C, int(d), replace=False)) for d in degs])
+           .astype(np.int32) if degs.sum() else np.zeros(0, np.int32))
+    vals = rng.random(len(idx)).astype(np.float32)
+    h = 256
+    g = S.MaxKGraph(T(indptr, dev), T(idx, dev), T(vals, dev), num_cols=C)
+    x = rng.random((C, h)).astype(np.float32)
+    grad = rng.random((V, h)).astype(np.float32)
+    if C > 0:
+        data, sel = S.topk_cbsr(T(x, dev), k)
+    else:
+        data = torch.zeros((0, k), device=dev)
+        sel = torch.zeros((0, k), dtype=torch.uint8, device=dev)
+    d_np, s_np = data.cpu().numpy(), sel.cpu().numpy()
+    ref = oracle.np_forward(indptr, idx, vals, d_np, s_np, h) if V else np.zeros((0, h))
+    ref_b = oracle.np_backward(indptr, idx, vals, grad, s_np) if C else np.zeros((0, k))
+    chk = lambda got, want: oracle.parity_error(got.cpu().numpy(), want) <= TOL  # noqa: E731
+    assert chk(g.forward(data, sel, h, out=torch.full((V, h), float("nan"), device=dev)), ref)
+    assert chk(S.spgemm_forward(g, data, sel, h, edge_sel=True), ref)
+    rec = (S.cbsr_gather_records(data, sel) if C > 0
+           else torch.zeros((0, 5 * k), dtype=torch.uint8, device=dev))
+    assert chk(g.forward_records(rec, k, h, out=torch.full((V, h), float("nan"), device=dev)), ref)
+    v4 = rng.random((len(idx), 4)).astype(np.float32)
+    ym = g.forward_multi(data, sel, T(v4, dev), h)
+    assert tuple(ym.shape) == (4, V, h)
+    for q in range(4):
+        rq = oracle.np_forward(indptr, idx, v4[:, q].copy(), d_np, s_np, h) if V else np.zeros((0, h))
+        assert chk(ym[q], rq)
+    g4 = rng.random((4, V, h)).astype(np.float32)
+    rb4 = sum(oracle.np_backward(indptr, idx, v4[:, q].copy(), g4[q], s_np) for q in range(4)) \
+        if C else np.zeros((0, k))
+    assert chk(g.backward_multi(T(g4, dev), sel, T(v4, dev)), rb4)
+    algos = [_lib.MAXK_BWD_AUTO, _lib.MAXK_BWD_ATOMIC, _lib.MAXK_BWD_STAGED, _lib.MAXK_BWD_LOCAL,
+             _lib.MAXK_BWD_STAGED_EDGE, _lib.MAXK_BWD_EDGE_GATHER]
+    if k in (32, 64):
+        algos.append(_lib.MAXK_BWD_TILE)
+    for a in algos:
+        dx = g.backward(T(grad, dev), sel, out=torch.full((C, k), float("nan"), device=dev), algo=a)
+        assert chk(dx, ref_b), a
