@@ -97,3 +97,38 @@ def test_oracle_not_imported_by_product_package():
             if f.endswith(".py"):
                 src = open(os.path.join(dirpath, f)).read()
                 assert "oracle" not in re.findall(r"^\s*(?:from|import)\s+(\w+)", src, re.M), f
+
+
+_NULL_SWEEP = r"""
+import ctypes, sys
+sys.path.insert(0, sys.argv[1])
+from spgemm_new_amd import _lib
+L = ctypes.CDLL(_lib.LIB_PATH)
+for name, (res, args) in _lib.SIGNATURES.items():
+    if res is not ctypes.c_int or name in ("maxk_abi_version", "maxk_tile_record_words",
+                                            "maxk_tile_part_planes"):
+        continue
+    f = getattr(L, name)
+    f.restype, f.argtypes = res, args
+    for n in (1, 1 << 20):
+        vals = [n if a in (ctypes.c_int, ctypes.c_int64, ctypes.c_size_t) else
+                0.0 if a is ctypes.c_float else None for a in args]
+        print(name, n, f(*vals), flush=True)
+"""
+
+
+def test_null_buffers_rejected_before_any_launch():
+    """Every buffer-taking entry point, called with null pointers and non-zero
+    sizes (1 and 2^20 for every integer argument), returns a MAXK_E_* code from
+    its argument checks -- no crash, and no HIP call (which would launch on null
+    buffers on a GPU; here it would return a positive HIP error).  One child
+    process for the sweep, so a crash is reported with the entry point it hit."""
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    p = subprocess.run([__import__("sys").executable, "-c", _NULL_SWEEP, root],
+                       capture_output=True, text=True, timeout=300)
+    lines = p.stdout.strip().splitlines()
+    assert p.returncode == 0, (lines[-1:] if lines else "", p.stderr[-2000:])
+    assert len(lines) >= 60
+    for ln in lines:
+        name, n, rc = ln.split()
+        assert int(rc) < 0, f"{name} with null buffers and sizes {n} returned {rc}"
