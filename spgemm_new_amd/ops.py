@@ -174,6 +174,11 @@ class MaxKGraph:
     Parameters mirror the reference's graph tuple ``(indptr, indices, values)``
     (utils/models.py:67, 227); ``values`` defaults to ones (sum aggregation, as
     in training, utils/models.py:227).
+
+    Every call runs asynchronously on the current stream and reuses the graph's
+    cached workspaces (carry slots, staging rows, edge selectors, TILE partial
+    planes), so the calls on one graph must be ordered on one stream; work on
+    several streams at once needs one MaxKGraph per stream.
     """
 
     def __init__(self, indptr: torch.Tensor, indices: torch.Tensor,
