@@ -24,6 +24,8 @@ def choose_shape(num_rows: int, num_cols: int, cus: int = 256,
     splits = max(1, min(8, cus // groups, num_rows))
     # as many groups as the CUs left over allow: smaller groups, same sweep
     groups = max(groups, min(cus // splits, num_cols))
+    if groups > cus:   # whole rounds of one-range workgroups
+        groups = min(-(-groups // cus) * cus, num_cols)
     size = -(-num_cols // groups)
     groups = -(-num_cols // size)
     return groups, size, groups * splits

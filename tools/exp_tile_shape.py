@@ -21,7 +21,7 @@ world = 1
 if graph.count("/"):                      # e.g. reddit/8: rank 0's row block of world 8
     graph, world = graph.split("/")[0], int(graph.split("/")[1])
 shapes = [tuple(int(x) for x in s.split(",")) for s in sys.argv[3:]] or [None]
-K = 32
+K = int(os.environ.get("TILE_K", "32"))
 dev = torch.device("cuda:0")
 V, E = CONFIGS[graph]
 indptr, indices = synthetic_csr_gpu(V, E, device=dev)
