@@ -412,7 +412,9 @@ int maxk_sspmm_backward_tile(const void *headers, const int64_t *header_start,
  *  maxk_tile_plan_shape: (num_groups, group_size, num_workgroups) for num_cus
  *    CUs -- groups of <= 2048 (k = 32) / 1024 (k = 64) destinations and S <= 8
  *    equal source ranges per group (num_workgroups = num_groups * S, one piece
- *    each, S <= num_rows) so that about one workgroup runs per CU.  Any other
+ *    each, S <= num_rows) so that about one workgroup runs per CU; when the
+ *    groups outnumber the CUs (S = 1), their count is rounded up to whole
+ *    rounds of num_cus workgroups (smaller groups, no idle last round).  Any other
  *    num_workgroups <= num_groups * num_rows is valid (ranges straddling
  *    groups), measured slower on Reddit; more would leave empty workgroup
  *    ranges and is refused (MAXK_E_ARG) by the build and the backward.
