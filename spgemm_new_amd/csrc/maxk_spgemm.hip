@@ -267,9 +267,6 @@ __device__ __forceinline__ void fwd_edges_vec(int e0, int e1, const int32_t *__r
 #ifndef FWD_U
 #define FWD_U 8
 #endif
-#ifndef FWD_ABLATE
-#define FWD_ABLATE 0  // development timing ablations (results wrong): bits 1 / 2 / 4 below
-#endif
     constexpr int U = STEPS < FWD_U ? STEPS : FWD_U;  // gathers in flight per lane
     using D = typename VecT<VEC>::D;
     using SB = typename VecT<VEC>::S;
@@ -277,9 +274,6 @@ __device__ __forceinline__ void fwd_edges_vec(int e0, int e1, const int32_t *__r
     const int sub = lane % LPE;
     const int slot = lane / LPE;
     float *my_acc = acc + slot * kMaxDim;
-#if FWD_ABLATE & 1
-    float ablate_sink = 0.f;
-#endif
     for (int base = e0; base < e1; base += kWave) {
         const int n = (e1 - base) < kWave ? (e1 - base) : kWave;
         int my_c = 0;
@@ -299,12 +293,6 @@ __device__ __forceinline__ void fwd_edges_vec(int e0, int e1, const int32_t *__r
                 const int t = (s0 + u) * EPS + slot;
                 const int c = __shfl(my_c, t < kWave ? t : 0);
                 v[u] = __shfl(my_v, t < kWave ? t : 0);
-#if FWD_ABLATE & 4  // no gathers: lane-made data and distinct selectors
-                if (true) {
-                    d[u] = D{} + v[u];
-                    sb[u] = (SB)(0x03020100u * 0 + (uint32_t)(sub * VEC) * 0x01010101u + 0x03020100u);
-                } else
-#endif
                 if (t < n) {
                     if constexpr (RS == 0) {
                         const size_t off = (size_t)c * K + sub * VEC;
@@ -332,15 +320,7 @@ __device__ __forceinline__ void fwd_edges_vec(int e0, int e1, const int32_t *__r
 #pragma unroll
             for (int u = 0; u < U; ++u) {
                 const int t = (s0 + u) * EPS + slot;
-#if FWD_ABLATE & 1  // no LDS read-modify-write: the products summed in a register
-                if (t < n) {
-                    if constexpr (VEC == 4) ablate_sink += v[u] * (d[u].x + d[u].y + d[u].z + d[u].w) + (float)sb[u];
-                    else if constexpr (VEC == 2) ablate_sink += v[u] * (d[u].x + d[u].y) + (float)sb[u];
-                    else ablate_sink += v[u] * d[u] + (float)sb[u];
-                }
-#else
                 if (t < n) rmw_acc<VEC>(my_acc, sb[u], v[u], d[u]);
-#endif
                 if constexpr (ESEL) {
                     // one dword store per 4 selector bytes: neighbouring lanes of the
                     // edge hand theirs over (byte / short stores ran at ~1 TB/s)
@@ -371,9 +351,6 @@ __device__ __forceinline__ void fwd_edges_vec(int e0, int e1, const int32_t *__r
             }
         }
     }
-#if FWD_ABLATE & 1
-    my_acc[lane] += ablate_sink;   // keeps the sums live (one LDS op per call)
-#endif
 }
 
 
@@ -451,9 +428,6 @@ __device__ __forceinline__ void flush_row(float *acc, int copies, float *__restr
         for (int c4 = lane; c4 < (dim >> 2); c4 += kWave) {
             f4 a = reinterpret_cast<f4 *>(acc)[c4];
             reinterpret_cast<f4 *>(acc)[c4] = f4{0.f, 0.f, 0.f, 0.f};
-#if FWD_ABLATE & 2  // timing ablation: copy 0 only (the other copies neither summed nor zeroed)
-            copies = 1;
-#endif
             for (int cp = 1; cp < copies; ++cp) {
                 f4 *q = reinterpret_cast<f4 *>(acc + cp * kMaxDim) + c4;
                 a += *q;
@@ -1763,9 +1737,6 @@ __global__ __launch_bounds__(kBlock) void bwd_warp4_kernel(
 #ifndef LOCAL_U
 #define LOCAL_U 8
 #endif
-#ifndef LOCAL_ABLATE
-#define LOCAL_ABLATE 0
-#endif
 #ifndef LOCAL_R
 #define LOCAL_R 16  // edge records per SGPR round (k = 32, 64)
 #endif
@@ -1849,11 +1820,7 @@ __device__ __forceinline__ void local_issue(const int32_t *__restrict__ rec_rc,
     // selector bytes for all groups, then all gathers back to back
 #pragma unroll
     for (int u = 0; u < NG; ++u) {
-#if LOCAL_ABLATE & 2  // development ablation: computed column instead of the LDS selector
-        col[u] = (uint32_t)((l * 8 + rd.ai[u]) & 255);
-#else
         col[u] = sl[rd.ai[u]];
-#endif
     }
 #pragma unroll
     for (int u = 0; u < NG; ++u) rd.gv[u] = *g_at<WIDE>(grad, ro[u], col[u]);
@@ -1864,13 +1831,6 @@ __device__ __forceinline__ void local_commit(const LocalRound<K> &rd, float *acc
 {
     constexpr int EPS = kWave / K;
     constexpr int NG = LocalRound<K>::NG;
-#if LOCAL_ABLATE & 1  // development ablation: no LDS update (sum kept in a register)
-    float t = 0.f;
-#pragma unroll
-    for (int u = 0; u < NG; ++u) t = fmaf(rd.vv[u], rd.gv[u], t);
-    if (t == 12345.f) acc[rd.ai[0]] = t;
-    return;
-#endif
 #pragma unroll
     for (int u = 0; u < NG; ++u) {
         if (!((rd.clash >> u) & 1u)) {
@@ -3117,9 +3077,6 @@ __global__ __launch_bounds__(kTileWaves * kWave) void bwd_tile_kernel(const Tile
     // measured no better): Reddit k=32 2.81 -> 2.78 ms
 #define TILE_KPF 2
 #endif
-#ifndef TILE_ABLATE
-#define TILE_ABLATE 0  // development timing ablations (results wrong): bits 1 / 2 / 4 / 8 below
-#endif
         // the window must stay inside the record stream's padding: 512 records =
         // 1024 dwords after the last wave's stream (kTileRecPad in maxk_plan.hip)
         static_assert(TILE_PF_AHEAD + 4 * kWave <= kTileRecWords * 512,
@@ -3180,12 +3137,8 @@ __global__ __launch_bounds__(kTileWaves * kWave) void bwd_tile_kernel(const Tile
                              : "=&s"(pa), "=&s"(pb) : "s"(rb), "s"(ro), "s"(ro + 64) : "memory");
             // this wave's DMA of chunk c and header of chunk c landed; after the
             // barrier everyone's have, and chunk c-1's buffer is free
-#if TILE_ABLATE & 1  // timing ablation (wrong results): no chunk barrier
-            asm volatile("s_waitcnt vmcnt(%2)" : "+v"(h), "+v"(pf) : "n"(kTileVmcnt) : "memory");
-#else
             asm volatile("s_waitcnt vmcnt(%2)\n\ts_barrier" : "+v"(h), "+v"(pf) : "n"(kTileVmcnt)
                          : "memory");
-#endif
             const uint32_t cnt = (uint32_t)__builtin_amdgcn_readfirstlane(h.x);
             // (every step must issue exactly 3 DMA + 1 header load + 1 prefetch: the
             // counted vmcnt above relies on it.  A step that issues fewer lets the wave
@@ -3200,10 +3153,6 @@ __global__ __launch_bounds__(kTileWaves * kWave) void bwd_tile_kernel(const Tile
             prefetch();
             const uint32_t g0n = (cnt & 0xffffu) >> 2, gn = g0n + (cnt >> 18);
             uint32_t n = 0u - gn, m = 0u - g0n;
-#if TILE_ABLATE & 2  // timing ablation: no record processing
-            n = 0u;
-            m = 0u;
-#endif
             // the record groups must have landed before anything reads (or copies)
             // their SGPRs -- also when this chunk has no records: a skipped wait let
             // the next step's s_loads into the same SGPRs race with these (SMEM
@@ -3229,13 +3178,7 @@ __global__ __launch_bounds__(kTileWaves * kWave) void bwd_tile_kernel(const Tile
                 gb[i] = pb[i];
             }
             tile_groups2(ga, n, m, lo, hi, selv, acc0, acc1);
-#if TILE_ABLATE & 8  // timing ablation: the first two record groups only
-            n = 0u;
-#endif
             tile_groups2(gb, n, m, lo, hi, selv, acc0, acc1);
-#if TILE_ABLATE & 4  // timing ablation: the four record groups loaded before the barrier only
-            n = 0u;
-#endif
             tile_group_loop(rb, ro + 128, n, m, lo, hi, selv, acc0, acc1);
             ro += 32 * gn;
         };

@@ -77,9 +77,13 @@ ESEL_AUTO = os.environ.get("MAXK_ESEL", "1") != "0"
 # STAGED_EDGE 3.88 / 1.48 fwd + bwd; products N = 1, 78 MB: STAGED_EDGE)
 ESEL_MIN_SEL_BYTES = int(os.environ.get("MAXK_ESEL_MIN_SEL_BYTES", 64 << 20))
 # AUTO backward: "measure" (time the candidates once per graph and shape; the fastest
-# is kept) or "fixed" (a rule of the shape alone, no timing: the same algorithm -- and
-# so the same fp32 summation order -- on every run and machine)
+# is kept) or "fixed" (a rule of the shape alone, no timing: the same algorithm on every
+# run and machine, and so the same fp32 summation order on every run of one machine;
+# TILE's source-range count follows the device's CU count, so across machines with
+# different CU counts TILE's partial sums may group differently)
 AUTO_MODE = os.environ.get("MAXK_AUTO", "measure")
+# MAXK_AUTO=fixed: the CU count its TILE rank-block rule is stated in (MI355X)
+FIXED_RULE_CUS = 256
 # edge-selector buffers kept per graph (one per live selector tensor: a forward
 # per layer before the backwards)
 ESEL_CACHE = int(os.environ.get("MAXK_ESEL_CACHE", 4))
@@ -554,10 +558,12 @@ class MaxKGraph:
             # destinations that fit one TILE group per CU (a rank's own-column block at
             # products N=8: 306 K columns, TILE 0.455 vs STAGED 0.566 ms fwd+bwd measured,
             # profiles/r5_rank_products_n8_candidates.txt); BASELINE's N=1 shapes are
-            # unchanged (Reddit / proteins are long-row, products has 2.45 M columns)
+            # unchanged (Reddit / proteins are long-row, products has 2.45 M columns).
+            # The bound is MI355X's 256 CUs as a constant, not the device's count, so
+            # the fixed choice (and its summation order) is the same on every box
+            # 
             from . import tile
-            cus = torch.cuda.get_device_properties(self.device).multi_processor_count
-            if self.num_cols <= tile.max_group(k) * cus and self.tile_plan(k) is not None:
+            if self.num_cols <= tile.max_group(k) * FIXED_RULE_CUS and self.tile_plan(k) is not None:
                 return _lib.MAXK_BWD_TILE
         if ESEL_AUTO and h <= 256 and k == 8:
             return _lib.MAXK_BWD_EDGE_GATHER

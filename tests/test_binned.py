@@ -23,6 +23,12 @@ sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(
                                 "tools", "variants_lib"))
 
 TOL = 1e-4
+# the GPU tests need the ablation library, built only on request
+# (MAXK_BUILD_VARIANTS=1 or __graft_entry__.build_variants()); they skip without it
+_VLIB = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "tools",
+                     "variants_lib", "libmaxk_variants.so")
+needs_vlib = pytest.mark.skipif(not os.path.exists(_VLIB),
+                                reason="ablation library not built (MAXK_BUILD_VARIANTS=1)")
 
 
 def _hub_csr(v=600, hub_every=15, seed=3):
@@ -110,6 +116,7 @@ def _graph(dev, kind, num_cols=None):
 
 
 @pytest.mark.gpu
+@needs_vlib
 @pytest.mark.parametrize("kind", ["small", "hub", "rect"])
 def test_device_plan_equals_reference(dev, kind):
     import variants as V
@@ -125,6 +132,7 @@ def test_device_plan_equals_reference(dev, kind):
 
 
 @pytest.mark.gpu
+@needs_vlib
 @pytest.mark.parametrize("k", [8, 16, 32])
 @pytest.mark.parametrize("kind", ["small", "hub", "rect"])
 @pytest.mark.parametrize("h", [256, 100])
@@ -153,6 +161,7 @@ def test_binned_backward(dev, oracle, k, kind, h):
 
 
 @pytest.mark.gpu
+@needs_vlib
 def test_binned_values_per_call(dev, oracle):
     """Per-call edge values."""
     import variants as V
@@ -167,6 +176,7 @@ def test_binned_values_per_call(dev, oracle):
 
 
 @pytest.mark.gpu
+@needs_vlib
 def test_binned_plan_refused_for_heavy_padding(dev):
     """A destination with a huge in-degree needs a window per in-edge: the plan
     is dropped (too many padding slots) and BINNED raises."""

@@ -20,7 +20,11 @@ sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(
 import variants as V  # noqa: E402
 
 TOL = 1e-4
-pytestmark = pytest.mark.gpu
+# the ablation library is built only on request (MAXK_BUILD_VARIANTS=1 or
+# __graft_entry__.build_variants()); without it these tests skip
+pytestmark = [pytest.mark.gpu,
+              pytest.mark.skipif(not os.path.exists(V.LIB_PATH),
+                                 reason="ablation library not built (MAXK_BUILD_VARIANTS=1)")]
 
 
 def T(a, dev):

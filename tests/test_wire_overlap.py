@@ -1,0 +1,145 @@
+"""The row-partitioned step under REAL stream concurrency.
+
+gloo completes every collective before returning, so the async_op overlap
+paths of spgemm_new_amd/distributed.py (forward records / all-gather / rows,
+the backward's reverse exchange) never ran with a collective in flight.  Here
+all ranks of a world run as threads on cuda:0, each on its own stream, and every
+collective is delivered on a side stream behind a spin kernel that stands for
+the wire (tools/wire_model.ThreadFabric: RCCL's ordering -- after the queued
+work, wait() = an event wait on the current stream, the tensors recorded on the
+side stream).  Each case runs two steps with DIFFERENT inputs (the second reuses
+the exchange buffers the first filled) and checks:
+
+* bitwise equality with the same code under synchronous collectives (gloo's
+  semantics: the delivery done before the call returns);
+* every rank's Y / dXs rows against the fp64 oracle of the whole graph (1e-4);
+* every async handle was waited;
+* the negative control: the same run with handles whose wait() does nothing
+  produces wrong results -- so the delivery really lands after the consumers
+  would have read it, and a missing wait would be caught.
+"""
+import os
+import sys
+
+import numpy as np
+import pytest
+import torch
+
+from spgemm_new_amd.graphs import random_cbsr, small_csr
+
+sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))),
+                                "tools"))
+
+pytestmark = pytest.mark.gpu
+
+CASES = [dict(world=2, k=8, overlap=True, halo="records", R=1, records=True, seed=41),
+         dict(world=2, k=32, overlap=True, halo="allgather", R=1, records=True, seed=42),
+         dict(world=3, k=16, overlap=False, halo="records", R=1, records=True, seed=43),
+         dict(world=3, k=64, overlap=True, halo="records", R=1, records=True, seed=44),
+         dict(world=2, k=8, overlap=True, halo="records", R=1, records=False, seed=45),
+         dict(world=2, k=32, overlap=True, halo="records", R=4, records=True, seed=46),
+         dict(world=3, k=32, overlap=True, halo="allgather", R=1, records=True, seed=47)]
+
+
+def _problem(cfg):
+    rng = np.random.default_rng(cfg["seed"])
+    indptr, indices = small_csr(int(rng.integers(900, 1500)), seed=cfg["seed"])
+    v, k, R = len(indptr) - 1, cfg["k"], cfg["R"]
+    h = 256
+    shape = (len(indices),) if R == 1 else (len(indices), R)
+    values = rng.standard_normal(shape).astype(np.float32)
+    steps = []
+    for s in range(2):
+        data, sel = random_cbsr(v, k, h, seed=cfg["seed"] * 10 + s)
+        gshape = (v, h) if R == 1 else (R, v, h)
+        steps.append((data, sel, rng.standard_normal(gshape).astype(np.float32)))
+    return indptr, indices, values, h, steps
+
+
+def _run(cfg, prob, monkeypatch, **fabric_kw):
+    import spgemm_new_amd.distributed as D
+    import spgemm_new_amd.ops as ops
+    from wire_model import ThreadFabric, install
+    monkeypatch.setattr(ops, "AUTO_MODE", "fixed")   # no timing: the same algorithms every run
+    dev = torch.device("cuda:0")
+    indptr, indices, values, h, steps = prob
+    world, R = cfg["world"], cfg["R"]
+    fabric = ThreadFabric(world, dev, **fabric_kw)
+    restore = install(fabric, D)
+    tip, tix, tv = (torch.from_numpy(a).to(dev) for a in (indptr, indices, values))
+    torch.cuda.synchronize()
+
+    def rank_fn(r):
+        m = D.PartitionedMaxK(tip, tix, tv, r, world, dev, panel_cost=128,
+                              overlap=cfg["overlap"], halo_mode=cfg["halo"],
+                              records=cfg["records"])
+        r0, r1 = m.bounds[r], m.bounds[r + 1]
+        out = []
+        for data, sel, grad in steps:
+            d_l = m.local_rows(torch.from_numpy(data).to(dev))
+            s_l = m.local_rows(torch.from_numpy(sel).to(dev))
+            if R == 1:
+                y = m.forward(d_l, s_l, h)
+                dx = m.backward(m.local_rows(torch.from_numpy(grad).to(dev)), s_l)
+            else:
+                y = m.forward_multi(d_l, s_l, h)
+                dx = m.backward_multi(torch.from_numpy(grad[:, r0:r1]).contiguous().to(dev), s_l)
+            out.append((y.clone(), dx.clone()))      # ordered on this rank's stream
+        return [(y.cpu().numpy(), dx.cpu().numpy()) for y, dx in out], m.halo_mode, m.overlap
+
+    try:
+        res = fabric.run(rank_fn)
+    finally:
+        restore()
+    return res, fabric
+
+
+def _truth(prob, R, step):
+    from oracle import oracle as O
+    indptr, indices, values, h, steps = prob
+    data, sel, grad = steps[step]
+    if R == 1:
+        return (O.np_forward(indptr, indices, values, data, sel, h),
+                O.np_backward(indptr, indices, values, grad, sel))
+    yr = np.stack([O.np_forward(indptr, indices, values[:, j].copy(), data, sel, h)
+                   for j in range(R)])
+    dr = sum(O.np_backward(indptr, indices, values[:, j].copy(), grad[j], sel) for j in range(R))
+    return yr, dr
+
+
+def _errors(res, prob, R, step):
+    from oracle import oracle as O
+    yr, dr = _truth(prob, R, step)
+    ys = [r[0][step][0] for r in res]
+    dxs = [r[0][step][1] for r in res]
+    y = np.concatenate(ys, axis=0 if R == 1 else 1)
+    return O.parity_error(y, yr), O.parity_error(np.concatenate(dxs), dr)
+
+
+@pytest.mark.parametrize("cfg", CASES, ids=[
+    f"N{c['world']}-k{c['k']}-{'ov' if c['overlap'] else 'single'}-{c['halo']}-R{c['R']}"
+    f"{'' if c['records'] else '-rows'}" for c in CASES])
+def test_overlap_paths_under_concurrency(cfg, monkeypatch):
+    prob = _problem(cfg)
+    sync, _ = _run(cfg, prob, monkeypatch, fixed_us=0.0, sync=True)
+    conc, fab = _run(cfg, prob, monkeypatch, fixed_us=1500.0)
+    assert fab.waited and all(w.waited for w in fab.waited), "an async handle was never waited"
+    if cfg["halo"] == "allgather" and cfg["overlap"]:
+        assert all(r[1] == "allgather" for r in conc)
+    for step in range(2):
+        for r in range(cfg["world"]):
+            for a, b in zip(sync[r][0][step], conc[r][0][step]):
+                assert np.array_equal(a, b, equal_nan=True), (step, r)
+        ey, ed = _errors(conc, prob, cfg["R"], step)
+        assert ey <= 1e-4 and ed <= 1e-4, (step, ey, ed)
+
+
+@pytest.mark.parametrize("cfg", [CASES[0], CASES[1], CASES[2]], ids=["records", "allgather", "single"])
+def test_missing_wait_is_detected(cfg, monkeypatch):
+    """Negative control: the same concurrent run with wait() a no-op must be wrong
+    at the second step (its consumers read the first step's exchange buffers)."""
+    prob = _problem(cfg)
+    bad, _ = _run(cfg, prob, monkeypatch, fixed_us=3000.0, no_wait=True)
+    torch.cuda.synchronize()
+    ey, ed = _errors(bad, prob, cfg["R"], 1)
+    assert max(ey, ed) > 1e-3, (ey, ed)

@@ -39,23 +39,62 @@ class Loopback:
         self.req = torch.cat(reqs)
         self.calls = 0
         self.halo = None
+        self._bounds_t = torch.tensor(bounds, device=indices.device)
+
+    wire = None   # a wire_model.Wire: the delivery on a side stream behind a modeled wire
 
     def __call__(self, out, inp, out_split=None, in_split=None, async_op=False):
         self.calls += 1
         if self.calls == 1:                      # HaloPlan: request counts
             out.copy_(self.counts)
-        elif self.calls == 2:                    # HaloPlan: requested ids
+            return D._Done() if async_op else out
+        if self.calls == 2:                      # HaloPlan: requested ids
             out.copy_(self.req)
             self.halo = inp.clone()              # my halo ids, grouped by owner
             self.halo32 = self.halo.to(torch.int32)
-        elif out.dtype == torch.uint8 and out.shape[1] == 5 * self.k:   # halo CBSR rows
-            D_ops.cbsr_gather_records(self.data, self.sel, self.halo32, out=out)
+            return D._Done() if async_op else out
+        if out.dtype == torch.uint8 and out.shape[1] == 5 * self.k:   # halo CBSR rows
+            def deliver():
+                if out_split is not None and sum(out_split) != self.halo32.numel():
+                    # one round of a pipelined exchange: the rows of this round
+                    rows = self._round_rows(out_split)
+                    D_ops.cbsr_gather_records(self.data, self.sel, rows, out=out)
+                else:
+                    D_ops.cbsr_gather_records(self.data, self.sel, self.halo32, out=out)
         elif out.dtype == torch.uint8:           # halo selectors only
-            out.copy_(self.sel[self.halo])
+            def deliver():
+                out.copy_(self.sel[self.halo])
         else:                                    # reverse: partial sums from the peers
-            out.copy_(inp[: out.shape[0]] if inp.shape[0] >= out.shape[0] else
-                      torch.ones_like(out))
-        return D._Done() if async_op else out
+            def deliver():
+                out.copy_(inp[: out.shape[0]] if inp.shape[0] >= out.shape[0] else
+                          torch.ones_like(out))
+        if self.wire is None:
+            deliver()
+            return D._Done() if async_op else out
+        w = self.wire.issue(out.numel() * out.element_size(), deliver, (out, inp), async_op)
+        return w if async_op else out
+
+    def _round_rows(self, out_split):
+        """Global ids of the halo rows one round of a pipelined exchange carries:
+        from every owner q, the next out_split[q] of its halo nodes (in order)."""
+        if not hasattr(self, "_next"):
+            self._next = None
+        world = len(out_split)
+        if self._next is None or all(n == 0 for n in self._next_left):
+            owner_counts = torch.bincount(
+                torch.searchsorted(self._bounds_t, self.halo, right=True) - 1,
+                minlength=world).tolist()
+            starts = [0]
+            for c in owner_counts[:-1]:
+                starts.append(starts[-1] + c)
+            self._next, self._next_left = list(starts), list(owner_counts)
+        parts = []
+        for q in range(world):
+            n = out_split[q]
+            parts.append(self.halo32[self._next[q]:self._next[q] + n])
+            self._next[q] += n
+            self._next_left[q] -= n
+        return torch.cat(parts)
 
 
 import spgemm_new_amd.ops as D_ops  # noqa: E402
@@ -69,14 +108,24 @@ class GatherLoopback:
     def __init__(self, bounds, data, sel):
         self.bounds, self.data, self.sel = bounds, data, sel
 
+    wire = None
+
     def __call__(self, out, inp, async_op=False):
         world = len(self.bounds) - 1
         max_own = out.shape[0] // world
-        for q in range(world):
-            r0, r1 = self.bounds[q], self.bounds[q + 1]
-            rows = torch.arange(r0, r1, device=out.device, dtype=torch.int32)
-            D_ops.cbsr_gather_records(self.data, self.sel, rows, out=out[q * max_own:q * max_own + r1 - r0])
-        return D._Done() if async_op else out
+
+        def deliver():
+            for q in range(world):
+                r0, r1 = self.bounds[q], self.bounds[q + 1]
+                rows = torch.arange(r0, r1, device=out.device, dtype=torch.int32)
+                D_ops.cbsr_gather_records(self.data, self.sel, rows,
+                                          out=out[q * max_own:q * max_own + r1 - r0])
+        if self.wire is None:
+            deliver()
+            return D._Done() if async_op else out
+        nbytes = (world - 1) * max_own * out.shape[1]
+        w = self.wire.issue(nbytes, deliver, (out, inp), async_op)
+        return w if async_op else out
 
 
 def timed(fn, reps=20):
@@ -255,8 +304,68 @@ def breakdown(graph="products", k=32, world=8, rank=0):
         print(f"  {name:36s} {timed(fn, reps=10):.3f} ms", flush=True)
 
 
+def wire_table(graph="products", k=32, worlds=(4, 8), rates=(None, 0, 300, 500, 700),
+               reps=20, **pm_kw):
+    """Rank 0's whole step (forward + backward) with the exchanges delivered on a
+    side stream behind a modeled wire (tools/wire_model.Wire: bytes received /
+    rate + 10 us), so the overlap paths really overlap: rate None = the plain
+    loopback (delivery inline, no wire: the step before the wire), 0 = side
+    stream with no spin (the delivery copies alone), else GB/s per rank."""
+    sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+    from wire_model import Wire
+    dev = torch.device("cuda:0")
+    V, E = CONFIGS[graph]
+    h = 256
+    indptr, indices = synthetic_csr_gpu(V, E, device=dev)
+    gen = torch.Generator(device=dev)
+    gen.manual_seed(5)
+    values = torch.rand(E, generator=gen, device=dev)
+    X = torch.rand((V, h), generator=gen, device=dev)
+    G = torch.rand((V, h), generator=gen, device=dev)
+    data, sel = topk_cbsr(X, k)
+    D.PartitionedMaxK._max_over_ranks = lambda self, *xs: xs[0] if len(xs) == 1 else list(xs)
+    if isinstance(worlds, int):
+        worlds = (worlds,)
+    if isinstance(rates, int):
+        rates = (rates,)
+    for world in worlds:
+        bounds = D.row_partition(indptr, world)
+        lb = Loopback(indptr, indices, bounds, 0, data, sel)
+        gl = GatherLoopback(bounds, data, sel)
+        D.a2a, D.ag = lb, gl
+        m = D.PartitionedMaxK(indptr, indices, values, 0, world, dev, **pm_kw)
+        d_l, s_l, g_l = m.local_rows(data), m.local_rows(sel), m.local_rows(G)
+        hb = m.halo_bytes(k)
+        fwd_in = hb["allgather_fwd"] if m.halo_mode == "allgather" else hb["records_fwd"]
+        print(f"{graph} k={k} N={world} rank 0: own {m.plan.num_own} halo {m.plan.num_halo} "
+              f"mode {m.halo_mode} overlap {m.overlap} rounds {getattr(m, 'rounds', 1)} | wire "
+              f"bytes in {fwd_in / 1e6:.0f} MB fwd, {hb['reverse_bwd'] / 1e6:.0f} MB bwd", flush=True)
+        for rate in rates:
+            w = None if rate is None else Wire(dev, rate_GBs=rate if rate else None)
+            lb.wire = gl.wire = w
+            tf = timed(lambda: m.forward(d_l, s_l, h), reps=reps)
+            tb = timed(lambda: m.backward(g_l, s_l), reps=reps)
+            ts = timed(lambda: (m.forward(d_l, s_l, h), m.backward(g_l, s_l)), reps=reps)
+            wire_ms = "" if rate in (None, 0) else \
+                f" | modeled wire fwd {(fwd_in / (rate * 1e6)) + 0.01:.3f} bwd " \
+                f"{hb['reverse_bwd'] / (rate * 1e6) + 0.01:.3f} ms"
+            label = "inline (no wire)" if rate is None else "side stream, no spin" if rate == 0 \
+                else f"{rate} GB/s"
+            print(f"  {label:22s} fwd {tf:.3f} bwd {tb:.3f} step {ts:.3f} ms{wire_ms}", flush=True)
+        lb.wire = gl.wire = None
+        del m, lb, gl, d_l, s_l, g_l
+        torch.cuda.empty_cache()
+
+
 if __name__ == "__main__":
-    if len(sys.argv) > 1 and sys.argv[1] == "breakdown":
+    if len(sys.argv) > 1 and sys.argv[1] == "wire":
+        kw = {}
+        for a in sys.argv[3:]:
+            key, val = a.split("=")
+            kw[key] = (tuple(int(x) for x in val.split(",")) if "," in val else
+                       int(val) if val.isdigit() else val)
+        wire_table(sys.argv[2] if len(sys.argv) > 2 else "products", **kw)
+    elif len(sys.argv) > 1 and sys.argv[1] == "breakdown":
         breakdown(*(sys.argv[2:3] or ["products"]))
     elif len(sys.argv) > 1 and sys.argv[1] == "single":
         for w in [int(x) for x in (sys.argv[3] if len(sys.argv) > 3 else "2,4,8").split(",")]:
