@@ -319,6 +319,39 @@ int maxk_sspmm_backward(int algo, const int32_t *sched, int64_t num_panels,
                         void *workspace, size_t workspace_bytes, void *stream);
 
 /* ---------------------------------------------------------------------------
+ * Backward SSpMM, APPEND algorithm (write-combined propagation blocking; no
+ * reference counterpart -- it replaces K2's atomicAdd push,
+ * spmm_maxk_backward.cu:80,101, and is NON-DETERMINISTIC like it: the sum order
+ * of a destination follows the arrival order of its products).
+ * Destinations are cut into num_bins bins of bin_size columns
+ * (maxk_append_bins: a bin's k-vectors fit 160 KB of LDS).  Phase 1 pushes every
+ * edge's k products, with its destination, to the region of (its destination's
+ * bin, the pushing workgroup's XCD group) through an atomic cursor; the regions
+ * of one bin are consecutive, so phase 2 streams each bin once into LDS and
+ * writes its dXs rows.  Plan (once per graph and k, maxk_append_plan_build):
+ * region_base int32[num_bins * 8 + 1], the first entry of every region in the
+ * panel schedule `sched` the backward will use -- the plan belongs to that graph
+ * and schedule.  num_rel: 1 (values fp32[E], cbsr_sel node selectors, or edge
+ * selectors uint8[E, k] in CSR order when edge_sel != 0), or 4 / 8 / 16 relations
+ * (values fp32[E, num_rel], grad fp32[num_rel, num_rows, dim_origin], node
+ * selectors; dim_k in {8, 16, 32, 64}: the backward of maxk_spgemm_forward_multi,
+ * relations summed per edge).  dim_k a power of two in [4, 256].  Workspace:
+ * maxk_backward_append_workspace_bytes.  Writes every element of dxs.
+ * ------------------------------------------------------------------------- */
+#define MAXK_BWD_APPEND 7
+int maxk_append_bins(int num_cols, int dim_k, int *num_bins, int *bin_size);
+int maxk_append_plan_build(const int32_t *sched, int64_t num_panels, const int32_t *indptr,
+                           const int32_t *indices, int num_rows, int num_cols, int dim_k,
+                           int32_t *region_base, int num_bins, int bin_size, void *stream);
+size_t maxk_backward_append_workspace_bytes(int64_t num_edges, int dim_k, int num_bins);
+int maxk_sspmm_backward_append(const int32_t *sched, int64_t num_panels, const int32_t *indptr,
+                               const int32_t *indices, const float *values, int num_rel,
+                               const float *grad, const uint8_t *cbsr_sel, int edge_sel,
+                               int num_rows, int num_cols, int64_t num_edges, int dim_origin,
+                               int dim_k, const int32_t *region_base, int num_bins, int bin_size,
+                               float *dxs, void *workspace, size_t workspace_bytes, void *stream);
+
+/* ---------------------------------------------------------------------------
  * Backward SSpMM, LOCAL algorithm: destination-owned dXs in LDS, no atomics
  * and no staging rows.  Needs a plan (built once per graph, ops.py
  * MaxKGraph.local_plan): destinations split into `num_waves` ranges

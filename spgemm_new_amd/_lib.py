@@ -30,10 +30,14 @@ MAXK_BWD_LOCAL = 3
 MAXK_BWD_TILE = 4
 MAXK_BWD_STAGED_EDGE = 5
 MAXK_BWD_EDGE_GATHER = 6
+MAXK_BWD_APPEND = 7     # write-combined propagation blocking (non-deterministic order)
+# Python level: APPEND reading the forward's edge selectors (the C entry's edge_sel = 1)
+MAXK_BWD_APPEND_EDGE = 8
 # backward_multi only (Python level; the C entry is maxk_sspmm_backward_multi with
 # MAXK_BWD_STAGED / MAXK_BWD_EDGE_GATHER): relations summed per edge in phase 1
 MAXK_BWD_MULTI_STAGED = 16
 MAXK_BWD_MULTI_EDGE_GATHER = 17
+MAXK_BWD_MULTI_APPEND = 18   # maxk_sspmm_backward_append with num_rel > 1
 MAXK_TOPK_ORDER_COLUMN = 0
 MAXK_TOPK_ORDER_VALUE = 1
 MAXK_TOPK_ORDER_LANE = 2
@@ -70,6 +74,11 @@ SIGNATURES = {
     "maxk_grad_interleave": (_I, [_P, _I, _I, _I, _P, _P]),
     "maxk_sspmm_backward_local_rel8": (_I, [_P, _I, _P, _I, _I, _P, _P, _P, _P, _I, _I, _I, _P,
                                             _P]),
+    "maxk_append_bins": (_I, [_I, _I, ctypes.POINTER(ctypes.c_int), ctypes.POINTER(ctypes.c_int)]),
+    "maxk_append_plan_build": (_I, [_P, _L, _P, _P, _I, _I, _I, _P, _I, _I, _P]),
+    "maxk_backward_append_workspace_bytes": (_S, [_L, _I, _I]),
+    "maxk_sspmm_backward_append": (_I, [_P, _L, _P, _P, _P, _I, _P, _P, _I, _I, _I, _L, _I, _I,
+                                        _P, _I, _I, _P, _P, _S, _P]),
     "maxk_sspmm_backward_multi": (_I, [_I, _P, _L, _P, _P, _P, _I, _P, _P, _I, _I, _L, _I, _I, _P,
                                        _P, _P, _L, _P, _P, _S, _P]),
     "maxk_sspmm_backward_tile": (_I, [_P, _P, _P, _P, _P, _I, _I, _I, _P, _P, _P, _I, _I, _I, _I,

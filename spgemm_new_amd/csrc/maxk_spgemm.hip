@@ -1261,7 +1261,35 @@ struct PRow {
 // wave scatters land in lines its XCD's L2 fills before writing them back --
 // plain stores, to be combined there (non-temporal ones would go out as
 // partial lines).
-constexpr int kPmCsc = 0, kPmEdge = 1, kPmBin = 2;
+constexpr int kPmCsc = 0, kPmEdge = 1, kPmBin = 2, kPmAppend = 3;
+
+// kPmAppend -- the APPEND backward (MAXK_BWD_APPEND): the edge's products are
+// appended, in arrival order, to its destination bin's region for this
+// workgroup's XCD group (blockIdx % 8): one returning atomic per edge on the
+// region's cursor (line-padded, initialised to the region's first entry by
+// append_reset_kernel) gives the entry index, then the destination (4 B) and the
+// K products go out as plain stores.  All appends of one XCD group to one bin
+// land at that region's single write frontier, so its L2 gathers them into whole
+// lines before they leave (the round-3 BINNED kept deterministic slots instead,
+// and with ~25 partly written lines per bin segment they left L2 half-written:
+// DESIGN §5).  The order in a region is the arrival order -- non-deterministic,
+// as the reference's atomicAdd K2 (spmm_maxk_backward.cu:80,101).
+struct AppendArgs {
+    uint32_t magic;             // floor(2^32 / bin_size): bin = c / bin_size via umulhi + fixup
+    int bin_size;
+    int32_t *cursor;            // [num_bins * 8 * kCursorStride]
+    int32_t *dst;               // [E] destination of each entry
+};
+constexpr int kCursorStride = 32;  // one 128-B line per cursor
+constexpr size_t kAppendLds = 160 * 1024;   // phase 2: a bin's rows in one workgroup's LDS
+constexpr int kAppendGroups = 8;   // XCD groups: blockIdx % 8
+
+__device__ __forceinline__ int append_bin(int c, const AppendArgs &ap)
+{
+    int q = (int)__umulhi((uint32_t)c, ap.magic);
+    if (c - q * ap.bin_size >= ap.bin_size) ++q;
+    return q;
+}
 
 template <int K, bool ESEL = false, int PM = kPmCsc>
 __device__ __forceinline__ void bwd_edges_stage_vec(int e0, int e1,
@@ -1269,9 +1297,11 @@ __device__ __forceinline__ void bwd_edges_stage_vec(int e0, int e1,
                                                     const float *__restrict__ val,
                                                     const int32_t *__restrict__ csc_pos,
                                                     const uint8_t *__restrict__ sel,
-                                                    const float *gs, float *__restrict__ P)
+                                                    const float *gs, float *__restrict__ P,
+                                                    const AppendArgs &ap = AppendArgs{})
 {
-    constexpr bool CSRP = PM == kPmEdge;
+    constexpr bool CSRP = PM == kPmEdge || PM == kPmAppend;
+    constexpr bool APP = PM == kPmAppend;
     constexpr int KP = PM == kPmCsc ? PRow<K>::KP : K;
     constexpr int LPE = KP / 4;
     constexpr int EPS = kWave / LPE;
@@ -1293,6 +1323,7 @@ __device__ __forceinline__ void bwd_edges_stage_vec(int e0, int e1,
         for (int s0 = 0; s0 < STEPS; s0 += U) {
             if (s0 * EPS >= n) break;
             uint32_t sb[U];
+            int cu[U], slot_at[U];
 #pragma unroll
             for (int u = 0; u < U; ++u) {
                 const int t = (s0 + u) * EPS + slot;
@@ -1300,11 +1331,19 @@ __device__ __forceinline__ void bwd_edges_stage_vec(int e0, int e1,
                 const size_t row = ESEL ? (size_t)(base + t) : (size_t)c;
                 sb[u] = t < n && sub * 4 < K
                             ? *reinterpret_cast<const uint32_t *>(sel + row * K + sub * 4) : 0u;
+                if constexpr (APP) {  // the entry's place: the U atomics in flight together
+                    cu[u] = c;
+                    slot_at[u] = 0;
+                    if (t < n && sub == 0)
+                        slot_at[u] = atomicAdd(ap.cursor + ((size_t)append_bin(c, ap) * kAppendGroups +
+                                                            (blockIdx.x & (kAppendGroups - 1))) *
+                                                               kCursorStride, 1);
+                }
             }
 #pragma unroll
             for (int u = 0; u < U; ++u) {
                 const int t = (s0 + u) * EPS + slot;
-                const int p = __shfl(my_p, t < kWave ? t : 0);
+                const int p = APP ? __shfl(slot_at[u], slot * LPE) : __shfl(my_p, t < kWave ? t : 0);
                 const float v = __shfl(my_v, t < kWave ? t : 0);
                 if (t < n) {
                     f4 o = f4{0.f, 0.f, 0.f, 0.f};
@@ -1318,9 +1357,11 @@ __device__ __forceinline__ void bwd_edges_stage_vec(int e0, int e1,
                     // products 7.85 -> 8.20 ms): the staging lines would evict selector lines
                     f4 *dst = reinterpret_cast<f4 *>(P + (size_t)p * KP + sub * 4);
 #ifndef MAXK_BIN_NT_STORE
-                    if constexpr (PM == kPmBin)
+                    if constexpr (PM == kPmBin || PM == kPmAppend) {
+                        // plain stores: combined into lines in L2 (see kPmAppend)
                         *dst = o;
-                    else
+                        if (APP && sub == 0) ap.dst[p] = cu[u];
+                    } else
 #endif
                         __builtin_nontemporal_store(o, dst);
                 }
@@ -1446,9 +1487,11 @@ __device__ __forceinline__ void bwd_multi_edges(int e0, int e1, const int32_t *_
                                                 const float *__restrict__ val,
                                                 const int32_t *__restrict__ csc_pos,
                                                 const uint8_t *__restrict__ sel, const char *gs,
-                                                float *__restrict__ P)
+                                                float *__restrict__ P,
+                                                const AppendArgs &ap = AppendArgs{})
 {
-    constexpr bool CSRP = PM == kPmEdge;
+    constexpr bool CSRP = PM == kPmEdge || PM == kPmAppend;
+    constexpr bool APP = PM == kPmAppend;
     constexpr int KP = PM == kPmCsc ? PRow<K>::KP : K;
     constexpr int LPE = KP / 4;
     constexpr int EPS = kWave / LPE;
@@ -1475,6 +1518,7 @@ __device__ __forceinline__ void bwd_multi_edges(int e0, int e1, const int32_t *_
         for (int s0 = 0; s0 < STEPS; s0 += U) {
             if (s0 * EPS >= n) break;
             uint32_t sb[U];
+            int cu[U], slot_at[U];
 #pragma unroll
             for (int u = 0; u < U; ++u) {
                 const int t = (s0 + u) * EPS + slot;
@@ -1482,11 +1526,19 @@ __device__ __forceinline__ void bwd_multi_edges(int e0, int e1, const int32_t *_
                 sb[u] = t < n && sub * 4 < K
                             ? *reinterpret_cast<const uint32_t *>(sel + (size_t)c * K + sub * 4)
                             : 0u;
+                if constexpr (APP) {
+                    cu[u] = c;
+                    slot_at[u] = 0;
+                    if (t < n && sub == 0)
+                        slot_at[u] = atomicAdd(ap.cursor + ((size_t)append_bin(c, ap) * kAppendGroups +
+                                                            (blockIdx.x & (kAppendGroups - 1))) *
+                                                               kCursorStride, 1);
+                }
             }
 #pragma unroll
             for (int u = 0; u < U; ++u) {
                 const int t = (s0 + u) * EPS + slot;
-                const int p = __shfl(my_p, t);
+                const int p = APP ? __shfl(slot_at[u], slot * LPE) : __shfl(my_p, t);
                 f4 v[NS];
 #pragma unroll
                 for (int s = 0; s < NS; ++s)
@@ -1510,8 +1562,13 @@ __device__ __forceinline__ void bwd_multi_edges(int e0, int e1, const int32_t *_
                             o[i] = acc;
                         }
                     }
-                    __builtin_nontemporal_store(
-                        o, reinterpret_cast<f4 *>(P + (size_t)p * KP + sub * 4));
+                    if constexpr (APP) {   // plain stores: combined into lines in L2
+                        *reinterpret_cast<f4 *>(P + (size_t)p * KP + sub * 4) = o;
+                        if (sub == 0) ap.dst[p] = cu[u];
+                    } else {
+                        __builtin_nontemporal_store(
+                            o, reinterpret_cast<f4 *>(P + (size_t)p * KP + sub * 4));
+                    }
                 }
             }
         }
@@ -1540,6 +1597,132 @@ __global__ __launch_bounds__(kBlock) void bwd_multi_stage_kernel(
         stage_rel_rows<R>(gs, grad, plane, r, dim);
         bwd_multi_edges<K, R, PM>(eb, ee, idx, val, csc_pos, sel, gs, P);
     }
+}
+
+// ---------------------------------------------------------------------------
+// APPEND backward (MAXK_BWD_APPEND): write-combined
+// propagation blocking.  Phase 1 is the STAGED push with the products appended
+// to destination bins (kPmAppend above); phase 2 streams each bin's entries
+// once and sums them into the bin's LDS rows with LDS float atomics, then
+// writes the bin's dXs rows whole.  Bin b holds destinations [b*bin_size,
+// (b+1)*bin_size), bin_size*K*4 <= 160 KB; its 8 regions (one per XCD group)
+// are consecutive, so a bin is one contiguous range of entries
+// [region_base[8b], region_base[8b+8]).  Per edge: 4 + 4K bytes out in phase 1
+// and back in phase 2, against STAGED's random 64-B+ row stores and the CSC
+// segmented sum.  Sum order: arrival order (non-deterministic).
+// ---------------------------------------------------------------------------
+template <int K, bool ESEL>
+__global__ __launch_bounds__(kBlock) void bwd_append_kernel(
+    const int2 *__restrict__ sched, int64_t num_panels, const int32_t *__restrict__ indptr,
+    const int32_t *__restrict__ idx, const float *__restrict__ val,
+    const float *__restrict__ grad, const uint8_t *__restrict__ sel, int num_rows, int dim,
+    float *__restrict__ P, AppendArgs ap)
+{
+    extern __shared__ __attribute__((aligned(16))) float lds[];
+    float *gs = lds + (threadIdx.x / kWave) * kMaxDim;
+    zero_lds(gs, kMaxDim);  // columns >= dim read as 0
+    const int64_t w = (int64_t)blockIdx.x * kWavesPerBlock + threadIdx.x / kWave;
+    if (w >= num_panels) return;
+    const int2 a = sched[w], b = sched[w + 1];
+    const int i0 = a.x, j0 = a.y, i1 = b.x, j1 = b.y;
+    const int rlast = i1 < num_rows ? i1 : num_rows - 1;
+    for (int r = i0; r <= rlast; ++r) {
+        const int rb = indptr[r], re = indptr[r + 1];
+        const int eb = rb > j0 ? rb : j0;
+        const int ee = re < j1 ? re : j1;
+        if (eb >= ee) continue;
+        stage_row(gs, grad + (size_t)r * dim, dim);
+        bwd_edges_stage_vec<K, ESEL, kPmAppend>(eb, ee, idx, val, nullptr, sel, gs, P, ap);
+    }
+}
+
+template <int K, int R>
+__global__ __launch_bounds__(kBlock) void bwd_multi_append_kernel(
+    const int2 *__restrict__ sched, int64_t num_panels, const int32_t *__restrict__ indptr,
+    const int32_t *__restrict__ idx, const float *__restrict__ val,
+    const float *__restrict__ grad, int64_t plane, const uint8_t *__restrict__ sel,
+    int num_rows, int dim, float *__restrict__ P, AppendArgs ap)
+{
+    extern __shared__ __attribute__((aligned(16))) float lds[];
+    char *gs = reinterpret_cast<char *>(lds + (threadIdx.x / kWave) * (kMaxDim * R));
+    const int64_t w = (int64_t)blockIdx.x * kWavesPerBlock + threadIdx.x / kWave;
+    if (w >= num_panels) return;
+    const int2 a = sched[w], b = sched[w + 1];
+    const int i0 = a.x, j0 = a.y, i1 = b.x, j1 = b.y;
+    const int rlast = i1 < num_rows ? i1 : num_rows - 1;
+    for (int r = i0; r <= rlast; ++r) {
+        const int rb = indptr[r], re = indptr[r + 1];
+        const int eb = rb > j0 ? rb : j0;
+        const int ee = re < j1 ? re : j1;
+        if (eb >= ee) continue;
+        stage_rel_rows<R>(gs, grad, plane, r, dim);
+        bwd_multi_edges<K, R, kPmAppend>(eb, ee, idx, val, nullptr, sel, gs, P, ap);
+    }
+}
+
+// cursor of region j := its first entry (phase 1's atomics then return entry indices)
+__global__ __launch_bounds__(kBlock) void append_reset_kernel(const int32_t *__restrict__ region_base,
+                                                              int n, int32_t *__restrict__ cursor)
+{
+    const int j = blockIdx.x * kBlock + threadIdx.x;
+    if (j < n) cursor[(size_t)j * kCursorStride] = region_base[j];
+}
+
+constexpr int kReduceThreads = 1024;
+
+// Phase 2: one workgroup per bin.  LPE = K/4 lanes per entry (16 B each), U
+// entries per lane in flight; each lane adds its 4 products to the bin's LDS rows
+// with ds_add_f32.  Entries of another bin (impossible for a consistent plan) are
+// skipped rather than corrupting LDS.
+template <int K>
+__global__ __launch_bounds__(kReduceThreads) void bwd_bin_reduce_kernel(
+    const int32_t *__restrict__ region_base, int bin_size, int num_cols,
+    const int32_t *__restrict__ dst, const float *__restrict__ P, float *__restrict__ dxs)
+{
+    extern __shared__ __attribute__((aligned(16))) float lds[];
+    constexpr int LPE = K / 4;
+    constexpr int EPW = kWave / LPE;   // entries per wave-instruction
+    constexpr int U = 8;
+    const int b = blockIdx.x;
+    const int c0 = b * bin_size;
+    const int nd = min(bin_size, num_cols - c0);
+    const int tid = threadIdx.x;
+    for (int i = tid; i < nd * LPE; i += kReduceThreads)
+        reinterpret_cast<f4 *>(lds)[i] = f4{0.f, 0.f, 0.f, 0.f};
+    __syncthreads();
+    const int64_t e0 = region_base[(size_t)b * kAppendGroups];
+    const int64_t e1 = region_base[(size_t)(b + 1) * kAppendGroups];
+    const int lane = lane_id();
+    const int sub = lane % LPE, slot = lane / LPE;
+    const int wv = tid / kWave;
+    constexpr int NW = kReduceThreads / kWave;
+    for (int64_t base = e0 + (int64_t)wv * EPW * U; base < e1; base += (int64_t)NW * EPW * U) {
+        int d[U];
+        f4 v[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const int64_t e = base + u * EPW + slot;
+            d[u] = -1;
+            if (e < e1) {
+                d[u] = __builtin_nontemporal_load(dst + e) - c0;
+                v[u] = __builtin_nontemporal_load(reinterpret_cast<const f4 *>(P + e * K) + sub);
+            }
+        }
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            if ((uint32_t)d[u] < (uint32_t)nd) {
+                float *a = lds + (size_t)d[u] * K + sub * 4;
+                atomicAdd(a + 0, v[u].x);
+                atomicAdd(a + 1, v[u].y);
+                atomicAdd(a + 2, v[u].z);
+                atomicAdd(a + 3, v[u].w);
+            }
+        }
+    }
+    __syncthreads();
+    f4 *out = reinterpret_cast<f4 *>(dxs + (size_t)c0 * K);
+    for (int i = tid; i < nd * LPE; i += kReduceThreads)
+        __builtin_nontemporal_store(reinterpret_cast<const f4 *>(lds)[i], out + i);
 }
 
 // GNNAdvisor-style SAG baseline (kernels/spmm_gnna.cu:60-140, the reference's
@@ -3659,6 +3842,89 @@ struct BwdSegsum {
     }
 };
 
+// APPEND backward (MAXK_BWD_APPEND): per-graph plan = the region base of every
+// (bin, XCD group); per call: cursors reset, phase 1 (single relation, node or
+// edge selectors; or R in {4, 8, 16} relations summed per edge), phase 2.
+// One panel per wave as everywhere; the XCD group of panel w is (w / 4) % 8.
+__global__ __launch_bounds__(kBlock) void append_count_kernel(
+    const int2 *__restrict__ sched, int64_t num_panels, const int32_t *__restrict__ idx,
+    AppendArgs ap, int32_t *__restrict__ counts)
+{
+    const int64_t w = (int64_t)blockIdx.x * kWavesPerBlock + threadIdx.x / kWave;
+    if (w >= num_panels) return;
+    const int j0 = sched[w].y, j1 = sched[w + 1].y;
+    const int grp = (int)(blockIdx.x & (kAppendGroups - 1));
+    for (int e = j0 + lane_id(); e < j1; e += kWave)
+        atomicAdd(counts + (size_t)append_bin(idx[e], ap) * kAppendGroups + grp, 1);
+}
+
+inline uint32_t append_magic(int bin_size)
+{
+    const uint64_t m = (1ull << 32) / (uint64_t)bin_size;
+    return m > 0xffffffffull ? 0xffffffffu : (uint32_t)m;
+}
+
+template <int K>
+struct BwdAppend {
+    template <int R>
+    static void launch_multi(unsigned blocks, const int2 *sc, int64_t P, const int32_t *indptr,
+                             const int32_t *idx, const float *val, const float *grad,
+                             int64_t plane, const uint8_t *sel, int V, int dim, float *Pbuf,
+                             const AppendArgs &ap, hipStream_t st)
+    {
+        const size_t lds = (size_t)kWavesPerBlock * kMaxDim * R * sizeof(float);
+        hipLaunchKernelGGL((bwd_multi_append_kernel<K, R>), dim3(blocks), dim3(kBlock), lds, st,
+                           sc, P, indptr, idx, val, grad, plane, sel, V, dim, Pbuf, ap);
+    }
+    static int run(const int32_t *sched, int64_t P, const int32_t *indptr, const int32_t *idx,
+                   const float *val, int num_rel, const float *grad, const uint8_t *sel,
+                   bool esel, int V, int C, int dim, const int32_t *region_base, int num_bins,
+                   int bin_size, float *dxs, float *Pbuf, int32_t *dst, int32_t *cursor,
+                   hipStream_t st)
+    {
+        if constexpr (K < 4) {
+            return MAXK_E_DIM;
+        } else {
+            const int ng = num_bins * kAppendGroups;
+            hipLaunchKernelGGL(append_reset_kernel, dim3((unsigned)ceil_div(ng, kBlock)),
+                               dim3(kBlock), 0, st, region_base, ng, cursor);
+            int rc = launch_status();
+            if (rc) return rc;
+            const AppendArgs ap{append_magic(bin_size), bin_size, cursor, dst};
+            const unsigned blocks = (unsigned)ceil_div(P, kWavesPerBlock);
+            const int2 *sc = reinterpret_cast<const int2 *>(sched);
+            if (num_rel == 1) {
+                if (esel)
+                    hipLaunchKernelGGL((bwd_append_kernel<K, true>), dim3(blocks), dim3(kBlock),
+                                       row_lds_bytes(), st, sc, P, indptr, idx, val, grad, sel, V,
+                                       dim, Pbuf, ap);
+                else
+                    hipLaunchKernelGGL((bwd_append_kernel<K, false>), dim3(blocks), dim3(kBlock),
+                                       row_lds_bytes(), st, sc, P, indptr, idx, val, grad, sel, V,
+                                       dim, Pbuf, ap);
+            } else {
+                if constexpr (K < 8 || K > 64) {
+                    return MAXK_E_DIM;
+                } else {
+                    const int64_t plane = (int64_t)V * dim;
+                    switch (num_rel) {
+                    case 4: launch_multi<4>(blocks, sc, P, indptr, idx, val, grad, plane, sel, V, dim, Pbuf, ap, st); break;
+                    case 8: launch_multi<8>(blocks, sc, P, indptr, idx, val, grad, plane, sel, V, dim, Pbuf, ap, st); break;
+                    case 16: launch_multi<16>(blocks, sc, P, indptr, idx, val, grad, plane, sel, V, dim, Pbuf, ap, st); break;
+                    default: return MAXK_E_ARG;
+                    }
+                }
+            }
+            rc = launch_status();
+            if (rc) return rc;
+            hipLaunchKernelGGL(bwd_bin_reduce_kernel<K>, dim3((unsigned)num_bins),
+                               dim3(kReduceThreads), (size_t)bin_size * K * sizeof(float), st,
+                               region_base, bin_size, C, dst, Pbuf, dxs);
+            return launch_status();
+        }
+    }
+};
+
 // Phase 1 of the multi-relation STAGED backward (R in {4, 8, 16}, k in {8, 16,
 // 32, 64}); phase 2 is BwdSegsum.
 template <int K>
@@ -4253,6 +4519,102 @@ int maxk_sspmm_backward_multi(int algo, const int32_t *sched, int64_t num_panels
                                              indices, values, grad, (int64_t)num_rows * dim_origin,
                                              cbsr_sel, csc_pos, num_rows, dim_origin, Pbuf, st);
         });
+}
+
+int maxk_append_bins(int num_cols, int dim_k, int *num_bins, int *bin_size)
+{
+    if (num_cols < 0 || !num_bins || !bin_size) return MAXK_E_ARG;
+    if (dim_k < 4 || dim_k > kMaxDim || (dim_k & (dim_k - 1))) return MAXK_E_DIM;
+    if (num_cols == 0) {
+        *num_bins = 0;
+        *bin_size = 1;
+        return MAXK_OK;
+    }
+    // the bin's rows fill at most 160 KB of LDS; beyond 256 bins, whole rounds of
+    // 256 (one workgroup per CU: products k=8 -> 512 bins of 4,784); below, at
+    // least ~64 destinations per bin and up to 256 bins for parallelism
+    const int cap = (int)(kAppendLds / (4 * dim_k));
+    int64_t nb = ceil_div((int64_t)num_cols, cap);
+    const int64_t par = ceil_div((int64_t)num_cols, 64) < 256 ? ceil_div((int64_t)num_cols, 64) : 256;
+    if (nb > 256) nb = ceil_div(nb, 256) * 256;
+    else if (nb < par) nb = par;
+    if (nb < 1) nb = 1;
+    const int64_t bs = ceil_div((int64_t)num_cols, nb);
+    *bin_size = (int)bs;
+    *num_bins = (int)ceil_div((int64_t)num_cols, bs);
+    return MAXK_OK;
+}
+
+int maxk_append_plan_build(const int32_t *sched, int64_t num_panels, const int32_t *indptr,
+                           const int32_t *indices, int num_rows, int num_cols, int dim_k,
+                           int32_t *region_base, int num_bins, int bin_size, void *stream)
+{
+    (void)indptr;
+    if (!sched || !region_base || num_panels < 1 || num_rows < 0 || num_cols < 0 ||
+        num_bins < 0 || bin_size < 1)
+        return MAXK_E_ARG;
+    int nb = 0, bs = 0;
+    const int rc0 = maxk_append_bins(num_cols, dim_k, &nb, &bs);
+    if (rc0) return rc0;
+    if (nb != num_bins || bs != bin_size) return MAXK_E_ARG;
+    hipStream_t st = as_stream(stream);
+    const int ng = num_bins * kAppendGroups;
+    const hipError_t me = hipMemsetAsync(region_base, 0, (size_t)(ng + 1) * sizeof(int32_t), st);
+    if (me != hipSuccess) return (int)me;
+    if (num_cols > 0 && num_rows > 0) {
+        if (!indices) return MAXK_E_ARG;
+        const AppendArgs ap{append_magic(bin_size), bin_size, nullptr, nullptr};
+        hipLaunchKernelGGL(append_count_kernel, dim3((unsigned)ceil_div(num_panels, kWavesPerBlock)),
+                           dim3(kBlock), 0, st, reinterpret_cast<const int2 *>(sched), num_panels,
+                           indices, ap, region_base);
+        const int rc = launch_status();
+        if (rc) return rc;
+    }
+    hipLaunchKernelGGL(exclusive_scan_1block, dim3(1), dim3(256), 0, st, region_base, ng,
+                       region_base + ng);
+    return launch_status();
+}
+
+size_t maxk_backward_append_workspace_bytes(int64_t num_edges, int dim_k, int num_bins)
+{
+    return align_up((size_t)num_edges * dim_k * sizeof(float), 256) +
+           align_up((size_t)num_edges * sizeof(int32_t), 256) +
+           align_up((size_t)num_bins * kAppendGroups * kCursorStride * sizeof(int32_t), 256);
+}
+
+int maxk_sspmm_backward_append(const int32_t *sched, int64_t num_panels, const int32_t *indptr,
+                               const int32_t *indices, const float *values, int num_rel,
+                               const float *grad, const uint8_t *cbsr_sel, int edge_sel,
+                               int num_rows, int num_cols, int64_t num_edges, int dim_origin,
+                               int dim_k, const int32_t *region_base, int num_bins, int bin_size,
+                               float *dxs, void *workspace, size_t workspace_bytes, void *stream)
+{
+    if (!sched || !indptr || !dxs || !region_base || num_panels < 1 || num_rows < 0 ||
+        num_cols < 0 || num_edges < 0 || num_edges > INT32_MAX)
+        return MAXK_E_ARG;
+    if (!dims_ok(dim_origin, dim_k) || dim_k < 4 || (dim_k & (dim_k - 1))) return MAXK_E_DIM;
+    if (num_rel != 1 && num_rel != 4 && num_rel != 8 && num_rel != 16) return MAXK_E_ARG;
+    if (num_rel > 1 && (edge_sel || dim_k < 8 || dim_k > 64 || (dim_origin & 3)))
+        return num_rel > 1 && edge_sel ? MAXK_E_ARG : MAXK_E_DIM;
+    int nb = 0, bs = 0;
+    const int rc0 = maxk_append_bins(num_cols, dim_k, &nb, &bs);
+    if (rc0) return rc0;
+    if (nb != num_bins || bs != bin_size) return MAXK_E_ARG;
+    hipStream_t st = as_stream(stream);
+    if (num_cols == 0) return MAXK_OK;
+    if (num_rows == 0 || num_edges == 0) return zero_floats(dxs, (size_t)num_cols * dim_k, st);
+    if (!indices || !values || !grad || !cbsr_sel) return MAXK_E_ARG;
+    if (!workspace || workspace_bytes < maxk_backward_append_workspace_bytes(num_edges, dim_k, num_bins))
+        return MAXK_E_WORKSPACE;
+    char *ws = static_cast<char *>(workspace);
+    float *Pbuf = reinterpret_cast<float *>(ws);
+    ws += align_up((size_t)num_edges * dim_k * sizeof(float), 256);
+    int32_t *dst = reinterpret_cast<int32_t *>(ws);
+    ws += align_up((size_t)num_edges * sizeof(int32_t), 256);
+    int32_t *cursor = reinterpret_cast<int32_t *>(ws);
+    return dispatch_k<BwdAppend>(dim_k, sched, num_panels, indptr, indices, values, num_rel, grad,
+                                 cbsr_sel, edge_sel != 0, num_rows, num_cols, dim_origin,
+                                 region_base, num_bins, bin_size, dxs, Pbuf, dst, cursor, st);
 }
 
 size_t maxk_backward_local_lds_bytes(int dmax, int dim_k)

@@ -182,7 +182,8 @@ class PartitionedMaxK:
     def __init__(self, indptr, indices, values, rank: int, world: int, device,
                  engine=None, row_cost: int = 16, overlap: bool | str = True, records: bool = True,
                  local_block: bool = False, overlap_backward: bool | None = None,
-                 bwd_algo: int | None = None, halo_mode: str = "auto", **engine_kw):
+                 bwd_algo: int | None = None, halo_mode: str = "auto", rounds: int = 1,
+                 **engine_kw):
         """indptr: the GLOBAL row pointer (V + 1 entries, cheap); indices /
         values: the global arrays, or with ``local_block=True`` only this rank's
         edges (rows [bounds[rank], bounds[rank + 1]) of ``row_partition(indptr,
@@ -202,12 +203,28 @@ class PartitionedMaxK:
         decided once with an all-reduce so every rank calls the same collective.
         The halo part computes on the same edges in the same order either way,
         so Y is bitwise the same; the backward's reverse exchange is the
-        all-to-all-v of halo partial sums in both modes."""
+        all-to-all-v of halo partial sums in both modes.
+
+        ``rounds`` (R >= 1): every exchange is split into R
+        all-to-all-v rounds, round j carrying the j-th slice of each peer's rows
+        (slices of equal count), and the halo columns are numbered round-major so
+        a round's rows are one contiguous range.  With the own | halo split, the
+        records forward issues all R rounds at once and runs the halo columns of
+        round j as soon as round j has arrived (one engine per round), and the
+        backward sends round j's partial sums as soon as its columns are done, so
+        the exchange pipelines with the halo compute instead of only with the
+        own part.  Backward: with an order-independent local algorithm (TILE with
+        one source range, LOCAL) dXs is bitwise the R = 1 result; the forward adds
+        each row's halo edges round by round (a different fp32 grouping, 1e-4)."""
         self.rank, self.world, self.device = rank, world, torch.device(device)
         self.bounds = row_partition(indptr, world, row_cost)
         self.plan = HaloPlan(indptr, indices, self.bounds, rank, world, self.device,
                              local_block=local_block)
         p = self.plan
+        if int(rounds) < 1:
+            raise RuntimeError("rounds must be >= 1")
+        self.rounds = int(rounds) if world > 1 else 1
+        self._round_tab = self._round_major(p, self.rounds)
         e0, e1 = p.edge_range
         if values.dim() not in (1, 2):
             raise RuntimeError("values must be fp32[E] or fp32[E, R]")
@@ -221,7 +238,10 @@ class PartitionedMaxK:
         self.send_rows = p.send_local.to(torch.int32).contiguous()
         # reverse exchange: the partial sums come back in send order; the owners'
         # add runs per own node over its (sorted) returns -- no atomics
-        order = torch.sort(p.send_local, stable=True).indices
+        # the peer of every send entry; a node's returns are added in peer order
+        # whatever the send order (rounds), so R does not change the sum
+        peer = self._send_peer
+        order = torch.sort(p.send_local * world + peer, stable=True).indices
         nodes, counts = torch.unique_consecutive(p.send_local[order], return_counts=True)
         seg_off = torch.zeros(nodes.numel() + 1, dtype=torch.int64, device=self.device)
         seg_off[1:] = torch.cumsum(counts, 0)
@@ -252,6 +272,7 @@ class PartitionedMaxK:
         elif not isinstance(overlap, bool):
             raise RuntimeError("overlap must be True, False or 'auto'")
         self.overlap = overlap and p.num_halo > 0
+        self.halo_rounds = []
         if self.overlap:
             li = p.local_indices.long()
             is_own = li < p.num_own
@@ -266,6 +287,11 @@ class PartitionedMaxK:
                             lv[mask].contiguous(), ncols, **engine_kw)
             self.local_own = part(is_own, 0, p.num_own)
             self.local_halo = part(~is_own, p.num_own, p.num_halo)
+            # one engine per round over its contiguous range of halo columns
+            if self.rounds > 1:
+                for (h0, h1, _, _, _, _) in self._round_tab:
+                    m = (li >= p.num_own + h0) & (li < p.num_own + h1)
+                    self.halo_rounds.append(part(m, p.num_own + h0, h1 - h0))
             hm = ~is_own
             ip_h = torch.zeros(p.num_own + 1, dtype=torch.int32, device=self.device)
             ip_h[1:] = torch.cumsum(torch.bincount(rows[hm], minlength=p.num_own), 0)
@@ -287,6 +313,71 @@ class PartitionedMaxK:
         self._halo_part = None   # its halo selectors: [num_halo, k] (view of records or rows)
 
     # --------------------------------------------------------------- helpers
+    def _round_major(self, p, R: int):
+        """Renumber the plan's halo nodes and send lists round-major (round j =
+        the j-th count slice of every peer's rows, peers in rank order) and
+        return the round table [(recv0, recv1, recv_counts, send0, send1,
+        send_counts)].  R = 1 leaves the plan as built (peer-major)."""
+        world, dev = self.world, self.device
+
+        def cuts(n):
+            return [n * j // R for j in range(R + 1)]
+
+        def order(counts):
+            off = [0]
+            for c in counts:
+                off.append(off[-1] + c)
+            perm, per_round = [], []
+            for j in range(R):
+                cnt = []
+                for q in range(world):
+                    c = cuts(counts[q])
+                    perm.append((off[q] + c[j], off[q] + c[j + 1]))
+                    cnt.append(c[j + 1] - c[j])
+                per_round.append(cnt)
+            return perm, per_round
+
+        rperm, rcnt = order(p.recv_counts)
+        sperm, scnt = order(p.send_counts)
+        peer_of = torch.repeat_interleave(torch.arange(world, device=dev),
+                                          torch.tensor(p.send_counts, device=dev),
+                                          output_size=sum(p.send_counts))
+        if R > 1:
+            ridx = torch.cat([torch.arange(a, b, device=dev) for a, b in rperm]) \
+                if p.num_halo else torch.zeros(0, dtype=torch.int64, device=dev)
+            sidx = torch.cat([torch.arange(a, b, device=dev) for a, b in sperm]) \
+                if sum(p.send_counts) else torch.zeros(0, dtype=torch.int64, device=dev)
+            inv = torch.empty_like(ridx)
+            inv[ridx] = torch.arange(ridx.numel(), device=dev)
+            p.halo_global = p.halo_global[ridx].contiguous()
+            li = p.local_indices.long()
+            hm = li >= p.num_own
+            li[hm] = p.num_own + inv[li[hm] - p.num_own]
+            p.local_indices = li.to(torch.int32).contiguous()
+            p.send_local = p.send_local[sidx].contiguous()
+            peer_of = peer_of[sidx].contiguous()
+        self._send_peer = peer_of
+        tab, r0, s0 = [], 0, 0
+        for j in range(R):
+            r1, s1 = r0 + sum(rcnt[j]), s0 + sum(scnt[j])
+            tab.append((r0, r1, rcnt[j], s0, s1, scnt[j]))
+            r0, s0 = r1, s1
+        return tab
+
+    def _a2a_rounds(self, out, inp, reverse: bool = False, async_op: bool = False):
+        """The halo exchange (forward: inp = send rows, out = halo rows; reverse:
+        inp = halo rows, out = send rows) as the plan's rounds, one
+        all-to-all-v each, in round order; returns the list of handles (async) or
+        out.  R = 1: the one all-to-all-v of the whole halo."""
+        works = []
+        for (r0, r1, rc, s0, s1, sc) in self._round_tab:
+            if reverse:
+                o, i, oc, ic = out[s0:s1], inp[r0:r1], sc, rc
+            else:
+                o, i, oc, ic = out[r0:r1], inp[s0:s1], rc, sc
+            works.append(a2a(o, i, oc, ic, async_op=async_op))
+        return works if async_op else out
+
     def _max_over_ranks(self, *xs: float) -> list[float] | float:
         """Element-wise MAX of the given floats over all ranks (one all-reduce;
         the values themselves at world 1)."""
@@ -362,10 +453,9 @@ class PartitionedMaxK:
 
     def _exchange(self, send_rows: torch.Tensor, width: int, dtype, reverse: bool = False):
         p = self.plan
-        sc, rc = (p.recv_counts, p.send_counts) if reverse else (p.send_counts, p.recv_counts)
-        out = torch.empty((sum(rc), width), dtype=dtype, device=self.device)
-        a2a(out, send_rows.contiguous(), rc, sc)
-        return out
+        n = sum(p.send_counts) if reverse else sum(p.recv_counts)
+        out = torch.empty((n, width), dtype=dtype, device=self.device)
+        return self._a2a_rounds(out, send_rows.contiguous(), reverse=reverse)
 
     def _use_records(self, k: int, eng) -> bool:
         return self.records and _records_ok(k) and hasattr(eng, "forward_records")
@@ -396,13 +486,13 @@ class PartitionedMaxK:
         k = data_own.shape[1]
         n = p.num_own + p.num_halo
         recv = self._buf(("recv", k), (p.num_halo, 5 * k), torch.uint8)
-        work = a2a(recv, self._pack(data_own, sel_own), p.recv_counts, p.send_counts,
-                   async_op=True)
+        works = self._a2a_rounds(recv, self._pack(data_own, sel_own), async_op=True)
         data = self._buf(("data_all", k), (n, k), torch.float32)
         sel = self._buf(("sel_all_fwd", k), (n, k), torch.uint8)
         data[: p.num_own] = data_own
         sel[: p.num_own] = sel_own
-        work.wait()
+        for w in works:
+            w.wait()
         hd = recv[:, : 4 * k]
         data[p.num_own:] = (hd if (5 * k) % 4 == 0 else hd.contiguous()).view(torch.float32)
         sel[p.num_own:] = recv[:, 4 * k:]
@@ -424,12 +514,19 @@ class PartitionedMaxK:
         if self._allgather_ok(k):
             return self._forward_allgather(data_own, sel_own, dim_origin)
         recv = self._buf(("recv", k), (p.num_halo, 5 * k), torch.uint8)
-        work = a2a(recv, self._pack(data_own, sel_own), p.recv_counts, p.send_counts,
-                   async_op=True)
+        works = self._a2a_rounds(recv, self._pack(data_own, sel_own), async_op=True)
         y = _train_fwd(self.local_own, data_own, sel_own, dim_origin)   # overlaps the exchange
-        work.wait()
-        # the halo block reads the received records in place and adds onto y
-        self.local_halo.forward_records(recv, k, dim_origin, out=y, accumulate=True)
+        if self.halo_rounds:
+            # round j's halo columns as soon as round j has arrived (the later rounds
+            # still on the wire)
+            for w, eng, (r0, r1, _, _, _, _) in zip(works, self.halo_rounds, self._round_tab):
+                w.wait()
+                eng.forward_records(recv[r0:r1], k, dim_origin, out=y, accumulate=True)
+        else:
+            for w in works:
+                w.wait()
+            # the halo block reads the received records in place and adds onto y
+            self.local_halo.forward_records(recv, k, dim_origin, out=y, accumulate=True)
         self._fwd_sel, self._halo_part = sel_own, recv[:, 4 * k:]
         return y
 
@@ -531,10 +628,10 @@ class PartitionedMaxK:
         p = self.plan
         k = data_own.shape[1]
         recv = torch.empty((p.num_halo, 5 * k), dtype=torch.uint8, device=self.device)
-        work = a2a(recv, self._pack(data_own, sel_own), p.recv_counts, p.send_counts,
-                   async_op=True)
+        works = self._a2a_rounds(recv, self._pack(data_own, sel_own), async_op=True)
         y = _train_fwd(self.local_own, data_own, sel_own, dim_origin)   # overlaps the exchange
-        work.wait()
+        for w in works:
+            w.wait()
         h_data, h_sel = self._unpack(recv, k)
         h_sel = h_sel.contiguous()
         self._fwd_sel, self._halo_part = sel_own, h_sel
@@ -588,7 +685,8 @@ class PartitionedMaxK:
                 back.data_ptr(), k, order.data_ptr(), seg_off.data_ptr(), nodes.data_ptr(),
                 nodes.numel(), own.data_ptr(), _lib.stream_ptr(own.device)), "maxk_segment_rows_add")
         elif nodes.numel() > 0:
-            own.index_add_(0, p.send_local, back)
+            # the same fixed order as the device path: per node, its returns in peer order
+            own.index_add_(0, p.send_local[order], back[order])
         return own
 
     def backward(self, grad_own: torch.Tensor, sel_own: torch.Tensor | None = None,
@@ -609,13 +707,22 @@ class PartitionedMaxK:
             return self._return_halo(self._local_bwd(self.local, grad_own, sel))
         p = self.plan
         k = sel.shape[1]
-        dh = self._local_bwd(self.local_halo, grad_own, sel[p.num_own:])
         back = self._buf(("back", k), (sum(p.send_counts), k), torch.float32)
-        work = a2a(back, dh, p.send_counts, p.recv_counts, async_op=True)
+        if self.halo_rounds:
+            # round j's partial sums travel while the later rounds' columns (and then
+            # the own columns) are computed
+            works = []
+            for eng, (r0, r1, rc, s0, s1, sc) in zip(self.halo_rounds, self._round_tab):
+                dh = self._local_bwd(eng, grad_own, sel[p.num_own + r0:p.num_own + r1])
+                works.append(a2a(back[s0:s1], dh, sc, rc, async_op=True))
+        else:
+            dh = self._local_bwd(self.local_halo, grad_own, sel[p.num_own:])
+            works = self._a2a_rounds(back, dh, reverse=True, async_op=True)
         # the own part: the forward's selector tensor itself when it is the last one
         own_sel = self._fwd_sel if last else sel[: p.num_own]
         own = self._local_bwd(self.local_own, grad_own, own_sel)   # overlaps the exchange
-        work.wait()
+        for w in works:
+            w.wait()
         return self._add_returns(back, own)
 
     def _local_bwd(self, eng, grad, sel):

@@ -22,6 +22,7 @@ ranges and bands) are built once per graph by the library's device builders
 """
 from __future__ import annotations
 
+import ctypes
 import os
 
 import torch
@@ -145,16 +146,23 @@ def _validate_csr(indptr: torch.Tensor, indices: torch.Tensor, num_cols: int) ->
         raise RuntimeError(f"indices out of range: every column must be in [0, {num_cols})")
 
 
-_ESEL_ALGOS = (_lib.MAXK_BWD_STAGED_EDGE, _lib.MAXK_BWD_EDGE_GATHER)
+_ESEL_ALGOS = (_lib.MAXK_BWD_STAGED_EDGE, _lib.MAXK_BWD_EDGE_GATHER, _lib.MAXK_BWD_APPEND_EDGE)
+# non-deterministic algorithms (the sum order follows the arrival order of the
+# products, as the reference's atomicAdd K2): never chosen under MAXK_DETERMINISTIC=1
+_NONDET_ALGOS = (_lib.MAXK_BWD_ATOMIC, _lib.MAXK_BWD_APPEND, _lib.MAXK_BWD_APPEND_EDGE)
 
 
 _ALGO_NAMES = {_lib.MAXK_BWD_ATOMIC: "atomic", _lib.MAXK_BWD_STAGED: "staged",
                _lib.MAXK_BWD_LOCAL: "local", _lib.MAXK_BWD_TILE: "tile",
-               _lib.MAXK_BWD_STAGED_EDGE: "staged_edge", _lib.MAXK_BWD_EDGE_GATHER: "edge_gather"}
+               _lib.MAXK_BWD_STAGED_EDGE: "staged_edge", _lib.MAXK_BWD_EDGE_GATHER: "edge_gather",
+               _lib.MAXK_BWD_APPEND: "append", _lib.MAXK_BWD_APPEND_EDGE: "append_edge"}
 
 
 def _edge_gather_ok(k: int) -> bool:
     return 4 <= k <= 256 and k & (k - 1) == 0
+
+
+_append_ok = _edge_gather_ok   # APPEND: k a power of two in [4, 256] as well
 
 
 def _min_ms(fn, reps: int | None = None) -> float:
@@ -248,6 +256,7 @@ class MaxKGraph:
         self._csc = None
         self._local = {}
         self._tile = {}
+        self._append = {}
         # TILE source ranges (None: enough to fill the CUs); 1 makes each
         # destination's sum one sequential FMA chain in source-row order, the same
         # bits whatever other columns the graph holds (tests of the row partition)
@@ -460,6 +469,23 @@ class MaxKGraph:
                                            dtype=torch.float32, device=self.device)
             self._tile[dim_k] = plan
         return self._tile[dim_k]
+
+    def append_plan(self, dim_k: int) -> dict:
+        """Plan of the APPEND backward (maxk_append_plan_build): the destination
+        bins and the first entry of every (bin, XCD group) region for this graph's
+        backward panel schedule.  Built once per k on the device."""
+        if dim_k not in self._append:
+            L = _lib.load()
+            nb, bs = ctypes.c_int(0), ctypes.c_int(0)
+            _lib.check(L.maxk_append_bins(self.num_cols, dim_k, ctypes.byref(nb), ctypes.byref(bs)),
+                       "maxk_append_bins")
+            base = torch.empty(nb.value * 8 + 1, dtype=torch.int32, device=self.device)
+            _lib.check(L.maxk_append_plan_build(
+                self.bwd_sched.data_ptr(), self.bwd_num_panels, self.indptr.data_ptr(),
+                self.indices.data_ptr(), self.num_rows, self.num_cols, dim_k, base.data_ptr(),
+                nb.value, bs.value, _stream(base)), "maxk_append_plan_build")
+            self._append[dim_k] = {"region_base": base, "num_bins": nb.value, "bin_size": bs.value}
+        return self._append[dim_k]
 
     def tile_values(self, plan, values: torch.Tensor) -> None:
         """Make the TILE records hold ``values`` (fp32[E]: the graph's own, changed
@@ -780,6 +806,11 @@ class MaxKGraph:
                     if best is None or t < best[0]:
                         best = (t, a)
                 algo = self._bwd_choice[key] = best[1]
+        if algo == _lib.MAXK_BWD_MULTI_APPEND:
+            if not staged_ok:
+                raise RuntimeError("multi-relation APPEND backward needs R in {4, 8, 16}, k in "
+                                   "{8, 16, 32, 64}, h % 4 == 0 and 16-B aligned grad/values")
+            return self._backward_multi_append(grad, cbsr_sel, values, out)
         if algo in (_lib.MAXK_BWD_MULTI_STAGED, _lib.MAXK_BWD_MULTI_EDGE_GATHER):
             if not staged_ok:
                 raise RuntimeError("multi-relation STAGED backward needs R in {4, 8, 16}, k in "
@@ -810,6 +841,24 @@ class MaxKGraph:
             csc_sched.data_ptr(), CP, csc_indptr.data_ptr(), ws.data_ptr(), ws.numel(),
             _stream(out)), "maxk_sspmm_backward_multi")
         self.last_bwd_algo = "multi_edge_gather" if edge_order else "multi_staged"
+        return out
+
+    def _backward_multi_append(self, grad, sel, values, out):
+        """The relations summed per edge in phase 1 as MULTI_STAGED, the per-edge
+        vectors appended to destination bins and reduced per bin in LDS
+        (maxk_sspmm_backward_append with num_rel = R; non-deterministic order)."""
+        L = _lib.load()
+        k, h, R = sel.shape[1], grad.shape[2], values.shape[1]
+        plan = self.append_plan(k)
+        ws = self._workspace(("bwd_append", k), L.maxk_backward_append_workspace_bytes(
+            self.num_edges, k, plan["num_bins"]))
+        _lib.check(L.maxk_sspmm_backward_append(
+            self.bwd_sched.data_ptr(), self.bwd_num_panels, self.indptr.data_ptr(),
+            self.indices.data_ptr(), values.data_ptr(), R, grad.data_ptr(), sel.data_ptr(), 0,
+            self.num_rows, self.num_cols, self.num_edges, h, k, plan["region_base"].data_ptr(),
+            plan["num_bins"], plan["bin_size"], out.data_ptr(), ws.data_ptr(), ws.numel(),
+            _stream(out)), "maxk_sspmm_backward_append")
+        self.last_bwd_algo = "multi_append"
         return out
 
     def _backward_composed(self, grad, cbsr_sel, values, out, algo):
@@ -1269,6 +1318,22 @@ def sspmm_backward(g: MaxKGraph, grad, sel, out=None, values=None, algo: int = _
             plan["edge_rc"].data_ptr(), ev.data_ptr(), grad.data_ptr(),
             sel.data_ptr(), g.num_rows, dim_origin, k, out.data_ptr(), _stream(out)),
             "maxk_sspmm_backward_local")
+        return out
+    if algo in (_lib.MAXK_BWD_APPEND, _lib.MAXK_BWD_APPEND_EDGE):
+        if not _append_ok(k):
+            raise RuntimeError("APPEND backward needs k a power of two in [4, 256]")
+        esel = algo == _lib.MAXK_BWD_APPEND_EDGE
+        sel_arg = g.make_edge_selectors(sel) if esel else sel
+        plan = g.append_plan(k)
+        ws = g._workspace(("bwd_append", k), L.maxk_backward_append_workspace_bytes(
+            g.num_edges, k, plan["num_bins"]))
+        g.last_bwd_algo = _ALGO_NAMES[algo]
+        _lib.check(L.maxk_sspmm_backward_append(
+            g.bwd_sched.data_ptr(), g.bwd_num_panels, g.indptr.data_ptr(), g.indices.data_ptr(),
+            values.data_ptr(), 1, grad.data_ptr(), sel_arg.data_ptr(), int(esel), g.num_rows,
+            g.num_cols, g.num_edges, dim_origin, k, plan["region_base"].data_ptr(),
+            plan["num_bins"], plan["bin_size"], out.data_ptr(), ws.data_ptr(), ws.numel(),
+            _stream(out)), "maxk_sspmm_backward_append")
         return out
     csc_pos = csc_indptr = csc_sched = None
     CP = 0

@@ -817,3 +817,70 @@ def test_partitioned_hip_engine_empty_ranks(V, world, overlap):
     ey, ed, bounds = q.get(timeout=5)
     assert bounds[-1] == V and any(bounds[i] == bounds[i + 1] for i in range(world))
     assert ey <= 1e-4 and ed <= 1e-4, (ey, ed)
+
+
+def _rounds_worker(rank, world, port, q, halo_mode, k):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from spgemm_new_amd.distributed import PartitionedMaxK
+        indptr, indices = small_csr(1100, seed=6)
+        v, h = len(indptr) - 1, 64
+        rng = np.random.default_rng(4)
+        values = rng.standard_normal(len(indices)).astype(np.float32)
+        data, sel = random_cbsr(v, k, h, seed=5)
+        grad = rng.standard_normal((v, h)).astype(np.float32)
+        res = {}
+        for R in (1, 2, 3):
+            m = PartitionedMaxK(torch.from_numpy(indptr), torch.from_numpy(indices),
+                                torch.from_numpy(values), rank, world, "cpu", engine=OracleEngine,
+                                overlap=True, halo_mode=halo_mode, rounds=R)
+            assert m.rounds == R and (R == 1 or len(m.halo_rounds) == R)
+            tab = m._round_tab
+            assert tab[0][0] == 0 and tab[-1][1] == m.plan.num_halo
+            assert tab[-1][4] == sum(m.plan.send_counts)
+            sel_l = m.local_rows(torch.from_numpy(sel))
+            y = m.forward(m.local_rows(torch.from_numpy(data)), sel_l, h)
+            dx = m.backward(m.local_rows(torch.from_numpy(grad)), sel_l)
+            # a selector tensor other than the forward's goes through the round exchange
+            dx2 = m.backward(m.local_rows(torch.from_numpy(grad)), sel_l.clone())
+            assert torch.equal(dx, dx2)
+            res[R] = (y.numpy(), dx.numpy(), m.halo_mode)
+        for R in (2, 3):
+            # backward: the same column sums, returns added in peer order -> bitwise
+            assert np.array_equal(res[R][1], res[1][1]), R
+            assert np.max(np.abs(res[R][0] - res[1][0]) / np.maximum(1, np.abs(res[1][0]))) <= 1e-5
+        ys, dxs = [None] * world, [None] * world
+        dist.all_gather_object(ys, res[3][0])
+        dist.all_gather_object(dxs, res[3][1])
+        if rank == 0:
+            from oracle import oracle as O
+            ey = O.parity_error(np.concatenate(ys), O.np_forward(indptr, indices, values, data, sel, h))
+            ed = O.parity_error(np.concatenate(dxs), O.np_backward(indptr, indices, values, grad, sel))
+            q.put((ey, ed, res[3][2]))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world,halo_mode,k", [(2, "records", 8), (3, "records", 16),
+                                               (3, "allgather", 8), (8, "records", 8),
+                                               (8, "allgather", 32)])
+def test_round_pipelined_exchange(world, halo_mode, k):
+    """rounds = 2 / 3: the halo numbered round-major, every
+    exchange in R all-to-all-v rounds, the records forward and the overlapped
+    backward one engine per round: dXs bitwise the rounds = 1 result, Y within
+    fp32 regrouping (1e-5), both against the fp64 oracle of the whole graph."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_rounds_worker, args=(r, world, port, q, halo_mode, k))
+             for r in range(world)]
+    for p in procs:
+        p.start()
+    for p in procs:
+        p.join(timeout=300)
+    assert all(p.exitcode == 0 for p in procs), [p.exitcode for p in procs]
+    ey, ed, mode = q.get(timeout=5)
+    assert mode == halo_mode
+    assert ey <= 1e-4 and ed <= 1e-4, (ey, ed)

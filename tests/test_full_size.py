@@ -63,7 +63,7 @@ def test_full_size_properties(dev, graph, k):
     del a, ref, xm
     # backward: adjoint identity, algorithms agree
     algos = [_lib.MAXK_BWD_STAGED, _lib.MAXK_BWD_ATOMIC, _lib.MAXK_BWD_STAGED_EDGE,
-             _lib.MAXK_BWD_EDGE_GATHER]
+             _lib.MAXK_BWD_EDGE_GATHER, _lib.MAXK_BWD_APPEND, _lib.MAXK_BWD_APPEND_EDGE]
     if g.local_plan(k) is not None:   # slow on products (78 source bands) but must be right
         algos.append(_lib.MAXK_BWD_LOCAL)
     tile_plan = g.tile_plan(k)
@@ -98,7 +98,8 @@ def test_full_size_properties(dev, graph, k):
             # source-row order with one fp32 FMA each (tools/exp_tile_local_bits.py)
             assert torch.equal(t, outs[_lib.MAXK_BWD_LOCAL])
     auto = g.backward(Gr, sel)
-    assert g.last_bwd_algo in {"staged", "atomic", "local", "tile", "staged_edge", "edge_gather"}
+    assert g.last_bwd_algo in {"staged", "atomic", "local", "tile", "staged_edge", "edge_gather",
+                               "append", "append_edge"}
     assert _rel(auto, ref) <= TOL
 
 

@@ -305,7 +305,7 @@ def breakdown(graph="products", k=32, world=8, rank=0):
 
 
 def wire_table(graph="products", k=32, worlds=(4, 8), rates=(None, 0, 300, 500, 700),
-               reps=20, **pm_kw):
+               reps=20, rounds=(1,), **pm_kw):
     """Rank 0's whole step (forward + backward) with the exchanges delivered on a
     side stream behind a modeled wire (tools/wire_model.Wire: bytes received /
     rate + 10 us), so the overlap paths really overlap: rate None = the plain
@@ -328,12 +328,15 @@ def wire_table(graph="products", k=32, worlds=(4, 8), rates=(None, 0, 300, 500, 
         worlds = (worlds,)
     if isinstance(rates, int):
         rates = (rates,)
-    for world in worlds:
+    rates = tuple(None if r == -1 else r for r in rates)   # -1 on the command line: inline
+    if isinstance(rounds, int):
+        rounds = (rounds,)
+    for world, R in [(w, r) for w in worlds for r in rounds]:
         bounds = D.row_partition(indptr, world)
         lb = Loopback(indptr, indices, bounds, 0, data, sel)
         gl = GatherLoopback(bounds, data, sel)
         D.a2a, D.ag = lb, gl
-        m = D.PartitionedMaxK(indptr, indices, values, 0, world, dev, **pm_kw)
+        m = D.PartitionedMaxK(indptr, indices, values, 0, world, dev, rounds=R, **pm_kw)
         d_l, s_l, g_l = m.local_rows(data), m.local_rows(sel), m.local_rows(G)
         hb = m.halo_bytes(k)
         fwd_in = hb["allgather_fwd"] if m.halo_mode == "allgather" else hb["records_fwd"]
