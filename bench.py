@@ -582,6 +582,15 @@ def config_sweep(args, dev, only=None):
                                    lambda: g.backward(G, sel, out=dx)], steps, warmup)
             algo = g.last_bwd_algo
             nb = g._fwd_blocks.get((k, h), 0)
+            # the non-deterministic APPEND backward, timed beside
+            # the deterministic choice (min of 3 after one call; AUTO never takes it)
+            from spgemm_new_amd.ops import _min_ms
+            dx_a = torch.empty_like(dx)
+            append_ms = round(_min_ms(lambda: g.backward(G, sel, out=dx_a,
+                                                         algo=_lib.MAXK_BWD_APPEND)), 4)
+            append_err = float(((dx_a - dx).abs() / dx.abs().clamp_min(1)).max())
+            del dx_a
+            g._append.clear()
             b = g.nbytes_fwd(k, h)
             torch.cuda.synchronize()
             dx_st = g.backward(G, sel, algo=_lib.MAXK_BWD_STAGED)
@@ -598,6 +607,8 @@ def config_sweep(args, dev, only=None):
                 "step_GBs": round(2 * b / (sum(st) / len(st) / 1e3) / 1e9, 1),
                 "bwd_algo": algo,
                 "bwd_candidates_ms": getattr(g, "bwd_candidates", {}).get((k, h, True)),
+                "append_bwd_ms_nondeterministic": append_ms,
+                "append_vs_timed_max_rel_diff": append_err,
                 "fwd_form": (f"column-blocked nb={nb}" if nb else
                                                "packed CBSR records" if k <= 16 else "plain"),
                 "bwd_check": chk,
@@ -666,6 +677,10 @@ def config_sweep(args, dev, only=None):
             cand_b[nm] = round(_min_ms(lambda: g.backward_multi(G, sel, vals, out=dx, algo=a)), 4)
         cand_b["composed"] = round(_min_ms(lambda: g._backward_composed(G, sel, vals, dx,
                                                                         _lib.MAXK_BWD_AUTO)), 4)
+        # the non-deterministic write-combined form, reported beside
+        # the deterministic choice; AUTO never takes it (measured slower)
+        cand_b["multi_append_nondeterministic"] = round(_min_ms(
+            lambda: g.backward_multi(G, sel, vals, out=dx, algo=_lib.MAXK_BWD_MULTI_APPEND)), 4)
         g.forward_multi(data, sel, vals, h, out=y)
         g.backward_multi(G, sel, vals, out=dx)
         b = E * (4 + 4 * R + 5 * k) + R * 4 * h * V

@@ -29,6 +29,7 @@ import warnings
 import torch
 import torch.distributed as dist
 
+from . import _lib
 from .ops import MaxKGraph
 
 
@@ -77,6 +78,11 @@ def ag(out: torch.Tensor, inp: torch.Tensor, async_op: bool = False):
 # benchmark's k = 32 (160 B per node), reach this many bytes
 OVERLAP_MIN_HALO_BYTES = 64 << 20
 OVERLAP_BYTES_PER_HALO_NODE = 160
+
+# rounds="auto": a two-round pipelined exchange when some rank's halo has at least
+# this many times its own nodes and its records reach ROUNDS_MIN_HALO_BYTES
+ROUNDS_MIN_HALO_RATIO = 4.0
+ROUNDS_MIN_HALO_BYTES = 256 << 20
 
 # all-gather the CBSR instead of the all-to-all-v of halo records when some
 # rank's halo covers more than this fraction of V ("when the halo
@@ -182,7 +188,8 @@ class PartitionedMaxK:
     def __init__(self, indptr, indices, values, rank: int, world: int, device,
                  engine=None, row_cost: int = 16, overlap: bool | str = True, records: bool = True,
                  local_block: bool = False, overlap_backward: bool | None = None,
-                 bwd_algo: int | None = None, halo_mode: str = "auto", rounds: int = 1,
+                 bwd_algo: int | None = None, halo_mode: str = "auto", rounds: int | str = "auto",
+                 pipeline_fwd: bool = True, own_bwd_algo: int | str | None = "auto",
                  **engine_kw):
         """indptr: the GLOBAL row pointer (V + 1 entries, cheap); indices /
         values: the global arrays, or with ``local_block=True`` only this rank's
@@ -215,15 +222,50 @@ class PartitionedMaxK:
         the exchange pipelines with the halo compute instead of only with the
         own part.  Backward: with an order-independent local algorithm (TILE with
         one source range, LOCAL) dXs is bitwise the R = 1 result; the forward adds
-        each row's halo edges round by round (a different fp32 grouping, 1e-4)."""
+        each row's halo edges round by round (a different fp32 grouping, 1e-4).
+        ``pipeline_fwd=False`` keeps the rounds in the exchange and the backward
+        but runs the forward's halo columns once, after the last round.
+
+        ``own_bwd_algo``: the own-column part's backward in the overlapped
+        backward, which runs while the reverse exchange is in flight.  A kernel
+        that holds every CU's registers (TILE: one 16-wave workgroup per CU)
+        leaves no room for the collective's kernel, so the two serialise
+        (modeled wire, products N = 8 rank step 3.76 -> 3.58 ms at
+        500 GB/s); "auto" (default) therefore takes STAGED where the part's own
+        choice would be TILE, a MAXK_BWD_* code pins it, None keeps the part's
+        choice (``bwd_algo``, when given, pins every part instead)."""
         self.rank, self.world, self.device = rank, world, torch.device(device)
         self.bounds = row_partition(indptr, world, row_cost)
         self.plan = HaloPlan(indptr, indices, self.bounds, rank, world, self.device,
                              local_block=local_block)
         p = self.plan
-        if int(rounds) < 1:
-            raise RuntimeError("rounds must be >= 1")
+        # overlap and rounds are decided together, collectively (one all-reduce MAX of
+        # the halo size and the halo / own ratio), so every rank splits the same way and
+        # calls the same number of collectives (ADVICE r3)
+        if overlap != "auto" and not isinstance(overlap, bool):
+            raise RuntimeError("overlap must be True, False or 'auto'")
+        if rounds != "auto" and (not isinstance(rounds, int) or rounds < 1):
+            raise RuntimeError("rounds must be an int >= 1 or 'auto'")
+        if overlap == "auto" or rounds == "auto":
+            hmax, ratio = self._max_over_ranks(float(p.num_halo),
+                                               p.num_halo / max(1, p.num_own))
+            if overlap == "auto":
+                # split only when the exchange is worth hiding: the split costs 0.15-0.4
+                # ms of compute per step on Reddit blocks (two engines, their own launches
+                # and partials: N=2/4/8 step 3.10/1.84/1.04 ms split vs 2.72/1.57/0.89
+                # single, tools/exp_rank_step.py) against 19-33 MB of halo records, a few
+                # tenths of that over 7 xGMI links; products' 200-340 MB are not
+                overlap = hmax * OVERLAP_BYTES_PER_HALO_NODE >= OVERLAP_MIN_HALO_BYTES
+            if rounds == "auto":
+                # two rounds when the halo dwarfs the own block (products N = 8: halo 7x
+                # own, 342 MB of records; modeled wire at 300 / 500 GB/s: step 4.43 ->
+                # 4.00 / 3.59 -> 3.39 ms; at N = 4, halo 3x own, two rounds measured
+                # slower at every rate: DESIGN §6)
+                rounds = 2 if (overlap and ratio >= ROUNDS_MIN_HALO_RATIO and
+                               hmax * OVERLAP_BYTES_PER_HALO_NODE >= ROUNDS_MIN_HALO_BYTES) else 1
         self.rounds = int(rounds) if world > 1 else 1
+        self.pipeline_fwd = bool(pipeline_fwd)
+        self.own_bwd_algo = own_bwd_algo
         self._round_tab = self._round_major(p, self.rounds)
         e0, e1 = p.edge_range
         if values.dim() not in (1, 2):
@@ -258,19 +300,6 @@ class PartitionedMaxK:
         # adds each row's own-column edges before its halo-column edges, a
         # different fp32 order than the single block's edge order.
         self.bwd_algo = bwd_algo
-        if overlap == "auto":
-            # split only when the exchange is worth hiding: the split costs 0.15-0.4 ms
-            # of compute per step on Reddit blocks (two engines, their own launches
-            # and partials: N=2/4/8 step 3.10/1.84/1.04 ms split vs 2.72/1.57/0.89
-            # single, tools/exp_rank_step.py) against 19-33 MB of halo records, a
-            # few tenths of that over 7 xGMI links; products' 200-340 MB are not.
-            # Decided on the LARGEST halo over the ranks (one all-reduce), so every
-            # rank takes the same decision (a per-rank choice let split
-            # and unsplit ranks call different collectives in all-gather mode)
-            overlap = self._max_over_ranks(float(p.num_halo)) * OVERLAP_BYTES_PER_HALO_NODE \
-                >= OVERLAP_MIN_HALO_BYTES
-        elif not isinstance(overlap, bool):
-            raise RuntimeError("overlap must be True, False or 'auto'")
         self.overlap = overlap and p.num_halo > 0
         self.halo_rounds = []
         if self.overlap:
@@ -402,6 +431,11 @@ class PartitionedMaxK:
             return "records" if mode == "auto" else mode
         if mode == "records":
             return mode
+        if mode == "auto" and self.rounds > 1:
+            # the pipelined forward runs on the records rounds (the same on every rank:
+            # rounds is decided collectively); products N = 8, modeled wire 500 GB/s:
+            # records in 2 rounds 3.39 ms vs all-gather 3.57 ms
+            return "records"
         p = self.plan
         V = self.bounds[-1]
         frac, unsplit = self._max_over_ranks(p.num_halo / max(1, V), 0.0 if self.overlap else 1.0)
@@ -516,7 +550,7 @@ class PartitionedMaxK:
         recv = self._buf(("recv", k), (p.num_halo, 5 * k), torch.uint8)
         works = self._a2a_rounds(recv, self._pack(data_own, sel_own), async_op=True)
         y = _train_fwd(self.local_own, data_own, sel_own, dim_origin)   # overlaps the exchange
-        if self.halo_rounds:
+        if self.halo_rounds and self.pipeline_fwd:
             # round j's halo columns as soon as round j has arrived (the later rounds
             # still on the wire)
             for w, eng, (r0, r1, _, _, _, _) in zip(works, self.halo_rounds, self._round_tab):
@@ -720,10 +754,26 @@ class PartitionedMaxK:
             works = self._a2a_rounds(back, dh, reverse=True, async_op=True)
         # the own part: the forward's selector tensor itself when it is the last one
         own_sel = self._fwd_sel if last else sel[: p.num_own]
-        own = self._local_bwd(self.local_own, grad_own, own_sel)   # overlaps the exchange
+        own = self._own_bwd(grad_own, own_sel)   # overlaps the exchange
         for w in works:
             w.wait()
         return self._add_returns(back, own)
+
+    def _own_bwd(self, grad, sel):
+        """The own-column part's backward while the reverse exchange is in flight
+        (own_bwd_algo: "auto" avoids the all-CU TILE kernel there)."""
+        eng, a = self.local_own, self.own_bwd_algo
+        if self.bwd_algo is not None or a is None:
+            return self._local_bwd(eng, grad, sel)
+        if a == "auto":
+            if not isinstance(eng, MaxKGraph):
+                return self._local_bwd(eng, grad, sel)
+            out = torch.empty((eng.num_cols, sel.shape[1]), dtype=torch.float32, device=self.device)
+            a = _lib.MAXK_BWD_AUTO
+            if eng.num_edges > 0 and eng.autotune_backward(grad, sel, out) == _lib.MAXK_BWD_TILE:
+                a = _lib.MAXK_BWD_STAGED
+            return eng.backward(grad, sel, out=out, algo=a)
+        return eng.backward(grad, sel, algo=a)
 
     def _local_bwd(self, eng, grad, sel):
         if self.bwd_algo is None:

@@ -85,6 +85,9 @@ ESEL_MIN_SEL_BYTES = int(os.environ.get("MAXK_ESEL_MIN_SEL_BYTES", 64 << 20))
 AUTO_MODE = os.environ.get("MAXK_AUTO", "measure")
 # MAXK_AUTO=fixed: the CU count its TILE rank-block rule is stated in (MI355X)
 FIXED_RULE_CUS = 256
+# MAXK_DETERMINISTIC=1: AUTO never takes an algorithm whose fp32 sum order follows
+# arrival order (ATOMIC; APPEND is never an AUTO candidate: measured slower)
+DETERMINISTIC = os.environ.get("MAXK_DETERMINISTIC", "0") == "1"
 # edge-selector buffers kept per graph (one per live selector tensor: a forward
 # per layer before the backwards)
 ESEL_CACHE = int(os.environ.get("MAXK_ESEL_CACHE", 4))
@@ -636,7 +639,7 @@ class MaxKGraph:
             if tile_ok and own and self._tile.get(k) is not None:
                 return _lib.MAXK_BWD_TILE
             return _lib.MAXK_BWD_STAGED
-        cands = [_lib.MAXK_BWD_STAGED, _lib.MAXK_BWD_ATOMIC]
+        cands = [_lib.MAXK_BWD_STAGED] + ([] if DETERMINISTIC else [_lib.MAXK_BWD_ATOMIC])
         if self.local_plan(k) is not None:
             cands.append(_lib.MAXK_BWD_LOCAL)
         if tile_ok and self.tile_plan(k) is not None:

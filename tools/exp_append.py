@@ -101,6 +101,11 @@ def proteins(reps, dev):
 
 
 def main():
+    if len(sys.argv) > 1 and sys.argv[1] == "one":   # one <graph> <k> <algo name> [reps]
+        code = {v: k_ for k_, v in NAMES.items()}[sys.argv[4]]
+        single(sys.argv[2], (int(sys.argv[3]),), (code,),
+               int(sys.argv[5]) if len(sys.argv) > 5 else 5, torch.device("cuda:0"))
+        return
     what = sys.argv[1] if len(sys.argv) > 1 else "all"
     reps = int(sys.argv[2]) if len(sys.argv) > 2 else 10
     dev = torch.device("cuda:0")

@@ -52,6 +52,10 @@ class Loopback:
             out.copy_(self.req)
             self.halo = inp.clone()              # my halo ids, grouped by owner
             self.halo32 = self.halo.to(torch.int32)
+            world = self._bounds_t.numel() - 1   # owner slices, once (no sync in a timed call)
+            self._owner_counts = torch.bincount(
+                torch.searchsorted(self._bounds_t, self.halo, right=True) - 1,
+                minlength=world).tolist()
             return D._Done() if async_op else out
         if out.dtype == torch.uint8 and out.shape[1] == 5 * self.k:   # halo CBSR rows
             def deliver():
@@ -81,9 +85,7 @@ class Loopback:
             self._next = None
         world = len(out_split)
         if self._next is None or all(n == 0 for n in self._next_left):
-            owner_counts = torch.bincount(
-                torch.searchsorted(self._bounds_t, self.halo, right=True) - 1,
-                minlength=world).tolist()
+            owner_counts = self._owner_counts
             starts = [0]
             for c in owner_counts[:-1]:
                 starts.append(starts[-1] + c)
@@ -292,6 +294,10 @@ def breakdown(graph="products", k=32, world=8, rank=0):
         "whole forward": lambda: m.forward(d_l, s_l, h),
         "whole backward": lambda: m.backward(g_l, s_l),
     }
+    if m.overlap:
+        hsel = m._block_sel(s_l)[p.num_own:].clone()
+        rows["own-column backward"] = lambda: m.local_own.backward(g_l, s_l)
+        rows["halo-column backward"] = lambda: m.local_halo.backward(g_l, hsel)
     dx = m.local.backward(g_l, m._block_sel(s_l))
     back = torch.empty((m.send_rows.numel(), k), device=dev)
     rows["reverse exchange (loopback)"] = lambda: lb(back, dx[p.num_own:])
@@ -299,7 +305,8 @@ def breakdown(graph="products", k=32, world=8, rank=0):
     rows["index_add"] = lambda: own.index_add_(0, p.send_local, back)
     rows["return (whole)"] = lambda: m._return_halo(dx)
     print(f"{graph} k={k} world={world} rank={rank}: own={p.num_own} halo={p.num_halo} "
-          f"bwd algo {m.local.last_bwd_algo}")
+          f"bwd algo {m.local.last_bwd_algo}; parts: own {getattr(m, 'local_own', None) and m.local_own.last_bwd_algo}"
+          f" halo {getattr(m, 'local_halo', None) and m.local_halo.last_bwd_algo}")
     for name, fn in rows.items():
         print(f"  {name:36s} {timed(fn, reps=10):.3f} ms", flush=True)
 
@@ -329,6 +336,10 @@ def wire_table(graph="products", k=32, worlds=(4, 8), rates=(None, 0, 300, 500, 
     if isinstance(rates, int):
         rates = (rates,)
     rates = tuple(None if r == -1 else r for r in rates)   # -1 on the command line: inline
+    pm_kw = {key: (None if v == "none" else v) for key, v in pm_kw.items()}
+    for key in ("overlap", "pipeline_fwd"):
+        if isinstance(pm_kw.get(key), int):
+            pm_kw[key] = bool(pm_kw[key])
     if isinstance(rounds, int):
         rounds = (rounds,)
     for world, R in [(w, r) for w in worlds for r in rounds]:
@@ -368,8 +379,9 @@ if __name__ == "__main__":
             kw[key] = (tuple(int(x) for x in val.split(",")) if "," in val else
                        int(val) if val.isdigit() else val)
         wire_table(sys.argv[2] if len(sys.argv) > 2 else "products", **kw)
-    elif len(sys.argv) > 1 and sys.argv[1] == "breakdown":
-        breakdown(*(sys.argv[2:3] or ["products"]))
+    elif len(sys.argv) > 1 and sys.argv[1] == "breakdown":   # breakdown [graph] [world]
+        breakdown(sys.argv[2] if len(sys.argv) > 2 else "products", 32,
+                  int(sys.argv[3]) if len(sys.argv) > 3 else 8)
     elif len(sys.argv) > 1 and sys.argv[1] == "single":
         for w in [int(x) for x in (sys.argv[3] if len(sys.argv) > 3 else "2,4,8").split(",")]:
             breakdown_single(sys.argv[2] if len(sys.argv) > 2 else "reddit", 32, w, 0)
