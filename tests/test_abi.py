@@ -123,12 +123,20 @@ def test_null_buffers_rejected_before_any_launch():
     its argument checks -- no crash, and no HIP call (which would launch on null
     buffers on a GPU; here it would return a positive HIP error).  One child
     process for the sweep, so a crash is reported with the entry point it hit."""
+    import ctypes
+
+    from spgemm_new_amd import _lib
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    # no device visible to the child (ADVICE r5): an entry point that missed a check
+    # then fails with a HIP error code instead of launching on null buffers
+    env = dict(os.environ, HIP_VISIBLE_DEVICES="", ROCR_VISIBLE_DEVICES="")
     p = subprocess.run([__import__("sys").executable, "-c", _NULL_SWEEP, root],
-                       capture_output=True, text=True, timeout=300)
+                       capture_output=True, text=True, timeout=300, env=env)
     lines = p.stdout.strip().splitlines()
     assert p.returncode == 0, (lines[-1:] if lines else "", p.stderr[-2000:])
-    assert len(lines) >= 60
+    swept = [n for n, (res, _) in _lib.SIGNATURES.items() if res is ctypes.c_int and n not in
+             ("maxk_abi_version", "maxk_tile_record_words", "maxk_tile_part_planes")]
+    assert len(lines) == 2 * len(swept), (len(lines), len(swept))
     for ln in lines:
         name, n, rc = ln.split()
         assert int(rc) < 0, f"{name} with null buffers and sizes {n} returned {rc}"
