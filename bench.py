@@ -822,8 +822,10 @@ def partitioned_configs(args, dev, world, rank, dist, kw):
             "own_nodes_rank0": p.num_own, "halo_nodes_rank0": p.num_halo,
             "halo_bytes_rank0": model.halo_bytes(k),
             "exchange_ms_max_over_ranks": {kk: round(float(v), 4) for kk, v in zip(names, t)},
+            "exchange_rounds": model.rounds,
             "local_bwd_algo_rank0": model.local.last_bwd_algo if not model.overlap else
-            {"own": model.local_own.last_bwd_algo, "halo": model.local_halo.last_bwd_algo},
+            {"own": model.local_own.last_bwd_algo,
+             "halo": (model.halo_rounds[0] if model.halo_rounds else model.local_halo).last_bwd_algo},
             "check": {"adjoint_rel_err": abs(lhs - rhs) / max(abs(lhs), 1e-30),
                       "what": "sum over ranks <Y_own, G_own> vs <X^_s own, dXs own> (fp64)"},
             "wall_s": round(time.time() - t0, 1)}
@@ -1227,7 +1229,9 @@ def main():
         result["exchange_ms_max_over_ranks"] = {kk: round(float(v), 4) for kk, v in zip(names, t)}
         result["exchange_bytes_rank0"] = {kk: v for kk, v in ex.items() if not kk.endswith("_ms")}
         result["local_bwd_algo_rank0"] = model.local.last_bwd_algo if not model.overlap else \
-            {"own": model.local_own.last_bwd_algo, "halo": model.local_halo.last_bwd_algo}
+            {"own": model.local_own.last_bwd_algo,
+             "halo": (model.halo_rounds[0] if model.halo_rounds else model.local_halo).last_bwd_algo}
+        result["exchange_rounds"] = model.rounds
         if dist and not args.no_configs and args.graph == "reddit":
             # configs 4 and 5 in the same launch (the driver's scaling runs are
             # `bench.py --gpus N`): the Reddit state is freed first

@@ -57,7 +57,7 @@ def _grad(R, r0, r1, dev):
     return torch.stack([synthetic_features(SEED_G + q, r0, r1, H, dev) for q in range(R)])
 
 
-def _worker(rank, world, port, graph, R, graphdir, outdir, q):
+def _worker(rank, world, port, graph, R, graphdir, outdir, q, rounds=1):
     import sys
     sys.path.insert(0, ROOT)
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
@@ -88,9 +88,11 @@ def _worker(rank, world, port, graph, R, graphdir, outdir, q):
         G = _grad(R, r0, r1, dev)
         tile = _lib.MAXK_BWD_TILE
         log("block generated")
-        kw = {} if R > 1 else {"bwd_algo": tile, "tile_splits": 1}
+        kw = {"rounds": rounds} if R > 1 else {"bwd_algo": tile, "tile_splits": 1,
+                                               "rounds": rounds}
         m = PartitionedMaxK(indptr, cols, vals, rank, world, dev, local_block=True, **kw)
-        log(f"partition built (halo {m.plan.num_halo}, mode {m.halo_mode})")
+        log(f"partition built (halo {m.plan.num_halo}, mode {m.halo_mode}, rounds {m.rounds})")
+        assert m.rounds == rounds
         if R == 1:
             y = m.forward(data, sel, H)
             dx = m.backward(G, sel)
@@ -163,15 +165,19 @@ def _rel_err(a, b):
 
 @pytest.mark.gpu
 @pytest.mark.timeout(900)   # up to 8 spawned ranks time-share one card: minutes on a busy box
-@pytest.mark.parametrize("graph,world,R", [("products", 2, 1), ("products", 4, 1),
-                                           ("products", 8, 1), ("proteins", 8, 8)])
-def test_partitioned_rows_match_single_gpu(graph, world, R, tmp_path, tmp_path_factory):
+@pytest.mark.parametrize("graph,world,R,rounds", [("products", 2, 1, 1), ("products", 4, 1, 1),
+                                                  ("products", 8, 1, 1), ("proteins", 8, 8, 1),
+                                                  ("products", 2, 1, 2)])
+def test_partitioned_rows_match_single_gpu(graph, world, R, rounds, tmp_path, tmp_path_factory):
+    """rounds = 1 pins the partition forms against one GPU (the default's two rounds
+    at products N = 8 would add per-round engines to 8 processes time-sharing one
+    card); rounds = 2 at N = 2 pins the round-pipelined exchange at full size."""
     y_ref, dx_ref, graphdir = _reference(graph, R, str(tmp_path_factory.mktemp(graph)))
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
     procs = [ctx.Process(target=_worker,
-                         args=(r, world, port, graph, R, graphdir, str(tmp_path), q))
+                         args=(r, world, port, graph, R, graphdir, str(tmp_path), q, rounds))
              for r in range(world)]
     # the children's OpenMP pools, and one hardware queue per rank: N processes time-share
     # the one card, and more queues than the scheduler maps at once stall every sync

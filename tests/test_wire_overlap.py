@@ -38,7 +38,13 @@ CASES = [dict(world=2, k=8, overlap=True, halo="records", R=1, records=True, see
          dict(world=3, k=64, overlap=True, halo="records", R=1, records=True, seed=44),
          dict(world=2, k=8, overlap=True, halo="records", R=1, records=False, seed=45),
          dict(world=2, k=32, overlap=True, halo="records", R=4, records=True, seed=46),
-         dict(world=3, k=32, overlap=True, halo="allgather", R=1, records=True, seed=47)]
+         dict(world=3, k=32, overlap=True, halo="allgather", R=1, records=True, seed=47),
+         # the round-pipelined exchange (round j's halo columns after round j's wait,
+         # round j's partial sums sent as soon as its columns are done)
+         dict(world=2, k=16, overlap=True, halo="records", R=1, records=True, seed=48, rounds=2),
+         dict(world=3, k=32, overlap=True, halo="records", R=1, records=True, seed=49, rounds=3),
+         dict(world=3, k=8, overlap=True, halo="allgather", R=1, records=True, seed=50, rounds=2),
+         dict(world=2, k=32, overlap=True, halo="records", R=4, records=True, seed=51, rounds=2)]
 
 
 def _problem(cfg):
@@ -72,7 +78,8 @@ def _run(cfg, prob, monkeypatch, **fabric_kw):
     def rank_fn(r):
         m = D.PartitionedMaxK(tip, tix, tv, r, world, dev, panel_cost=128,
                               overlap=cfg["overlap"], halo_mode=cfg["halo"],
-                              records=cfg["records"])
+                              records=cfg["records"], rounds=cfg.get("rounds", "auto"))
+        assert m.rounds == cfg.get("rounds", m.rounds)
         r0, r1 = m.bounds[r], m.bounds[r + 1]
         out = []
         for data, sel, grad in steps:
@@ -118,7 +125,8 @@ def _errors(res, prob, R, step):
 
 @pytest.mark.parametrize("cfg", CASES, ids=[
     f"N{c['world']}-k{c['k']}-{'ov' if c['overlap'] else 'single'}-{c['halo']}-R{c['R']}"
-    f"{'' if c['records'] else '-rows'}" for c in CASES])
+    f"{'' if c['records'] else '-rows'}{'-rounds%d' % c['rounds'] if 'rounds' in c else ''}"
+    for c in CASES])
 def test_overlap_paths_under_concurrency(cfg, monkeypatch):
     prob = _problem(cfg)
     sync, _ = _run(cfg, prob, monkeypatch, fixed_us=0.0, sync=True)
@@ -134,7 +142,8 @@ def test_overlap_paths_under_concurrency(cfg, monkeypatch):
         assert ey <= 1e-4 and ed <= 1e-4, (step, ey, ed)
 
 
-@pytest.mark.parametrize("cfg", [CASES[0], CASES[1], CASES[2]], ids=["records", "allgather", "single"])
+@pytest.mark.parametrize("cfg", [CASES[0], CASES[1], CASES[2], CASES[8]],
+                         ids=["records", "allgather", "single", "rounds3"])
 def test_missing_wait_is_detected(cfg, monkeypatch):
     """Negative control: the same concurrent run with wait() a no-op must be wrong
     at the second step (its consumers read the first step's exchange buffers)."""
