@@ -71,6 +71,7 @@ def _run(cfg, prob, monkeypatch, **fabric_kw):
     indptr, indices, values, h, steps = prob
     world, R = cfg["world"], cfg["R"]
     fabric = ThreadFabric(world, dev, **fabric_kw)
+    fabric.concurrent = fabric.streams_concurrent()
     restore = install(fabric, D)
     tip, tix, tv = (torch.from_numpy(a).to(dev) for a in (indptr, indices, values))
     torch.cuda.synchronize()
@@ -142,13 +143,20 @@ def test_overlap_paths_under_concurrency(cfg, monkeypatch):
         assert ey <= 1e-4 and ed <= 1e-4, (step, ey, ed)
 
 
-@pytest.mark.parametrize("cfg", [CASES[0], CASES[1], CASES[2], CASES[8]],
-                         ids=["records", "allgather", "single", "rounds3"])
+_SINGLE2 = dict(world=2, k=16, overlap=False, halo="records", R=1, records=True, seed=52)
+
+
+@pytest.mark.parametrize("cfg", [CASES[0], CASES[1], _SINGLE2, CASES[7]],
+                         ids=["records", "allgather", "single", "rounds2"])
 def test_missing_wait_is_detected(cfg, monkeypatch):
     """Negative control: the same concurrent run with wait() a no-op must be wrong
-    at the second step (its consumers read the first step's exchange buffers)."""
+    at the second step (its consumers read the first step's exchange buffers).
+    World 2 (four streams); if HIP placed a rank's compute and side streams on one
+    hardware queue (in-order: correct, so nothing to detect) the case is skipped."""
     prob = _problem(cfg)
-    bad, _ = _run(cfg, prob, monkeypatch, fixed_us=3000.0, no_wait=True)
+    bad, fab = _run(cfg, prob, monkeypatch, fixed_us=3000.0, no_wait=True)
     torch.cuda.synchronize()
+    if not fab.concurrent:
+        pytest.skip("compute and side streams shared a hardware queue in this run")
     ey, ed = _errors(bad, prob, cfg["R"], 1)
     assert max(ey, ed) > 1e-3, (ey, ed)

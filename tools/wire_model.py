@@ -154,6 +154,27 @@ class ThreadFabric:
         self.waited = []     # every async handle issued (checked by the tests)
 
     # ------------------------------------------------------------- plumbing
+    def streams_concurrent(self, spin_ms: float = 20.0) -> bool:
+        """Whether every rank's compute stream really runs beside its side stream:
+        HIP maps streams onto a few hardware queues (GPU_MAX_HW_QUEUES), and two
+        streams on one queue run in order -- correct, but not concurrent.  A long
+        spin on the side stream and a tiny op on the compute stream: concurrent when
+        the tiny op completes well before the spin."""
+        import time
+        ok = True
+        for r in range(self.world):
+            with torch.cuda.stream(self.sides[r]):
+                spin_us(spin_ms * 1e3, self.device)
+            done = torch.cuda.Event()
+            with torch.cuda.stream(self.streams[r]):
+                torch.cuda._sleep(1)
+                done.record()
+            t0 = time.perf_counter()
+            done.synchronize()
+            ok = ok and (time.perf_counter() - t0) * 1e3 < spin_ms / 2
+            torch.cuda.synchronize(self.device)
+        return ok
+
     def bind(self, rank: int):
         self._tl.rank = rank
         torch.cuda.set_stream(self.streams[rank])
