@@ -159,4 +159,5 @@ def test_missing_wait_is_detected(cfg, monkeypatch):
     if not fab.concurrent:
         pytest.skip("compute and side streams shared a hardware queue in this run")
     ey, ed = _errors(bad, prob, cfg["R"], 1)
-    assert max(ey, ed) > 1e-3, (ey, ed)
+    # stale or never-written buffers: errors above tolerance, or NaN
+    assert not (ey <= 1e-3 and ed <= 1e-3), (ey, ed)
