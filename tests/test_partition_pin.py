@@ -3,7 +3,9 @@ BASELINE shapes and rank counts.
 
 BASELINE config 4 (ogbn-products-shaped, k = 32) at world 2, 4 and 8 and
 config 5 (ogbn-proteins-shaped, R = 8 relations) at world 8, every rank on
-cuda:0 (gloo stands in for RCCL: the exchange is staged through host memory).
+cuda:0 (world 2 / 4: gloo stands in for RCCL, the exchange staged through host
+memory; world 8: the ranks are threads of one process and tools/wire_model.py's
+ThreadFabric exchanges their tensors on side streams).
 The parent process generates the graph's CSR once (power-law indptr and
 columns take many synchronising passes, and N processes time-share the one
 card) and each rank maps only its rows' slice of it; edge values, features and
@@ -163,16 +165,84 @@ def _rel_err(a, b):
     return float(((a - b).abs() / b.abs().clamp_min(1)).max()) if b.numel() else 0.0
 
 
+def _thread_ranks(graph, world, R, rounds, graphdir):
+    """World 8 as threads of this process (tools/wire_model.ThreadFabric: every
+    collective a real exchange between the ranks' tensors, delivered on side
+    streams with RCCL's ordering): eight processes time-sharing the one card spent
+    minutes in context switches at every synchronising step, one process does not.
+    Returns per rank (r0, r1, y, dx, halo, bitwise, fwd_split, rounds)."""
+    import sys
+
+    import numpy as np
+    sys.path.insert(0, os.path.join(ROOT, "tools"))
+    import spgemm_new_amd.distributed as D
+    from spgemm_new_amd import _lib
+    from spgemm_new_amd.graphs import synthetic_features
+    from spgemm_new_amd.ops import topk_cbsr
+    from wire_model import ThreadFabric, install
+    dev = torch.device("cuda", 0)
+    indptr = torch.from_numpy(np.load(os.path.join(graphdir, "indptr.npy"))).to(dev)
+    cols_all = np.load(os.path.join(graphdir, "indices.npy"), mmap_mode="r")
+    b = D.row_partition(indptr, world)
+    fabric = ThreadFabric(world, dev, fixed_us=0.0, timeout_s=600.0)
+    restore = install(fabric, D)
+
+    def rank_fn(rank):
+        r0, r1 = b[rank], b[rank + 1]
+        e0, e1 = int(indptr[r0]), int(indptr[r1])
+        cols = torch.from_numpy(np.ascontiguousarray(cols_all[e0:e1])).to(dev)
+        vals = _values(R, e0, e1, dev)
+        data, sel = topk_cbsr(synthetic_features(SEED_X, r0, r1, H, dev), K)
+        G = _grad(R, r0, r1, dev)
+        kw = {"rounds": rounds} if R > 1 else {"bwd_algo": _lib.MAXK_BWD_TILE, "tile_splits": 1,
+                                               "rounds": rounds}
+        m = D.PartitionedMaxK(indptr, cols, vals, rank, world, dev, local_block=True, **kw)
+        if R == 1:
+            y = m.forward(data, sel, H)
+            dx = m.backward(G, sel)
+            m1 = D.PartitionedMaxK(indptr, cols, vals, rank, world, dev, local_block=True,
+                                   overlap=False, **kw)
+            y1 = m1.forward(data, sel, H)
+            dx1 = m1.backward(G, sel)
+            bitwise = bool(torch.equal(dx, dx1))
+            fwd_split = _rel_err(y, y1)
+        else:
+            y = m.forward_multi(data, sel, H)
+            dx = m.backward_multi(G, sel)
+            bitwise, fwd_split = True, 0.0
+        return r0, r1, y.cpu(), dx.cpu(), m.plan.num_halo, bitwise, fwd_split, m.rounds
+
+    try:
+        return fabric.run(rank_fn)
+    finally:
+        restore()
+
+
 @pytest.mark.gpu
 @pytest.mark.timeout(900)   # up to 8 spawned ranks time-share one card: minutes on a busy box
 @pytest.mark.parametrize("graph,world,R,rounds", [("products", 2, 1, 1), ("products", 4, 1, 1),
                                                   ("products", 8, 1, 1), ("proteins", 8, 8, 1),
-                                                  ("products", 2, 1, 2)])
+                                                  ("products", 2, 1, 2), ("products", 8, 1, 2)])
 def test_partitioned_rows_match_single_gpu(graph, world, R, rounds, tmp_path, tmp_path_factory):
-    """rounds = 1 pins the partition forms against one GPU (the default's two rounds
-    at products N = 8 would add per-round engines to 8 processes time-sharing one
-    card); rounds = 2 at N = 2 pins the round-pipelined exchange at full size."""
+    """World 2 / 4: one gloo process per rank; world 8: the ranks as threads of
+    this process exchanging through tools/wire_model.ThreadFabric.  rounds = 1 and
+    the round-pipelined exchange (rounds = 2: products N = 8's default)."""
     y_ref, dx_ref, graphdir = _reference(graph, R, str(tmp_path_factory.mktemp(graph)))
+    if world >= 8:
+        res = _thread_ranks(graph, world, R, rounds, graphdir)
+        assert all(r[7] == rounds for r in res)
+        assert all(r[5] for r in res), "overlapped backward differs bitwise from the single block"
+        assert max(r[6] for r in res) <= TOL
+        rows = 0
+        for r0, r1, y, dx, halo, _, _, _ in res:
+            rows += r1 - r0
+            assert halo > 0
+            yr = y_ref[r0:r1] if R == 1 else y_ref[:, r0:r1]
+            assert y.shape == yr.shape
+            assert _rel_err(y, yr) <= TOL, (r0, _rel_err(y, yr))
+            assert _rel_err(dx, dx_ref[r0:r1]) <= TOL, (r0, _rel_err(dx, dx_ref[r0:r1]))
+        assert rows == y_ref.shape[-2]
+        return
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
