@@ -342,6 +342,8 @@ def wire_table(graph="products", k=32, worlds=(4, 8), rates=(None, 0, 300, 500, 
             pm_kw[key] = bool(pm_kw[key])
     if isinstance(rounds, int):
         rounds = (rounds,)
+    elif isinstance(rounds, str):   # "auto" / "none": PartitionedMaxK's own choice
+        rounds = ("auto",)
     for world, R in [(w, r) for w in worlds for r in rounds]:
         bounds = D.row_partition(indptr, world)
         lb = Loopback(indptr, indices, bounds, 0, data, sel)
