@@ -884,3 +884,58 @@ def test_round_pipelined_exchange(world, halo_mode, k):
     ey, ed, mode = q.get(timeout=5)
     assert mode == halo_mode
     assert ey <= 1e-4 and ed <= 1e-4, (ey, ed)
+
+
+class _FakePlan:
+    """The fields of HaloPlan that _round_major reads and rewrites."""
+
+    def __init__(self, rng, world, num_own):
+        self.num_own = num_own
+        self.recv_counts = [int(x) for x in rng.integers(0, 40, size=world)]
+        self.send_counts = [int(x) for x in rng.integers(0, 40, size=world)]
+        self.num_halo = sum(self.recv_counts)
+        self.halo_global = torch.arange(self.num_halo, dtype=torch.int64) * 7 + 1000
+        n_send = sum(self.send_counts)
+        self.send_local = torch.from_numpy(rng.integers(0, num_own, size=n_send)).long()
+        cols = rng.integers(0, num_own + self.num_halo, size=500)
+        self.local_indices = torch.from_numpy(cols).to(torch.int32)
+
+
+@pytest.mark.parametrize("world,R", [(2, 2), (3, 3), (8, 2), (5, 4), (4, 1)])
+def test_round_major_renumbering(world, R):
+    """_round_major: round j carries the j-th equal-count slice
+    of every peer's rows, in peer order; the halo renumbering is a permutation that
+    keeps every edge on the same global node; the send list is the same multiset in
+    the round-major order; the round table tiles both sides exactly."""
+    from spgemm_new_amd.distributed import PartitionedMaxK
+    rng = np.random.default_rng(world * 10 + R)
+    p = _FakePlan(rng, world, num_own=60)
+    old_global, old_send = p.halo_global.clone(), p.send_local.clone()
+    old_li = p.local_indices.clone().long()
+    self = PartitionedMaxK.__new__(PartitionedMaxK)
+    self.world, self.device = world, torch.device("cpu")
+    tab = self._round_major(p, R)
+    assert len(tab) == R and tab[0][0] == 0 and tab[0][3] == 0
+    assert tab[-1][1] == p.num_halo and tab[-1][4] == sum(p.send_counts)
+    for j in range(1, R):
+        assert tab[j][0] == tab[j - 1][1] and tab[j][3] == tab[j - 1][4]
+    roff = np.concatenate([[0], np.cumsum(p.recv_counts)])
+    soff = np.concatenate([[0], np.cumsum(p.send_counts)])
+    pos_r = pos_s = 0
+    for j, (r0, r1, rc, s0, s1, sc) in enumerate(tab):
+        assert r1 - r0 == sum(rc) and s1 - s0 == sum(sc)
+        for q in range(world):
+            a, b = p.recv_counts[q] * j // R, p.recv_counts[q] * (j + 1) // R
+            assert rc[q] == b - a
+            assert torch.equal(p.halo_global[pos_r:pos_r + rc[q]], old_global[roff[q] + a:roff[q] + b])
+            pos_r += rc[q]
+            a, b = p.send_counts[q] * j // R, p.send_counts[q] * (j + 1) // R
+            assert sc[q] == b - a
+            assert torch.equal(p.send_local[pos_s:pos_s + sc[q]], old_send[soff[q] + a:soff[q] + b])
+            assert bool((self._send_peer[pos_s:pos_s + sc[q]] == q).all())
+            pos_s += sc[q]
+    # every edge still points at the same global node
+    li = p.local_indices.long()
+    own = li < p.num_own
+    assert torch.equal(li[own], old_li[own])
+    assert torch.equal(p.halo_global[li[~own] - p.num_own], old_global[old_li[~own] - p.num_own])
