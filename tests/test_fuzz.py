@@ -125,10 +125,12 @@ def test_fuzz_parity(dev, oracle, seed):
 def test_fuzz_parity_fast_paths(dev, oracle, seed):
     """The same random problems through the forms the sweep above leaves to
     AUTO: the forward that also writes the edge selectors and the two
-    backwards that read them (STAGED_EDGE, EDGE_GATHER), the column-blocked
+    backwards that read them (STAGED_EDGE, EDGE_GATHER; and APPEND on node and
+    edge selectors, round 6), the column-blocked
     forward (random block count), and TILE (k = 32 / 64, h = 256) with a
     random number of source ranges per destination group; and the fused
-    multi-relation forward with both fused multi-relation backwards (R = 4, 8, 16)."""
+    multi-relation forward with the fused multi-relation backwards (R = 4, 8, 16),
+    MULTI_APPEND included."""
     from spgemm_new_amd import ops
     rng, V, C, indptr, indices, values, k, h, pc, rc = draw(seed)
     if rng.random() < 0.5 and k not in (32, 64):
@@ -153,7 +155,8 @@ def test_fuzz_parity_fast_paths(dev, oracle, seed):
     assert oracle.parity_error(y.cpu().numpy(), ref) <= TOL, f"{ctx} esel forward"
     algos = [_lib.MAXK_BWD_STAGED_EDGE]
     if ops._edge_gather_ok(k):
-        algos.append(_lib.MAXK_BWD_EDGE_GATHER)
+        # round 6: the write-combined APPEND backward, both selector forms
+        algos += [_lib.MAXK_BWD_EDGE_GATHER, _lib.MAXK_BWD_APPEND, _lib.MAXK_BWD_APPEND_EDGE]
     for a in algos:
         dx = torch.full((C, k), float("nan"), device=dev)
         g.backward(G, sel, out=dx, algo=a)
@@ -183,7 +186,8 @@ def test_fuzz_parity_fast_paths(dev, oracle, seed):
             refq = oracle.np_forward(indptr, indices, vals[:, q], data_np, sel_np, h)
             assert oracle.parity_error(ym[q], refq) <= TOL, f"{ctx} R={R} q={q}"
             ref_m += oracle.np_backward(indptr, indices, vals[:, q], gm[q], sel_np)
-        for a in (_lib.MAXK_BWD_MULTI_STAGED, _lib.MAXK_BWD_MULTI_EDGE_GATHER):
+        for a in (_lib.MAXK_BWD_MULTI_STAGED, _lib.MAXK_BWD_MULTI_EDGE_GATHER,
+                  _lib.MAXK_BWD_MULTI_APPEND):
             dxm = torch.full((C, k), float("nan"), device=dev)
             g.backward_multi(T(gm, dev), sel, T(vals, dev), out=dxm, algo=a)
             assert oracle.parity_error(dxm.cpu().numpy(), ref_m) <= TOL, f"{ctx} R={R} algo={a}"
