@@ -22,6 +22,11 @@ This module gives them one, with RCCL's stream semantics:
 ``ThreadFabric``: all ranks of a world as threads of one process, each with its
 own current stream and side stream, every collective a real exchange between
 their tensors (correctness under concurrency: `tests/test_wire_overlap.py`).
+
+Limits: the ranks must call the collectives from their own threads, so torch
+autograd (whose backward runs on one engine thread per device) cannot drive a
+partitioned backward here -- the explicit forward / backward calls can; and the
+spin kernel is one wave, where RCCL's kernels hold several CUs.
 """
 from __future__ import annotations
 
