@@ -15,8 +15,10 @@
 //                   this is the library's HIP dense SpMM on the same input)
 //   maxk            forward SpGEMM (merge-path schedule, no pre-zeroing)
 //   maxk_backward   backward SSpMM, the fastest of the algorithms below
-//   maxk_backward_{atomic,staged,staged_edge,local,tile}   (staged_edge: the
-//                   edge selectors written by maxk_spgemm_forward_esel; tile: k in {32, 64}; its plan
+//   maxk_backward_{atomic,staged,staged_edge,append,append_edge,local,tile}
+//                   (staged_edge / append_edge: the edge selectors written by
+//                   maxk_spgemm_forward_esel; append: its plan from
+//                   maxk_append_plan_build; tile: k in {32, 64}; its plan
 //                   from maxk_tile_plan_build, as MaxKGraph.tile_plan builds it)
 // Each time is the mean of 4 runs after 4 warm-ups, each run followed by a
 // device synchronise (spmm_base.h:58-75).  --check compares the forward
@@ -324,8 +326,30 @@ void test_graph(const std::string &dir, const std::string &graph, int idx, int c
             std::printf("%s maxk_backward_staged_edge %g\n", out.c_str(), te);
             compare("staged_edge");
             best = std::min(best, te);
-            HIPCHECK(hipFree(esel));
             HIPCHECK(hipFree(ws));
+            // APPEND (non-deterministic like ATOMIC): plan for the schedule passed
+            // below, then node selectors and the edge selectors stored above
+            int nb = 0, bs = 0;
+            MAXKCHECK(maxk_append_bins(V, k, &nb, &bs));
+            int32_t *region_base = dev_alloc<int32_t>((size_t)nb * 8 + 1);
+            MAXKCHECK(maxk_append_plan_build(sched, P, indptr, indices, V, V, k, region_base, nb,
+                                             bs, st));
+            const size_t ab = maxk_backward_append_workspace_bytes(E, k, nb);
+            void *aws = dev_alloc<char>(ab);
+            for (int es = 0; es < 2; ++es) {
+                const double ta = time_ms([&] {
+                    MAXKCHECK(maxk_sspmm_backward_append(sched, P, indptr, indices, val, 1, dense,
+                                                         es ? esel : sel, es, V, V, E, kDimOrigin, k,
+                                                         region_base, nb, bs, dxs, aws, ab, st));
+                });
+                const char *name = es ? "append_edge" : "append";
+                std::printf("%s maxk_backward_%s %g\n", out.c_str(), name, ta);
+                compare(name);
+                best = std::min(best, ta);
+            }
+            HIPCHECK(hipFree(aws));
+            HIPCHECK(hipFree(region_base));
+            HIPCHECK(hipFree(esel));
         }
         if (64 % k == 0 && E > 0) {
             // the plan MaxKGraph.local_plan() builds: ~10 KB of LDS per wave, 16 waves per CU

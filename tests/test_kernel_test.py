@@ -21,7 +21,8 @@ def test_harness_built():
 @pytest.mark.gpu
 def test_harness_runs_and_validates(tmp_path):
     """main.cu's output lines for k = 16 / 32 / 64, every backward algorithm (TILE
-    at k = 32 / 64, its plan built by maxk_tile_plan_build),
+    at k = 32 / 64, its plan built by maxk_tile_plan_build; APPEND with node and
+    edge selectors, its plan built by maxk_append_plan_build),
     and the --check validations (forward vs dense SpMM, backward algorithms
     against each other) on two small graphs read from raw int32 files."""
     for name, seed in (("g1", 3), ("g2", 4)):
@@ -40,7 +41,7 @@ def test_harness_runs_and_validates(tmp_path):
         assert (g, 16, "dense_spmm") in times
         for k in (16, 32, 64):
             algos = ["maxk_backward_atomic", "maxk_backward_staged", "maxk_backward_staged_edge",
-                     "maxk_backward_local"]
+                     "maxk_backward_append", "maxk_backward_append_edge", "maxk_backward_local"]
             if k in (32, 64):
                 algos.append("maxk_backward_tile")   # the TILE plan through the C ABI
             fwds = ["maxk"] + (["maxk_blocked4"] if k >= 32 else [])   # column-blocked forward
@@ -48,10 +49,11 @@ def test_harness_runs_and_validates(tmp_path):
                 assert times[(g, k, kern)] > 0, (g, k, kern)
             assert times[(g, k, "maxk_backward")] == min(times[(g, k, a)] for a in algos)
     checks = [ln for ln in lines if "validation" in ln]
-    # per graph: k=16 fwd + staged + staged_edge + local; k=32 and k=64 also tile
-    # and the blocked forward
-    assert len(checks) == 2 * (4 + 6 + 6), checks
+    # per graph: k=16 fwd + staged + staged_edge + append + append_edge + local;
+    # k=32 and k=64 also tile and the blocked forward
+    assert len(checks) == 2 * (6 + 8 + 8), checks
     assert all("validation pass!" in ln for ln in checks), checks
     assert sum("backward tile vs atomic" in ln for ln in checks) == 4
     assert sum("forward blocked4 vs plain" in ln for ln in checks) == 4
+    assert sum("backward append_edge vs atomic" in ln for ln in checks) == 6
     assert np.isfinite(list(times.values())).all()
