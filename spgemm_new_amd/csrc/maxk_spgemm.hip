@@ -254,12 +254,45 @@ __device__ __forceinline__ uint32_t dpp_xor2(uint32_t v)
     return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x4E, 0xF, 0xF, false);
 }
 
-template <int K, int RS = 0, bool ESEL = false, bool NTD = true>
+// The edge stream one batch ahead (FWD_PF): pf holds the lane's (column, value)
+// of the batch that starts at e0 on entry and of the batch that starts at e1 --
+// the next row's first -- on return, loaded while this batch's gathers run, so
+// a row's first gathers do not wait for its edge loads.  pend bounds the loads
+// (the panel's last edge).  Used by the cacheable-gather (column-blocked) form
+// only: Reddit k=32 forward 2.38 -> 2.34 ms, while the products forms (short
+// rows, non-temporal or packed gathers) lost 1-4 % with it.
+#ifndef FWD_PF
+#define FWD_PF 1
+#endif
+template <int K, bool NTD>
+constexpr bool fwd_pf_on()
+{
+    return K > 0 && FWD_PF && !NTD;
+}
+struct FwdPf {
+    int c = 0;
+    float v = 0.f;
+};
+__device__ __forceinline__ void fwd_pf_load(FwdPf &pf, int b, int pend,
+                                            const int32_t *__restrict__ idx,
+                                            const float *__restrict__ val)
+{
+    const int e = b + lane_id();
+    pf.c = 0;
+    pf.v = 0.f;
+    if (e < pend) {
+        pf.c = __builtin_nontemporal_load(idx + e);
+        pf.v = __builtin_nontemporal_load(val + e);
+    }
+}
+
+template <int K, int RS = 0, bool ESEL = false, bool NTD = true, bool PF = false>
 __device__ __forceinline__ void fwd_edges_vec(int e0, int e1, const int32_t *__restrict__ idx,
                                               const float *__restrict__ val,
                                               const float *__restrict__ data,
                                               const uint8_t *__restrict__ sel, float *acc,
-                                              uint8_t *__restrict__ esel)
+                                              uint8_t *__restrict__ esel, FwdPf *pf = nullptr,
+                                              int pend = 0)
 {
     using Lay = FwdLayout<K>;
     constexpr int VEC = Lay::VEC, LPE = Lay::LPE, EPS = Lay::EPS;
@@ -278,7 +311,11 @@ __device__ __forceinline__ void fwd_edges_vec(int e0, int e1, const int32_t *__r
         const int n = (e1 - base) < kWave ? (e1 - base) : kWave;
         int my_c = 0;
         float my_v = 0.f;
-        if (lane < n) {
+        if constexpr (PF) {
+            my_c = pf->c;
+            my_v = pf->v;
+            fwd_pf_load(*pf, base + kWave < e1 ? base + kWave : e1, pend, idx, val);
+        } else if (lane < n) {
             my_c = __builtin_nontemporal_load(idx + base + lane);
             my_v = __builtin_nontemporal_load(val + base + lane);
         }
@@ -499,24 +536,51 @@ __global__ __launch_bounds__(kBlock) void fwd_panel_kernel(
     // this panel's owner slot, and carry_fixup_owner_kernel adds the parts up
     // in panel order (one writer per row, no atomics, bitwise deterministic)
     const bool split_first = i0 < i1 && j0 > indptr[i0];
-    for (int r = i0; r < i1; ++r) {
-        const int re = indptr[r + 1];
-        if (e < re) fwd_edges<K, RS, ESEL, NTD>(e, re, k, idx, val, data, sel, acc, esel);
-        if (r == i0 && split_first)
-            flush_row<kStore>(acc, copies, owner + (size_t)w * dimp, dim);
-        else if (!ACC && sump)
-            flush_row<kStore>(acc, copies, out + (size_t)r * dim, dim, sump + (size_t)r * dim, nsump,
-                              (size_t)num_rows * dim);
-        else
-            flush_row<ACC ? kAdd : kStore>(acc, copies, out + (size_t)r * dim, dim);
-        e = re;
-    }
     int has_carry = 0;
-    if (i1 < num_rows) {
-        const int eb = e > indptr[i1] ? e : indptr[i1];
-        if (eb < j1) {
-            fwd_edges<K, RS, ESEL, NTD>(eb, j1, k, idx, val, data, sel, acc, esel);
-            has_carry = 1;
+    if constexpr (fwd_pf_on<K, NTD>()) {
+        // the edge stream one batch ahead across rows (FwdPf); e == eb at the carry
+        FwdPf pf;
+        fwd_pf_load(pf, j0, j1, idx, val);
+        for (int r = i0; r < i1; ++r) {
+            const int re = indptr[r + 1];
+            if (e < re)
+                fwd_edges_vec<K, RS, ESEL, NTD, true>(e, re, idx, val, data, sel, acc, esel, &pf, j1);
+            if (r == i0 && split_first)
+                flush_row<kStore>(acc, copies, owner + (size_t)w * dimp, dim);
+            else if (!ACC && sump)
+                flush_row<kStore>(acc, copies, out + (size_t)r * dim, dim, sump + (size_t)r * dim,
+                                  nsump, (size_t)num_rows * dim);
+            else
+                flush_row<ACC ? kAdd : kStore>(acc, copies, out + (size_t)r * dim, dim);
+            e = re;
+        }
+        if (i1 < num_rows) {
+            const int eb = e > indptr[i1] ? e : indptr[i1];
+            if (eb < j1) {
+                if (eb != e) fwd_pf_load(pf, eb, j1, idx, val);
+                fwd_edges_vec<K, RS, ESEL, NTD, true>(eb, j1, idx, val, data, sel, acc, esel, &pf, j1);
+                has_carry = 1;
+            }
+        }
+    } else {
+        for (int r = i0; r < i1; ++r) {
+            const int re = indptr[r + 1];
+            if (e < re) fwd_edges<K, RS, ESEL, NTD>(e, re, k, idx, val, data, sel, acc, esel);
+            if (r == i0 && split_first)
+                flush_row<kStore>(acc, copies, owner + (size_t)w * dimp, dim);
+            else if (!ACC && sump)
+                flush_row<kStore>(acc, copies, out + (size_t)r * dim, dim, sump + (size_t)r * dim,
+                                  nsump, (size_t)num_rows * dim);
+            else
+                flush_row<ACC ? kAdd : kStore>(acc, copies, out + (size_t)r * dim, dim);
+            e = re;
+        }
+        if (i1 < num_rows) {
+            const int eb = e > indptr[i1] ? e : indptr[i1];
+            if (eb < j1) {
+                fwd_edges<K, RS, ESEL, NTD>(eb, j1, k, idx, val, data, sel, acc, esel);
+                has_carry = 1;
+            }
         }
     }
     if (has_carry) {
@@ -1291,14 +1355,51 @@ __device__ __forceinline__ int append_bin(int c, const AppendArgs &ap)
     return q;
 }
 
-template <int K, bool ESEL = false, int PM = kPmCsc>
+// The STAGED push's edge stream one batch ahead (BWD_PF, the forward's FwdPf
+// with the staging position): on entry the lane's (column, value, position) of
+// the batch that starts at e0, on return those of the batch that starts at e1;
+// the panel kernel also loads the next row's gradient row during this row's
+// gathers.  Used with node selectors at k <= 16 only (products k=16 STAGED
+// 6.45 -> 6.28 ms, k=8 6.23 -> 6.02): the edge-selector forms (STAGED_EDGE,
+// EDGE_GATHER phase 1) and k = 32 lost 2-4 % with it.
+#ifndef BWD_PF
+#define BWD_PF 1
+#endif
+template <int K, bool ESEL, int PM>
+constexpr bool bwd_pf_on()
+{
+    return BWD_PF && K > 0 && K <= 16 && !ESEL && PM == kPmCsc;
+}
+struct BwdPf {
+    int c = 0, p = 0;
+    float v = 0.f;
+};
+template <bool CSRP>
+__device__ __forceinline__ void bwd_pf_load(BwdPf &pf, int b, int pend,
+                                            const int32_t *__restrict__ idx,
+                                            const float *__restrict__ val,
+                                            const int32_t *__restrict__ csc_pos)
+{
+    const int e = b + lane_id();
+    pf.c = 0;
+    pf.p = 0;
+    pf.v = 0.f;
+    if (e < pend) {
+        pf.c = __builtin_nontemporal_load(idx + e);
+        pf.v = __builtin_nontemporal_load(val + e);
+        pf.p = CSRP ? e : __builtin_nontemporal_load(csc_pos + e);
+    }
+}
+
+template <int K, bool ESEL = false, int PM = kPmCsc, bool PF = false>
 __device__ __forceinline__ void bwd_edges_stage_vec(int e0, int e1,
                                                     const int32_t *__restrict__ idx,
                                                     const float *__restrict__ val,
                                                     const int32_t *__restrict__ csc_pos,
                                                     const uint8_t *__restrict__ sel,
                                                     const float *gs, float *__restrict__ P,
-                                                    const AppendArgs &ap = AppendArgs{})
+                                                    const AppendArgs &ap = AppendArgs{},
+                                                    BwdPf *pf = nullptr, int pend = 0)
 {
     constexpr bool CSRP = PM == kPmEdge || PM == kPmAppend;
     constexpr bool APP = PM == kPmAppend;
@@ -1314,7 +1415,12 @@ __device__ __forceinline__ void bwd_edges_stage_vec(int e0, int e1,
         const int n = (e1 - base) < kWave ? (e1 - base) : kWave;
         int my_c = 0, my_p = 0;
         float my_v = 0.f;
-        if (lane < n) {
+        if constexpr (PF) {
+            my_c = pf->c;
+            my_v = pf->v;
+            my_p = pf->p;
+            bwd_pf_load<CSRP>(*pf, base + kWave < e1 ? base + kWave : e1, pend, idx, val, csc_pos);
+        } else if (lane < n) {
             my_c = __builtin_nontemporal_load(idx + base + lane);
             my_v = __builtin_nontemporal_load(val + base + lane);
             my_p = CSRP ? base + lane : __builtin_nontemporal_load(csc_pos + base + lane);
@@ -1404,6 +1510,40 @@ __global__ __launch_bounds__(kBlock) void bwd_panel_kernel(
     const int2 a = sched[w], b = sched[w + 1];
     const int i0 = a.x, j0 = a.y, i1 = b.x, j1 = b.y;
     const int rlast = i1 < num_rows ? i1 : num_rows - 1;
+    if constexpr (STAGED && bwd_pf_on<K, ESEL, PM>()) {
+        if (dim == kMaxDim) {
+            // the next row's gradient row and edge batch loaded while this row's
+            // selector gathers run: one f4 of G per lane, one BwdPf per lane
+            constexpr bool CSRP = PM == kPmEdge || PM == kPmAppend;
+            const int lane = lane_id();
+            f4 gn = f4{0.f, 0.f, 0.f, 0.f};
+            int gn_row = -1;
+            BwdPf pf;
+            bool first = true;
+            for (int r = i0; r <= rlast; ++r) {
+                const int rb = indptr[r], re = indptr[r + 1];
+                const int eb = rb > j0 ? rb : j0;
+                const int ee = re < j1 ? re : j1;
+                if (eb >= ee) continue;
+                if (gn_row != r)
+                    gn = __builtin_nontemporal_load(reinterpret_cast<const f4 *>(grad + (size_t)r * dim) + lane);
+                if (first) {
+                    bwd_pf_load<CSRP>(pf, eb, j1, idx, val, csc_pos);
+                    first = false;
+                }
+                wave_sync_lds();
+                reinterpret_cast<f4 *>(gs)[lane] = gn;
+                wave_sync_lds();
+                if (r < rlast) {
+                    gn = __builtin_nontemporal_load(reinterpret_cast<const f4 *>(grad + (size_t)(r + 1) * dim) + lane);
+                    gn_row = r + 1;
+                }
+                bwd_edges_stage_vec<K, ESEL, PM, true>(eb, ee, idx, val, csc_pos, sel, gs, P,
+                                                       AppendArgs{}, &pf, j1);
+            }
+            return;
+        }
+    }
     for (int r = i0; r <= rlast; ++r) {
         const int rb = indptr[r], re = indptr[r + 1];
         const int eb = rb > j0 ? rb : j0;

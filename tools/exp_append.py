@@ -5,7 +5,7 @@ the edge selectors written when the backward reads them) and backward times,
 median of `reps` HIP-event-timed calls, and each result's max relative
 difference to STAGED.
 
-usage: tools/exp_append.py [products|reddit|proteins|all] [reps]"""
+usage: tools/exp_append.py [products|reddit|proteins|all|staged] [reps]"""
 import os
 import sys
 
@@ -71,8 +71,9 @@ def single(name, ks, algos, reps, dev):
             tf = med(lambda: g.forward(data, sel, h, out=y, edge_sel=es), reps)
             g.forward(data, sel, h, out=y, edge_sel=es)
             tb = med(lambda: g.backward(G, sel, out=dx, algo=a), reps)
+            bits = int(dx.view(torch.int32).to(torch.int64).sum())
             print(f"{name} k={k} {NAMES[a]:12s} fwd {tf:.3f} bwd {tb:.3f} step {tf + tb:.3f} ms"
-                  f"  | vs staged {rel(dx, ref):.1e}", flush=True)
+                  f"  | vs staged {rel(dx, ref):.1e} bits {bits}", flush=True)
         del data, sel, dx, ref
         g._ws.clear()
         g._esel.clear()
@@ -113,6 +114,9 @@ def main():
         single("products", (8, 16, 32, 64),
                (_lib.MAXK_BWD_STAGED, _lib.MAXK_BWD_STAGED_EDGE, _lib.MAXK_BWD_EDGE_GATHER,
                 _lib.MAXK_BWD_APPEND, _lib.MAXK_BWD_APPEND_EDGE, _lib.MAXK_BWD_TILE), reps, dev)
+    if what == "staged":   # the deterministic push forms only
+        single("products", (8, 16, 32),
+               (_lib.MAXK_BWD_STAGED, _lib.MAXK_BWD_STAGED_EDGE, _lib.MAXK_BWD_EDGE_GATHER), reps, dev)
     if what in ("reddit", "all"):
         single("reddit", (32,), (_lib.MAXK_BWD_TILE, _lib.MAXK_BWD_APPEND,
                                  _lib.MAXK_BWD_APPEND_EDGE), reps, dev)

@@ -37,4 +37,6 @@ ref = {}
 for k in [int(a) for a in sys.argv[1:]] or [8, 16]:
     data, sel = topk_cbsr(X, k)
     ms = med(lambda: g.forward(data, sel, 256, out=y))
-    print(f"{GRAPH} k={k} fwd {ms:.3f} ms  checksum {float(y.double().sum()):.6e}", flush=True)
+    bits = int(y.view(torch.int32).to(torch.int64).sum())   # equal sums <=> (almost surely) equal bits
+    print(f"{GRAPH} k={k} fwd {ms:.3f} ms  checksum {float(y.double().sum()):.6e} bits {bits}",
+          flush=True)
