@@ -21,7 +21,8 @@ ESEL = (_lib.MAXK_BWD_STAGED_EDGE, _lib.MAXK_BWD_EDGE_GATHER, _lib.MAXK_BWD_APPE
 NAMES = {_lib.MAXK_BWD_STAGED: "staged", _lib.MAXK_BWD_STAGED_EDGE: "staged_edge",
          _lib.MAXK_BWD_EDGE_GATHER: "edge_gather", _lib.MAXK_BWD_APPEND: "append",
          _lib.MAXK_BWD_APPEND_EDGE: "append_edge", _lib.MAXK_BWD_TILE: "tile",
-         _lib.MAXK_BWD_MULTI_STAGED: "multi_staged", _lib.MAXK_BWD_MULTI_APPEND: "multi_append"}
+         _lib.MAXK_BWD_MULTI_STAGED: "multi_staged", _lib.MAXK_BWD_MULTI_APPEND: "multi_append",
+         _lib.MAXK_BWD_MULTI_EDGE_GATHER: "multi_edge_gather"}
 
 
 def med(fn, reps):
@@ -95,10 +96,11 @@ def proteins(reps, dev):
     data, sel = S.topk_cbsr(X, k)
     dx = torch.empty((V, k), device=dev)
     ref = g.backward_multi(G, sel, vals, algo=_lib.MAXK_BWD_MULTI_STAGED).clone()
-    for a in (_lib.MAXK_BWD_MULTI_STAGED, _lib.MAXK_BWD_MULTI_APPEND):
+    for a in (_lib.MAXK_BWD_MULTI_STAGED, _lib.MAXK_BWD_MULTI_EDGE_GATHER, _lib.MAXK_BWD_MULTI_APPEND):
         tb = med(lambda: g.backward_multi(G, sel, vals, out=dx, algo=a), reps)
+        bits = int(dx.view(torch.int32).to(torch.int64).sum())
         print(f"proteins R=8 k=32 {NAMES[a]:12s} bwd {tb:.3f} ms | vs multi_staged "
-              f"{rel(dx, ref):.1e}", flush=True)
+              f"{rel(dx, ref):.1e} bits {bits}", flush=True)
 
 
 def main():
