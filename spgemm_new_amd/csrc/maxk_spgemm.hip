@@ -512,8 +512,18 @@ __device__ __forceinline__ void zero_lds(float *acc, int n)
 
 // Panel-scheduled forward.  Rows [i0, i1) are finished and owned by this
 // wave (plain store); row i1 is in progress at the panel end -> carry.
+// Occupancy target of the forward's register allocation: 5 waves per SIMD (the
+// LDS row copies allow 5 at k = 8 / 32 and 10 at k = 16) fits the packed k = 16
+// form without scratch (products k=16 forward 3.17 -> 3.11 ms); the other forms
+// keep the compiler's 4 (at k = 32 / 64, 5 spills: Reddit 2.34 -> 2.62 ms).
+template <int K, int RS, bool ESEL>
+constexpr int fwd_waves_per_eu()
+{
+    return K == 16 && RS > 0 && !ESEL ? 5 : 1;
+}
 template <int K, int RS = 0, bool ACC = false, bool ESEL = false, bool NTD = true>
-__global__ __launch_bounds__(kBlock) void fwd_panel_kernel(
+__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(fwd_waves_per_eu<K, RS, ESEL>())))
+void fwd_panel_kernel(
     const int2 *__restrict__ sched, int64_t num_panels, const int32_t *__restrict__ indptr,
     const int32_t *__restrict__ idx, const float *__restrict__ val,
     const float *__restrict__ data, const uint8_t *__restrict__ sel, int num_rows, int dim,
